@@ -1,0 +1,208 @@
+"""Datasets, host DataLoader and GPU-resident batch sources.
+
+Reference parity (Module_3/shard_dataset.py):
+  * ``ShardDataset``        <- :50-77  (concatenate shards, truncate to max_windows, dummy zero labels)
+  * ``make_dataloader``     <- :82-98
+  * ``load_shards_to_gpu``  <- :103-115
+  * ``make_gpu_batch_iter`` <- :118-136  (per-epoch device randperm, drop-last, infinite)
+
+MI355X-first additions:
+  * ``load_shards_to_gpu`` streams shards through page-locked staging buffers with async H2D on a
+    dedicated copy stream (double-buffered, event-fenced) instead of one pageable ``.to()``; with the
+    native IO library present it uses ``hipHostMalloc`` + ``hipMemcpyAsync`` from C++ (csrc/io).
+  * ``DeviceIndexSampler`` produces the same epoch/drop-last batch order as ``make_gpu_batch_iter`` but as
+    a static int32 index table ``[steps, B]`` on the device, which the fused HIP train step gathers from
+    directly (no per-step gather kernel, graph-capturable).
+  * ``labels="parity"`` gives a learnable synthetic label (sign of the window mean) for convergence tests.
+"""
+from __future__ import annotations
+
+from typing import Iterator, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+from torch.utils.data import DataLoader, Dataset
+
+from .shards import load_shard, shard_header
+
+
+def make_labels(x: np.ndarray, mode: str = "zeros") -> np.ndarray:
+    if mode == "zeros":
+        return np.zeros(x.shape[0], dtype=np.int64)
+    if mode == "parity":
+        return (x.mean(axis=1) > 0).astype(np.int64)
+    raise ValueError(f"unknown label mode {mode!r}")
+
+
+class ShardDataset(Dataset):
+    """Concatenates shards into one in-memory [N, L] dataset with dummy labels."""
+
+    def __init__(self, shard_paths: Sequence[str], max_windows: Optional[int] = None, labels: str = "zeros"):
+        xs = [load_shard(p) for p in shard_paths]
+        if not xs:
+            raise RuntimeError("No shards assigned to this rank.")
+        arr = np.concatenate(xs, axis=0).astype(np.float32, copy=False)
+        if max_windows is not None:
+            arr = arr[:max_windows]
+        arr = np.ascontiguousarray(arr)
+        self.x = torch.from_numpy(arr)
+        self.y = torch.from_numpy(make_labels(arr, labels))
+
+    def __len__(self) -> int:
+        return self.x.shape[0]
+
+    def __getitem__(self, idx):
+        return self.x[idx].unsqueeze(0), self.y[idx]
+
+
+def make_dataloader(shard_paths: Sequence[str], batch_size: int, max_windows: Optional[int] = None,
+                    num_workers: int = 2, pin_memory: bool = True, shuffle: bool = True,
+                    labels: str = "zeros") -> Tuple[DataLoader, int]:
+    ds = ShardDataset(shard_paths, max_windows=max_windows, labels=labels)
+    dl = DataLoader(ds, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers,
+                    pin_memory=pin_memory and torch.cuda.is_available(), drop_last=True,
+                    persistent_workers=num_workers > 0)
+    return dl, len(ds)
+
+
+def _count_windows(shard_paths: Sequence[str], max_windows: Optional[int]) -> Tuple[int, int]:
+    total, L = 0, None
+    for p in shard_paths:
+        n, l = shard_header(p)
+        if L is None:
+            L = l
+        elif l != L:
+            raise RuntimeError(f"shard {p} has L={l}, expected {L}")
+        total += n
+    if L is None:
+        raise RuntimeError("No shards assigned to this rank.")
+    if max_windows is not None:
+        total = min(total, max_windows)
+    return total, L
+
+
+def load_shards_to_gpu(shard_paths: Sequence[str], device, max_windows: Optional[int] = None,
+                       labels: str = "zeros", chunk_windows: int = 16384,
+                       use_native: Optional[bool] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Upload this rank's shards once: returns (x [N, L] float32, y [N] int64) on ``device``.
+
+    On a GPU the upload is chunked through pinned staging buffers on a side copy stream; the
+    returned tensors are valid on the current stream (it waits on the copy stream).
+    """
+    device = torch.device(device)
+    n_total, L = _count_windows(shard_paths, max_windows)
+    if device.type != "cuda":
+        ds = ShardDataset(shard_paths, max_windows=max_windows, labels=labels)
+        return ds.x.to(device), ds.y.to(device)
+
+    if use_native is None or use_native:
+        try:
+            from ..ops import native_io
+            if native_io.available():
+                x = native_io.upload_shards(shard_paths, device, n_total, L)
+                y = _labels_on_device(x, labels)
+                return x, y
+        except Exception:
+            if use_native:
+                raise
+
+    x = torch.empty((n_total, L), dtype=torch.float32, device=device)
+    copy_stream = torch.cuda.Stream(device=device)
+    staging = [torch.empty((chunk_windows, L), dtype=torch.float32).pin_memory() for _ in range(2)]
+    done = [None, None]
+    row = 0
+    slot = 0
+    for p in shard_paths:
+        if row >= n_total:
+            break
+        mm = load_shard(p, mmap=True)
+        i = 0
+        while i < mm.shape[0] and row < n_total:
+            take = min(chunk_windows, mm.shape[0] - i, n_total - row)
+            if done[slot] is not None:
+                done[slot].synchronize()  # staging slot free again
+            staging[slot][:take].numpy()[:] = mm[i:i + take]
+            with torch.cuda.stream(copy_stream):
+                x[row:row + take].copy_(staging[slot][:take], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(copy_stream)
+            done[slot] = ev
+            slot ^= 1
+            row += take
+            i += take
+    torch.cuda.current_stream(device).wait_stream(copy_stream)
+    x.record_stream(torch.cuda.current_stream(device))
+    for ev in done:
+        if ev is not None:
+            ev.synchronize()
+    y = _labels_on_device(x, labels)
+    return x, y
+
+
+def _labels_on_device(x: torch.Tensor, labels: str) -> torch.Tensor:
+    if labels == "zeros":
+        return torch.zeros(x.shape[0], dtype=torch.long, device=x.device)
+    if labels == "parity":
+        return (x.mean(dim=1) > 0).long()
+    raise ValueError(f"unknown label mode {labels!r}")
+
+
+def make_gpu_batch_iter(x_gpu: torch.Tensor, y_gpu: torch.Tensor, batch_size: int,
+                        generator: Optional[torch.Generator] = None) -> Iterator[Tuple[torch.Tensor, torch.Tensor]]:
+    """Infinite iterator of random mini-batches gathered on the device: ``([B,1,L], [B])``."""
+    N = x_gpu.size(0)
+    if N < batch_size:
+        raise RuntimeError(f"Not enough windows ({N}) for a batch of {batch_size}")
+    device = x_gpu.device
+    while True:
+        perm = torch.randperm(N, device=device, generator=generator)
+        for start in range(0, N - batch_size + 1, batch_size):
+            sel = perm[start:start + batch_size]
+            yield x_gpu[sel].unsqueeze(1), y_gpu[sel]
+
+
+class DeviceIndexSampler:
+    """Epoch-permutation batch indices as a static device table for the fused step.
+
+    Same semantics as ``make_gpu_batch_iter``: a fresh ``randperm(N)`` per epoch, consecutive
+    ``batch_size`` slices, trailing partial batch dropped.  ``fill(table)`` writes the next
+    ``table.shape[0]`` batches into ``table`` (int32 [S, B]) in place, so a captured graph that
+    reads ``table`` sees new batches every replay.
+    """
+
+    def __init__(self, n_windows: int, batch_size: int, device, seed: Optional[int] = None):
+        if n_windows < batch_size:
+            raise RuntimeError(f"Not enough windows ({n_windows}) for a batch of {batch_size}")
+        self.N = n_windows
+        self.B = batch_size
+        self.device = torch.device(device)
+        self.steps_per_epoch = n_windows // batch_size
+        self.gen = None
+        if seed is not None:
+            self.gen = torch.Generator(device=self.device)
+            self.gen.manual_seed(seed)
+        self._perm: Optional[torch.Tensor] = None
+        self._cursor = self.steps_per_epoch  # force a new epoch on first use
+
+    def _new_epoch(self):
+        p = torch.randperm(self.N, device=self.device, generator=self.gen)
+        self._perm = p[: self.steps_per_epoch * self.B].to(torch.int32).view(self.steps_per_epoch, self.B)
+        self._cursor = 0
+
+    def fill(self, table: torch.Tensor) -> torch.Tensor:
+        S = table.shape[0]
+        if table.dtype != torch.int32 or table.shape[1] != self.B:
+            raise ValueError(f"index table must be int32 [S, {self.B}], got {table.dtype} {tuple(table.shape)}")
+        s = 0
+        while s < S:
+            if self._cursor >= self.steps_per_epoch:
+                self._new_epoch()
+            take = min(S - s, self.steps_per_epoch - self._cursor)
+            table[s:s + take].copy_(self._perm[self._cursor:self._cursor + take], non_blocking=True)
+            s += take
+            self._cursor += take
+        return table
+
+    def next_batch(self) -> torch.Tensor:
+        t = torch.empty((1, self.B), dtype=torch.int32, device=self.device)
+        return self.fill(t)[0]

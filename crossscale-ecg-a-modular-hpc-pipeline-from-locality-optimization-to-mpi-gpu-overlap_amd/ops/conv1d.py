@@ -1,0 +1,98 @@
+"""Single-channel valid conv1d (the Module-2 op) on three backends.
+
+* ``hip``   - ``conv1d_batch_hip`` (csrc/kernels/conv1d_valid.hip), fp32 or bf16, async on the torch stream.
+* ``cpu``   - ``conv1d_batch_omp_simd`` (csrc/cpu/conv1d_cpu.cpp), the reference C ABI
+              (Module_2/conv1d_openmp_simd.c:21-28) with OpenMP + AVX2/AVX-512.
+* ``torch`` - ``F.conv1d`` (MIOpen on the GPU / oneDNN on the CPU) — the baseline the paper compares to
+              (Module_2/benchmark_part_2.py:75-82).
+
+``run_omp_conv(x_np, w_np, nthreads)`` keeps the reference helper's signature (benchmark_part_2.py:48-59).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+
+def _as_2d(x: torch.Tensor) -> torch.Tensor:
+    if x.dim() == 3:
+        if x.shape[1] != 1:
+            raise ValueError("conv1d_valid is single-channel: expected [B,1,L]")
+        x = x[:, 0, :]
+    if x.dim() != 2:
+        raise ValueError(f"expected [B, L] or [B, 1, L], got {tuple(x.shape)}")
+    return x.contiguous()
+
+
+def conv1d_valid(x: torch.Tensor, w: torch.Tensor, backend: str = "auto", out: torch.Tensor | None = None,
+                 nthreads: int | None = None) -> torch.Tensor:
+    """y[b, i] = sum_k x[b, i+k] w[k] for x [B, L] (or [B,1,L]), w [K] -> y [B, L-K+1] (same rank as x)."""
+    keep3 = x.dim() == 3
+    x2 = _as_2d(x)
+    w1 = w.reshape(-1).contiguous()
+    B, L = x2.shape
+    K = w1.numel()
+    if K < 1 or K > L:
+        raise ValueError(f"kernel size {K} incompatible with L={L}")
+    outL = L - K + 1
+    if backend == "auto":
+        backend = "hip" if x2.is_cuda else "cpu"
+    if backend == "torch":
+        y = F.conv1d(x2.unsqueeze(1), w1.to(x2.dtype).view(1, 1, K))
+        return y if keep3 else y[:, 0, :]
+    if backend == "hip":
+        if not x2.is_cuda:
+            raise ValueError("hip backend needs a CUDA tensor")
+        wf = w1.to(device=x2.device, dtype=torch.float32)
+        if out is None:
+            out = torch.empty((B, outL), dtype=x2.dtype, device=x2.device)
+        lib = _lib.kernels()
+        if x2.dtype == torch.float32:
+            st = lib.conv1d_batch_hip(x2.data_ptr(), wf.data_ptr(), out.data_ptr(), B, L, K,
+                                      _lib.stream_ptr(x2.device))
+        elif x2.dtype == torch.bfloat16:
+            st = lib.conv1d_batch_hip_bf16(x2.data_ptr(), wf.data_ptr(), out.data_ptr(), B, L, K,
+                                           _lib.stream_ptr(x2.device))
+        else:
+            raise ValueError(f"unsupported dtype {x2.dtype}")
+        _lib.check(st, "conv1d_batch_hip")
+        return out.unsqueeze(1) if keep3 else out
+    if backend == "cpu":
+        if x2.is_cuda or x2.dtype != torch.float32:
+            raise ValueError("cpu backend needs a CPU float32 tensor")
+        y = torch.from_numpy(run_omp_conv(x2.numpy(), w1.float().numpy(), nthreads))
+        return y.unsqueeze(1) if keep3 else y
+    raise ValueError(f"unknown backend {backend!r}")
+
+
+def run_omp_conv(x_np: np.ndarray, w_np: np.ndarray, nthreads: int | None = None,
+                 y_np: np.ndarray | None = None) -> np.ndarray:
+    """Native CPU kernel with the reference C ABI. x [B, L] float32, w [K] float32 -> y [B, L-K+1]."""
+    x_np = np.ascontiguousarray(x_np, dtype=np.float32)
+    w_np = np.ascontiguousarray(w_np, dtype=np.float32).reshape(-1)
+    batch, L = x_np.shape
+    K = w_np.shape[0]
+    if K < 1 or K > L:
+        raise ValueError(f"kernel size {K} incompatible with L={L}")
+    outL = L - K + 1
+    if y_np is None:
+        y_np = np.empty((batch, outL), dtype=np.float32)
+    elif y_np.shape != (batch, outL) or y_np.dtype != np.float32 or not y_np.flags.c_contiguous:
+        raise ValueError("bad output buffer")
+    fp = C.POINTER(C.c_float)
+    _lib.cpu_lib().conv1d_batch_omp_simd(x_np.ctypes.data_as(fp), w_np.ctypes.data_as(fp), y_np.ctypes.data_as(fp),
+                                        batch, L, K, int(nthreads or os.cpu_count() or 1))
+    return y_np
+
+
+def conv1d_valid_reference(x: np.ndarray, w: np.ndarray) -> np.ndarray:
+    """float64 numpy reference (np.correlate per row)."""
+    x = np.asarray(x, dtype=np.float64)
+    w = np.asarray(w, dtype=np.float64).reshape(-1)
+    return np.stack([np.correlate(r, w, mode="valid") for r in x])

@@ -1,0 +1,197 @@
+"""Fused TinyECG training / inference on gfx950 (Python side of csrc/kernels/tiny_ecg_step.hip).
+
+One HIP launch computes every sample's forward+backward out of LDS and writes per-sample parameter
+gradients into a slab; a second launch reduces the slab and applies SGD+momentum to the flat fp32
+master weights.  ``FusedTinyTrainer`` captures a whole FedAvg local round (``steps`` x 2 launches)
+into one native hipGraph and replays it with a single ``hipGraphLaunch``.
+
+Reference semantics per step: Module_3/TRUE_FL_M3/part3_fedavg_overlap_mpi_gpu.py:103-132
+(train_step_G0/G1), batches as Module_3/shard_dataset.py:118-136, optimizer SGD(lr=1e-2, momentum=0.9).
+Differences: bf16 MFMA operands with fp32 accumulation (AMP numerics without a GradScaler), the loss is
+accumulated on the device and read once per round (the reference syncs + ``loss.item()`` every step).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ..models.tiny_ecg import TinyECG, num_params
+from ..data.dataset import DeviceIndexSampler
+
+
+def slab_stride(num_classes: int) -> int:
+    return (num_params(num_classes) + 1 + 63) // 64 * 64
+
+
+def _check_dataset(x: torch.Tensor, y: Optional[torch.Tensor], num_classes: int):
+    if x.dim() != 2 or x.dtype != torch.float32 or not x.is_cuda or x.stride(1) != 1:
+        raise ValueError(f"dataset must be a CUDA float32 [N, L] tensor with unit stride, got "
+                         f"{x.dtype} {tuple(x.shape)} stride {x.stride()} on {x.device}")
+    if y is not None:
+        if y.dtype != torch.int32 or y.dim() != 1 or y.shape[0] != x.shape[0] or y.device != x.device:
+            raise ValueError("labels must be int32 [N] on the dataset's device")
+
+
+def _check_idx(idx: torch.Tensor, B: int, N: int, device):
+    if idx.dtype != torch.int32 or idx.numel() < B or idx.device != device or not idx.is_contiguous():
+        raise ValueError("idx must be a contiguous int32 device tensor with >= B entries")
+
+
+def labels_int32(y: torch.Tensor, num_classes: int) -> torch.Tensor:
+    y32 = y.to(torch.int32).contiguous()
+    if y32.numel():
+        lo, hi = int(y32.min()), int(y32.max())
+        if lo < 0 or hi >= num_classes:
+            raise ValueError(f"labels must be in [0, {num_classes}), got [{lo}, {hi}]")
+    return y32
+
+
+def tiny_forward(flat_params: torch.Tensor, x: torch.Tensor, idx: Optional[torch.Tensor], batch: int,
+                 num_classes: int = 2) -> torch.Tensor:
+    """Logits [batch, C] of TinyECG for windows ``x[idx[b]]`` (or ``x[b]`` when idx is None)."""
+    _check_dataset(x, None, num_classes)
+    if idx is not None:
+        _check_idx(idx, batch, x.shape[0], x.device)
+    elif batch > x.shape[0]:
+        raise ValueError("batch larger than dataset")
+    out = torch.empty((batch, num_classes), dtype=torch.float32, device=x.device)
+    lib = _lib.kernels()
+    st = lib.ecg_tiny_forward(x.data_ptr(), x.shape[1], x.stride(0), _lib.ptr(idx), flat_params.data_ptr(),
+                              num_classes, out.data_ptr(), batch, _lib.stream_ptr(x.device))
+    _lib.check(st, "ecg_tiny_forward")
+    return out
+
+
+def tiny_step_grads(flat_params: torch.Tensor, x: torch.Tensor, y32: torch.Tensor, idx: Optional[torch.Tensor],
+                    batch: int, num_classes: int = 2, slab: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-sample gradient slab [batch, stride] (loss in column P) of one fused step (no update)."""
+    _check_dataset(x, y32, num_classes)
+    if idx is not None:
+        _check_idx(idx, batch, x.shape[0], x.device)
+    stride = slab_stride(num_classes)
+    if slab is None:
+        slab = torch.empty((batch, stride), dtype=torch.float32, device=x.device)
+    lib = _lib.kernels()
+    st = lib.ecg_tiny_step_grads(x.data_ptr(), x.shape[1], x.stride(0), _lib.ptr(idx), y32.data_ptr(),
+                                 flat_params.data_ptr(), num_classes, slab.data_ptr(), stride, batch,
+                                 1.0 / batch, _lib.stream_ptr(x.device))
+    _lib.check(st, "ecg_tiny_step_grads")
+    return slab
+
+
+def reduce_slab(slab: torch.Tensor, num_classes: int = 2):
+    """Sum a gradient slab: returns (grad [P], loss_sum [1]) without applying an update."""
+    P = num_params(num_classes)
+    grad = torch.empty(P, dtype=torch.float32, device=slab.device)
+    loss = torch.zeros(1, dtype=torch.float32, device=slab.device)
+    lib = _lib.kernels()
+    st = lib.ecg_slab_reduce_sgd(slab.data_ptr(), slab.shape[0], slab.shape[1], P, None, None, grad.data_ptr(),
+                                 loss.data_ptr(), 0.0, 0.0, 0.0, 0, 0, _lib.stream_ptr(slab.device))
+    _lib.check(st, "ecg_slab_reduce_sgd")
+    return grad, loss
+
+
+class FusedTinyTrainer:
+    """Single-GPU local trainer for TinyECG on the fused HIP step (one FL client).
+
+    ``model`` is flattened in place: its parameters become views of ``self.params`` so that
+    ``state_dict()`` / FedAvg collectives operate on the very buffer the kernels update.
+    """
+
+    def __init__(self, model: TinyECG, x_gpu: torch.Tensor, y_gpu: torch.Tensor, batch_size: int,
+                 steps_per_round: int, lr: float = 1e-2, momentum: float = 0.9, weight_decay: float = 0.0,
+                 nesterov: bool = False, seed: Optional[int] = None, use_graph: bool = True):
+        self.device = x_gpu.device
+        self.model = model
+        self.nc = model.num_classes
+        self.params = model.flat if model.flat is not None else model.flatten_parameters()
+        if self.params.device != self.device:
+            raise ValueError("model and dataset must be on the same device")
+        self.P = num_params(self.nc)
+        self.x = x_gpu.contiguous()
+        self.y32 = labels_int32(y_gpu, self.nc)
+        _check_dataset(self.x, self.y32, self.nc)
+        self.B = int(batch_size)
+        self.S = int(steps_per_round)
+        self.lr, self.momentum, self.wd, self.nesterov = float(lr), float(momentum), float(weight_decay), bool(nesterov)
+        self.stride = slab_stride(self.nc)
+        self.mom = torch.zeros_like(self.params)
+        self.slab = torch.empty((self.B, self.stride), dtype=torch.float32, device=self.device)
+        self.loss_acc = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.idx_table = torch.zeros((self.S, self.B), dtype=torch.int32, device=self.device)
+        self.sampler = DeviceIndexSampler(self.x.shape[0], self.B, self.device, seed=seed)
+        self.use_graph = use_graph
+        self._graphs = {}  # n_steps -> native hipGraphExec handle
+        self.steps_done = 0
+        lib = _lib.kernels()
+        smem = lib.ecg_tiny_smem_bytes(self.x.shape[1])
+        if smem > 160 * 1024:
+            raise ValueError(f"window length {self.x.shape[1]} too long for the fused kernel ({smem} B LDS)")
+
+    # ------------------------------------------------------------------ graph management
+    def _graph_for(self, n: int) -> C.c_void_p:
+        g = self._graphs.get(n)
+        if g is not None:
+            return g
+        g = C.c_void_p()
+        lib = _lib.kernels()
+        torch.cuda.synchronize(self.device)
+        st = lib.ecg_round_graph_create(C.byref(g), self.x.data_ptr(), self.x.shape[1], self.x.stride(0),
+                                        self.idx_table.data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
+                                        self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
+                                        n, self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd,
+                                        int(self.nesterov))
+        _lib.check(st, "ecg_round_graph_create")
+        self._graphs[n] = g
+        return g
+
+    def close(self):
+        graphs, self._graphs = getattr(self, "_graphs", {}), {}
+        for g in graphs.values():
+            if g.value:
+                _lib.kernels().ecg_round_graph_destroy(g)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ execution
+    def _eager_step(self, s: int):
+        lib = _lib.kernels()
+        st = lib.ecg_tiny_train_step(self.x.data_ptr(), self.x.shape[1], self.x.stride(0),
+                                     self.idx_table[s].data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
+                                     self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
+                                     self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd, int(self.nesterov),
+                                     _lib.stream_ptr(self.device))
+        _lib.check(st, "ecg_tiny_train_step")
+
+    def run_round(self, n_steps: Optional[int] = None, reset_loss: bool = True) -> None:
+        """Enqueue ``n_steps`` (default ``steps_per_round``) local SGD steps on the current stream (async)."""
+        n = self.S if n_steps is None else int(n_steps)
+        if not 0 < n <= self.S:
+            raise ValueError(f"n_steps must be in [1, {self.S}]")
+        if reset_loss:
+            self.loss_acc.zero_()
+            self._loss_steps = 0
+        self.sampler.fill(self.idx_table[:n])
+        if self.use_graph:
+            g = self._graph_for(n)
+            _lib.check(_lib.kernels().ecg_round_graph_launch(g, _lib.stream_ptr(self.device)),
+                       "ecg_round_graph_launch")
+        else:
+            for s in range(n):
+                self._eager_step(s)
+        self.steps_done += n
+        self._loss_steps = getattr(self, "_loss_steps", 0) + n
+
+    def avg_loss(self) -> float:
+        """Mean per-step loss since the last reset (synchronises)."""
+        return float(self.loss_acc.item()) / (self.B * max(1, getattr(self, "_loss_steps", self.S)))
+
+    def reset_momentum(self):
+        self.mom.zero_()

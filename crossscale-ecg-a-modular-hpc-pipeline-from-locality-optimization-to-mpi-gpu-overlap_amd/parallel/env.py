@@ -1,0 +1,123 @@
+"""Process-group bring-up: torchrun env, MPI/Slurm launcher shim, one GPU per local rank.
+
+Reference: ``comm = MPI.COMM_WORLD`` + ``setup_device() -> cuda:0`` (Module_3/part3_mpi_gpu_train.py:82-86,
+433-437; TRUE_FL_M3/part3_fedavg_overlap_mpi_gpu.py:60-65), one rank per node via ``srun``
+(run_part3_sweep.sh:38-42).  MI355X design: one process per GPU on an 8-GPU node, ``torch.distributed``
+backend ``"nccl"`` (== RCCL on ROCm, xGMI peer links), ``gloo`` on CPU.  ``mpiexec``/``srun`` keep
+working: OMPI_COMM_WORLD_* / PMI_* / SLURM_* variables are mapped onto RANK/WORLD_SIZE/LOCAL_RANK, so
+mpi4py is never needed.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+_MPI_MAP = [
+    # (rank, world, local_rank)
+    ("OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_RANK"),
+    ("PMI_RANK", "PMI_SIZE", "MPI_LOCALRANKID"),
+    ("PMIX_RANK", "PMIX_SIZE", "PMIX_LOCAL_RANK"),
+    ("SLURM_PROCID", "SLURM_NTASKS", "SLURM_LOCALID"),
+]
+
+
+def apply_launcher_env_shim(env: Optional[dict] = None) -> Optional[str]:
+    """If RANK/WORLD_SIZE are absent but an MPI/Slurm launcher set its own, translate them.
+
+    Returns the name of the launcher family that was mapped (or None)."""
+    env = os.environ if env is None else env
+    if "RANK" in env and "WORLD_SIZE" in env:
+        return None
+    for rk, ws, lr in _MPI_MAP:
+        if rk in env and ws in env:
+            env["RANK"] = env[rk]
+            env["WORLD_SIZE"] = env[ws]
+            env["LOCAL_RANK"] = env.get(lr, "0")
+            env.setdefault("MASTER_ADDR", env.get("SLURM_LAUNCH_NODE_IPADDR", "127.0.0.1"))
+            env.setdefault("MASTER_PORT", "29511")
+            return rk.split("_")[0]
+    return None
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+    initialized_here: bool = False
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1 and dist.is_available() and dist.is_initialized()
+
+
+_CTX: Optional[DistContext] = None
+
+
+def setup_device(local_rank: int = 0, prefer_gpu: bool = True) -> torch.device:
+    """``cuda:{local_rank}`` when a GPU is present (reference always used cuda:0, one GPU per node)."""
+    if prefer_gpu and torch.cuda.is_available():
+        n = torch.cuda.device_count()
+        dev = torch.device("cuda", local_rank % max(1, n))
+        torch.cuda.set_device(dev)
+        return dev
+    return torch.device("cpu")
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, prefer_gpu: bool = True) -> DistContext:
+    """Initialise (idempotently) the default process group from env; single process works without env."""
+    global _CTX
+    if _CTX is not None:
+        return _CTX
+    apply_launcher_env_shim()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    device = setup_device(local_rank, prefer_gpu)
+    if backend is None:
+        backend = "nccl" if device.type == "cuda" else "gloo"
+    ctx = DistContext(rank, world, local_rank, backend if world > 1 else "none", device)
+    if world > 1 and dist.is_available() and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+        ctx.initialized_here = True
+    elif world > 1 and dist.is_initialized():
+        ctx.backend = dist.get_backend()
+    _CTX = ctx
+    return ctx
+
+
+def get_context() -> DistContext:
+    return _CTX if _CTX is not None else init_distributed()
+
+
+def shutdown_distributed() -> None:
+    global _CTX
+    if _CTX is not None and _CTX.initialized_here and dist.is_initialized():
+        dist.destroy_process_group()
+    _CTX = None
+
+
+def barrier(ctx: Optional[DistContext] = None) -> None:
+    ctx = ctx or get_context()
+    if ctx.distributed:
+        if ctx.backend == "nccl":
+            dist.barrier(device_ids=[ctx.device.index])
+        else:
+            dist.barrier()

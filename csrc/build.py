@@ -1,0 +1,141 @@
+#!/usr/bin/env python3
+"""Build the native libraries in-tree (gfx950 only).
+
+Outputs (git-ignored, shipped to the GPU box with the repo snapshot) in ``<package>/_lib/``:
+
+* ``libecg_kernels.so`` - every HIP kernel in ``csrc/kernels/*.hip`` (hipcc --offload-arch=gfx950),
+  exposed through a C ABI that the Python layer binds with ctypes (launchers take a hipStream_t).
+* ``libecg_io.so``      - C++ mmap shard reader, pinned-ring prefetcher, bulk uploader (HIP runtime).
+* ``libconv1d_cpu.so``  - OpenMP + AVX2/AVX-512 CPU conv1d exporting ``conv1d_batch_omp_simd``.
+
+Incremental: a target is rebuilt only when the hash of its sources, headers and flags changed.
+Usage: ``python csrc/build.py [--force] [-j N] [--debug-asan-host]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+from typing import List
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+PKG_NAME = "crossscale-ecg-a-modular-hpc-pipeline-from-locality-optimization-to-mpi-gpu-overlap_amd"
+LIBDIR = os.path.join(ROOT, PKG_NAME, "_lib")
+OBJDIR = os.path.join(ROOT, "build", "obj")
+ARCH = os.environ.get("ECG_OFFLOAD_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
+def hipcc() -> str:
+    p = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+    if not os.path.exists(p):
+        raise RuntimeError("hipcc not found; the native build needs ROCm")
+    return p
+
+
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-pthread"]
+
+
+def _digest(paths: List[str], extra: List[str]) -> str:
+    h = hashlib.sha256()
+    for p in sorted(paths):
+        with open(p, "rb") as f:
+            h.update(p.encode())
+            h.update(f.read())
+    h.update(" ".join(extra).encode())
+    return h.hexdigest()
+
+
+def _up_to_date(target: str, digest: str) -> bool:
+    stamp = target + ".sha256"
+    return os.path.exists(target) and os.path.exists(stamp) and open(stamp).read().strip() == digest
+
+
+def _stamp(target: str, digest: str) -> None:
+    with open(target + ".sha256", "w") as f:
+        f.write(digest)
+
+
+def _run(cmd: List[str]) -> None:
+    r = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}")
+
+
+def build_kernels(force: bool, jobs: int, extra: List[str]) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "include", "*.h")))
+    target = os.path.join(LIBDIR, "libecg_kernels.so")
+    dig = _digest(srcs + hdrs, HIP_FLAGS + extra)
+    if not force and _up_to_date(target, dig):
+        return target
+    os.makedirs(OBJDIR, exist_ok=True)
+    objs = [os.path.join(OBJDIR, os.path.basename(s) + ".o") for s in srcs]
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        futs = [ex.submit(_run, [hipcc(), *HIP_FLAGS, *extra, "-I", os.path.join(CSRC, "include"), "-c", s, "-o", o])
+                for s, o in zip(srcs, objs)]
+        for f in futs:
+            f.result()
+    os.makedirs(LIBDIR, exist_ok=True)
+    _run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", target])
+    _stamp(target, dig)
+    return target
+
+
+def build_io(force: bool, extra: List[str]) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "io", "*.cpp")))
+    target = os.path.join(LIBDIR, "libecg_io.so")
+    flags = CXX_FLAGS + ["-D__HIP_PLATFORM_AMD__", "-I", os.path.join(ROCM, "include")]
+    dig = _digest(srcs, flags + extra)
+    if not force and _up_to_date(target, dig):
+        return target
+    os.makedirs(LIBDIR, exist_ok=True)
+    # host-only C++ against the HIP runtime API (no device code) - plain g++ keeps the build fast
+    _run(["g++", *flags, *extra, "-shared", *srcs, "-o", target, f"-L{ROCM}/lib", "-lamdhip64",
+          f"-Wl,-rpath,{ROCM}/lib"])
+    _stamp(target, dig)
+    return target
+
+
+def build_cpu(force: bool, extra: List[str]) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "cpu", "*.cpp")))
+    target = os.path.join(LIBDIR, "libconv1d_cpu.so")
+    flags = CXX_FLAGS + ["-fopenmp", "-mfma"]
+    dig = _digest(srcs, flags + extra)
+    if not force and _up_to_date(target, dig):
+        return target
+    os.makedirs(LIBDIR, exist_ok=True)
+    _run(["g++", *flags, *extra, "-shared", *srcs, "-o", target])
+    _stamp(target, dig)
+    return target
+
+
+def build_all(force: bool = False, jobs: int = 8, host_asan: bool = False, verbose: bool = True) -> List[str]:
+    extra_host = ["-fsanitize=address", "-fno-omit-frame-pointer"] if host_asan else []
+    outs = [build_kernels(force, jobs, []), build_io(force, extra_host), build_cpu(force, extra_host)]
+    if verbose:
+        for o in outs:
+            print(f"[build] {os.path.relpath(o, ROOT)}")
+    return outs
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("--debug-asan-host", action="store_true", help="host-only ASan for the C++ IO/CPU libs")
+    a = ap.parse_args(argv)
+    build_all(a.force, a.jobs, a.debug_asan_host)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,128 @@
+"""Numerics of the fused TinyECG HIP step vs a plain PyTorch fp32 reference of the same computation."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import crossscale_ecg  # noqa: F401
+from crossscale_ecg.models.tiny_ecg import TinyECG, num_params
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(B=64, L=500, N=300, nc=2, seed=0, labels="random"):
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(N, L, generator=g).to(dev)
+    if labels == "random":
+        y = torch.randint(0, nc, (N,), generator=g).to(dev)
+    else:
+        y = torch.zeros(N, dtype=torch.long, device=dev)
+    torch.manual_seed(seed)
+    model = TinyECG(num_classes=nc).to(dev)
+    idx = torch.randperm(N, generator=g)[:B].to(torch.int32).to(dev)
+    return dev, x, y, model, idx
+
+
+def _ref_grads(model, x, y, idx):
+    m = TinyECG(num_classes=model.num_classes).to(x.device)
+    m.load_state_dict(model.state_dict())
+    sel = idx.long()
+    loss = F.cross_entropy(m(x[sel].unsqueeze(1)), y[sel])
+    loss.backward()
+    g = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+    return g, loss.detach()
+
+
+@pytest.mark.parametrize("L", [500, 64, 333, 1000])
+def test_forward_matches_torch(L):
+    from crossscale_ecg.ops.fused_tiny import tiny_forward
+    dev, x, y, model, idx = _setup(L=L)
+    flat = model.flatten_parameters()
+    out = tiny_forward(flat, x, idx, idx.numel(), 2)
+    ref = model(x[idx.long()].unsqueeze(1))
+    torch.cuda.synchronize()
+    err = (out - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-3
+    assert err / scale < 2e-2, f"max err {err} (scale {scale})"
+
+
+@pytest.mark.parametrize("nc,L", [(2, 500), (5, 500), (2, 130)])
+def test_step_grads_match_autograd(nc, L):
+    from crossscale_ecg.ops.fused_tiny import tiny_step_grads, reduce_slab, labels_int32
+    dev, x, y, model, idx = _setup(nc=nc, L=L)
+    gref, lref = _ref_grads(model, x, y, idx)
+    flat = model.flatten_parameters()
+    slab = tiny_step_grads(flat, x, labels_int32(y, nc), idx, idx.numel(), nc)
+    grad, loss = reduce_slab(slab, nc)
+    torch.cuda.synchronize()
+    P = num_params(nc)
+    assert grad.numel() == P
+    assert abs(loss.item() / idx.numel() - lref.item()) < 1e-2 * max(1.0, abs(lref.item()))
+    # per-tensor relative error (bf16 operands, fp32 accumulation)
+    off = 0
+    for name, p in model.named_parameters():
+        n = p.numel()
+        a, b = grad[off:off + n], gref[off:off + n]
+        rel = (a - b).norm().item() / (b.norm().item() + 1e-6)
+        assert rel < 3e-2, f"{name}: rel err {rel:.4f} |ref|={b.norm().item():.3e}"
+        off += n
+
+
+def test_train_step_and_graph_match_torch_sgd():
+    from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
+    dev, x, y, model, idx = _setup(B=128, N=1024)
+    ref = TinyECG().to(dev)
+    ref.load_state_dict(model.state_dict())
+    opt = torch.optim.SGD(ref.parameters(), lr=1e-2, momentum=0.9)
+    tr = FusedTinyTrainer(model, x, y, batch_size=128, steps_per_round=4, seed=123)
+    tr.run_round()  # graph path
+    torch.cuda.synchronize()
+    # replay the same batches through torch
+    tab = tr.idx_table.clone()
+    for s in range(4):
+        sel = tab[s].long()
+        opt.zero_grad()
+        F.cross_entropy(ref(x[sel].unsqueeze(1)), y[sel]).backward()
+        opt.step()
+    got = tr.params[: num_params(2)]
+    want = torch.cat([p.detach().reshape(-1) for p in ref.parameters()])
+    rel = (got - want).norm().item() / want.norm().item()
+    assert rel < 1e-3, rel
+    # state_dict views the flat buffer
+    sd = model.state_dict()
+    assert torch.equal(sd["net.2.weight"].reshape(-1), tr.params[128:1408])
+    tr.close()
+
+
+def test_graph_equals_eager():
+    from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
+    dev, x, y, model, _ = _setup(B=64, N=640)
+    m2 = TinyECG().to(dev)
+    m2.load_state_dict(model.state_dict())
+    a = FusedTinyTrainer(model, x, y, 64, 5, seed=7, use_graph=True)
+    b = FusedTinyTrainer(m2, x, y, 64, 5, seed=7, use_graph=False)
+    for _ in range(3):
+        a.run_round()
+        b.run_round()
+    torch.cuda.synchronize()
+    assert torch.allclose(a.params, b.params, rtol=1e-5, atol=1e-6)
+    assert abs(a.avg_loss() - b.avg_loss()) < 1e-4
+    a.close()
+    b.close()
+
+
+def test_training_reduces_loss_on_learnable_labels():
+    from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    x = torch.randn(4096, 500, device=dev) + torch.randn(4096, 1, device=dev) * 0.5
+    y = (x.mean(1) > 0).long()
+    model = TinyECG().to(dev)
+    tr = FusedTinyTrainer(model, x, y, 256, 50, lr=5e-2, seed=0)
+    tr.run_round()
+    first = tr.avg_loss()
+    for _ in range(6):
+        tr.run_round()
+    last = tr.avg_loss()
+    assert last < first * 0.9, (first, last)
+    tr.close()

@@ -1,0 +1,109 @@
+"""HIP op numerics vs plain PyTorch fp32 references (Module-2 conv1d, flat SGD, gather/normalize)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import crossscale_ecg  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.mark.parametrize("B", [64, 128, 256, 512])
+@pytest.mark.parametrize("K", [3, 5, 7, 4, 32])
+def test_conv1d_valid_fp32(B, K):
+    from crossscale_ecg.ops.conv1d import conv1d_valid
+    x = torch.randn(B, 500, device=DEV)
+    w = torch.randn(K, device=DEV)
+    y = conv1d_valid(x, w, backend="hip")
+    ref = F.conv1d(x.unsqueeze(1).double(), w.double().view(1, 1, K))[:, 0].float()
+    torch.cuda.synchronize()
+    assert y.shape == (B, 500 - K + 1)
+    assert torch.allclose(y, ref, atol=1e-5, rtol=1e-5), (y - ref).abs().max().item()
+
+
+def test_conv1d_valid_bf16_and_3d_and_odd_alignment():
+    from crossscale_ecg.ops.conv1d import conv1d_valid
+    x = torch.randn(100, 1, 333, device=DEV)
+    w = torch.randn(7, device=DEV)
+    y = conv1d_valid(x, w, backend="hip")
+    assert y.shape == (100, 1, 327)
+    ref = F.conv1d(x, w.view(1, 1, 7))
+    assert torch.allclose(y, ref, atol=1e-5, rtol=1e-5)
+    xb = x[:, 0].bfloat16()
+    yb = conv1d_valid(xb, w, backend="hip")
+    refb = F.conv1d(xb.float().unsqueeze(1), w.view(1, 1, 7))[:, 0]
+    assert (yb.float() - refb).abs().max().item() < 2e-2 * refb.abs().max().item()
+
+
+@pytest.mark.parametrize("momentum,dampening,wd,nesterov", [(0.9, 0.0, 0.0, False), (0.0, 0.0, 1e-4, False),
+                                                             (0.9, 0.1, 1e-3, False), (0.9, 0.0, 0.0, True)])
+def test_flat_sgd_matches_torch(momentum, dampening, wd, nesterov):
+    from crossscale_ecg.ops.sgd import FlatSGD
+    n = 1459
+    p0 = torch.randn(n + 5, device=DEV)[:n].clone()
+    p = torch.zeros(1472, device=DEV)
+    p[:n] = p0
+    g = torch.zeros_like(p)
+    opt = FlatSGD(p, g, lr=0.05, momentum=momentum, dampening=dampening, weight_decay=wd, nesterov=nesterov)
+    q = torch.nn.Parameter(p0.clone())
+    ref = torch.optim.SGD([q], lr=0.05, momentum=momentum, dampening=dampening, weight_decay=wd, nesterov=nesterov)
+    for _ in range(4):
+        gg = torch.randn(n, device=DEV)
+        g[:n] = gg
+        opt.step()
+        q.grad = gg.clone()
+        ref.step()
+    torch.cuda.synchronize()
+    assert torch.allclose(p[:n], q.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_flat_sgd_found_inf_skips():
+    from crossscale_ecg.ops.sgd import FlatSGD
+    p = torch.ones(64, device=DEV)
+    g = torch.ones(64, device=DEV)
+    g[3] = float("inf")
+    fi = torch.zeros(1, dtype=torch.int32, device=DEV)
+    FlatSGD(p, g, lr=0.1, momentum=0.9).step(inv_scale=0.5, found_inf=fi)
+    torch.cuda.synchronize()
+    assert fi.item() == 1 and torch.all(p == 1)
+
+
+@pytest.mark.parametrize("normalize", [False, True])
+def test_gather_rows(normalize):
+    from crossscale_ecg.ops.gather import gather_rows
+    x = torch.randn(1000, 500, device=DEV) * 3 + 1
+    idx = torch.randperm(1000, device=DEV)[:256].int()
+    out = gather_rows(x, idx, normalize=normalize)
+    ref = x[idx.long()].double()
+    if normalize:
+        ref = (ref - ref.mean(1, keepdim=True)) / (ref.std(1, unbiased=False, keepdim=True) + 1e-8)
+    torch.cuda.synchronize()
+    assert torch.allclose(out.double(), ref, atol=1e-5, rtol=1e-5)
+    outb = gather_rows(x, idx, normalize=normalize, dtype=torch.bfloat16)
+    assert torch.allclose(outb.double(), ref, atol=3e-2 * max(1, ref.abs().max().item()), rtol=1e-2)
+
+
+def test_native_upload_and_prefetch(tmp_path):
+    from crossscale_ecg.data.shards import write_shards
+    from crossscale_ecg.ops import native_io
+    data = np.random.default_rng(0).normal(size=(1000, 500)).astype(np.float32)
+    paths = write_shards(data, str(tmp_path), shard_size=300)
+    x = native_io.upload_shards(paths, DEV, 900, 500, chunk_rows=128)
+    assert torch.equal(x.cpu(), torch.from_numpy(data[:900]))
+    pf = native_io.NativePrefetcher(paths, batch_size=128, num_slots=3, normalize=False, pinned=True)
+    pf.start()
+    dst = torch.empty(128, 500, device=DEV)
+    got = []
+    while True:
+        r = pf.next_batch_cpu()
+        if r is None:
+            break
+        slot, view, _ms = r
+        n = view.shape[0]
+        pf.h2d(slot, n, dst)
+        got.append(dst[:n].clone())
+    pf.close()
+    allx = torch.cat(got).cpu()
+    assert torch.equal(allx, torch.from_numpy(data))
