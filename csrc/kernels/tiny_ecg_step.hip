@@ -16,6 +16,8 @@
 // Precision: bf16 MFMA operands, fp32 accumulation, fp32 master weights/optimizer state (native bf16 AMP).
 #include "../include/ecg_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int C = 16;   // hidden channels
@@ -42,29 +44,33 @@ __host__ __device__ inline Layout make_layout(int nc) {
 
 // LDS carve (bytes), all offsets multiples of 16.
 struct Smem {
-  int Lp;         // L rounded up to 32 (tile pairs)
-  int xs_off, h1_off, dh2_off, red_off, bytes;
+  int Lp;  // L rounded up to 32 (tile pairs)
+  int xs_off, h1_off, dh2_off, ps_off, frag_off, red_off, bytes;
 };
 
-// red region (floats)
-constexpr int RED_DW2 = 0;                  // [16][16][5] = 1280 (param layout co*80+ci*5+k)
-constexpr int RED_DW1 = RED_DW2 + 1280;     // [16][8]: k<7 weight grad, k==7 bias grad
-constexpr int RED_DB2 = RED_DW1 + 128;      // [16]
-constexpr int RED_G = RED_DB2 + 16;         // [16] dL/dh2 scale per channel (dpooled / L)
-constexpr int RED_POOL = RED_G + 16;        // [WAVES][16] pooled partials
-constexpr int RED_FLOATS_FIXED = RED_POOL;
+// red region (floats): per-wave partials are written with plain stores and summed after a barrier
+// (deterministic; no LDS float atomics).
+constexpr int RED_G = 0;                            // [16] dL/dh2 scale per channel (dpooled / L)
+constexpr int RED_POOLED = 16;                      // [16] pooled features
+constexpr int RED_POOL = 32;                        // [WAVES][16] pooled partials
+__host__ __device__ constexpr int red_dw2(int waves) { return RED_POOL + waves * 16; }       // [WAVES][1280]
+__host__ __device__ constexpr int red_dw1(int waves) { return red_dw2(waves) + waves * 1280; }  // [WAVES][16][8]
+__host__ __device__ constexpr int red_db2(int waves) { return red_dw1(waves) + waves * 128; }   // [WAVES][16]
+__host__ __device__ constexpr int red_floats(int waves) { return red_db2(waves) + waves * 16; }
 
-__host__ __device__ inline Smem make_smem(int L, int waves) {
+__host__ __device__ inline Smem make_smem(int L, int waves, int nc = MAX_CLASSES) {
   Smem s;
   s.Lp = (L + 31) / 32 * 32;
   s.xs_off = 0;
-  int xs_bytes = ((s.Lp + 16) * 4 + 15) / 16 * 16;
+  const int xs_bytes = ((s.Lp + 16) * 4 + 15) / 16 * 16;
   s.h1_off = s.xs_off + xs_bytes;
-  int act_bytes = (s.Lp + 8) * C * 2;  // bf16 [Lp+8][16]
+  const int act_bytes = (s.Lp + 8) * C * 2;  // bf16 [Lp+8][16]
   s.dh2_off = s.h1_off + act_bytes;
-  s.red_off = s.dh2_off + act_bytes;
-  int red_bytes = ((RED_FLOATS_FIXED + waves * 16) * 4 + 15) / 16 * 16;
-  s.bytes = s.red_off + red_bytes;
+  s.ps_off = s.dh2_off + act_bytes;
+  const int ps_bytes = ((make_layout(nc).P) * 4 + 15) / 16 * 16;
+  s.frag_off = s.ps_off + ps_bytes;  // bf16 MFMA B fragments of conv2: [2 (fwd, dgrad)][3][64 lanes][8]
+  s.red_off = s.frag_off + 2 * 3 * 64 * 16;
+  s.bytes = s.red_off + (red_floats(waves) * 4 + 15) / 16 * 16;
   return s;
 }
 
@@ -88,9 +94,9 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     const int* __restrict__ Y,                           // [N] int32 labels (unused in MODE 1)
     const float* __restrict__ params, int nc,            // flat fp32 params
     float* __restrict__ out, int out_stride,             // MODE0: slab [B][out_stride]; MODE1: logits
-    float inv_B) {
+    float inv_B, unsigned long long* __restrict__ stamps) {  // stamps: diagnostic phase clock (nullptr = off)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const Smem sm = make_smem(L, WAVES);
+  const Smem sm = make_smem(L, WAVES, nc);
   const Layout lay = make_layout(nc);
   const int Lp = sm.Lp;
   const int NP = Lp / 32;  // tile pairs (32 time steps each)
@@ -98,6 +104,9 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
   float* xs = reinterpret_cast<float*>(smem + sm.xs_off);
   __bf16* h1s = reinterpret_cast<__bf16*>(smem + sm.h1_off);    // row (t+2), 16 channels
   __bf16* dh2s = reinterpret_cast<__bf16*>(smem + sm.dh2_off);  // row (t+4), 16 channels
+  float* ps = reinterpret_cast<float*>(smem + sm.ps_off);       // fp32 copy of the flat params
+  __bf16* fragF = reinterpret_cast<__bf16*>(smem + sm.frag_off); // [3][64][8] conv2 fwd B operand
+  __bf16* fragD = fragF + 3 * 64 * 8;                            // [3][64][8] conv2 dgrad B operand
   float* red = reinterpret_cast<float*>(smem + sm.red_off);
 
   const int tid = threadIdx.x;
@@ -106,119 +115,155 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
   const int h = lane >> 4;   // lane quarter
   const int c = lane & 15;   // channel owned by this lane in C-layout phases
   const int b = blockIdx.x;
-  const long row = idx ? (long)idx[b] : (long)b;
-  const float* xrow = X + row * ldx;
+#define ECG_STAMP(k) \
+  if (stamps && tid == 0) stamps[(long)b * 16 + (k)] = __builtin_amdgcn_s_memtime();
+  if (stamps && tid == 0) stamps[(long)b * 16 + 15] = __builtin_amdgcn_s_memrealtime();
+  ECG_STAMP(0)
 
-  // ---------------- phase 0: stage x, zero halos/accumulators, load weights -------------------
-  for (int i = tid; i < Lp + 16; i += WAVES * 64) {
-    int t = i - 3;
-    xs[i] = (t >= 0 && t < L) ? xrow[t] : 0.f;
+  // ---------------- phase 0: stage params + x into LDS, zero halos ------------------------------
+  // params: coalesced 16-B loads of the whole (tiny) parameter vector; every later weight access is LDS.
+  {
+    const int P4 = lay.P >> 2;
+    for (int i = tid; i < P4; i += WAVES * 64)
+      reinterpret_cast<float4*>(ps)[i] = reinterpret_cast<const float4*>(params)[i];
+    for (int i = (P4 << 2) + tid; i < lay.P; i += WAVES * 64) ps[i] = params[i];
+    // conv2 weights w2[co][ci][k] -> bf16 MFMA B fragments in lane order (read back with one
+    // ds_read_b128 per fragment).  fwd: B[r][co], r = 16k + ci; dgrad: B[r][ci], r = 16k + co;
+    // element (r, col) lives at frag[s = r>>5][lane = 16*((r&31)>>3) + col][j = r&7].
+    for (int e = tid; e < C * C * K2; e += WAVES * 64) {
+      const int co = e / (C * K2), ci = (e / K2) % C, k = e % K2;
+      const __bf16 v = ecg::to_bf16(params[lay.w2 + e]);
+      const int rf = 16 * k + ci, rd = 16 * k + co;
+      fragF[((rf >> 5) * 64 + 16 * ((rf & 31) >> 3) + co) * 8 + (rf & 7)] = v;
+      fragD[((rd >> 5) * 64 + 16 * ((rd & 31) >> 3) + ci) * 8 + (rd & 7)] = v;
+    }
+    // r in [80, 96) (the 6th, padding tap) is zero: s = 2, lane quarters 2 and 3
+    for (int e = tid; e < 2 * 32 * 8; e += WAVES * 64) {
+      const int which = e >> 8, l = 32 + ((e >> 3) & 31), j = e & 7;
+      (which ? fragD : fragF)[(2 * 64 + l) * 8 + j] = ecg::to_bf16(0.f);
+    }
+  }
+  int ylab = 0;
+  {
+    const long row = idx ? (long)idx[b] : (long)b;
+    if (MODE == 0) ylab = Y[row];  // label prefetched with the window (used by the head)
+    const float* xrow = X + row * ldx;
+    for (int i = tid; i < Lp + 16; i += WAVES * 64) {
+      const int t = i - 3;
+      xs[i] = (t >= 0 && t < L) ? xrow[t] : 0.f;
+    }
   }
   {
     // h1 halo rows: index 0,1 (t=-2,-1) and [Lp+2, Lp+8) ; dh2 halo rows: [0,4) and [Lp+4, Lp+8)
     uint32_t* h1w = reinterpret_cast<uint32_t*>(h1s);
     uint32_t* dhw = reinterpret_cast<uint32_t*>(dh2s);
     for (int i = tid; i < 8 * 8; i += WAVES * 64) {  // 8 rows x 8 dwords each
-      int r = i >> 3, d = i & 7;
-      int hr = r < 2 ? r : Lp + 2 + (r - 2);
+      const int r = i >> 3, d = i & 7;
+      const int hr = r < 2 ? r : Lp + 2 + (r - 2);
       h1w[hr * 8 + d] = 0u;
-      int dr = r < 4 ? r : Lp + 4 + (r - 4);
+      const int dr = r < 4 ? r : Lp + 4 + (r - 4);
       dhw[dr * 8 + d] = 0u;
     }
-    if (MODE == 0)
-      for (int i = tid; i < RED_G; i += WAVES * 64) red[i] = 0.f;
   }
-  float w1r[K1];
-#pragma unroll
-  for (int k = 0; k < K1; ++k) w1r[k] = params[lay.w1 + c * K1 + k];
-  const float b1r = params[lay.b1 + c];
-  const float b2r = params[lay.b2 + c];
-  // conv2 forward B operand: B[r][co], r = 32s + 8h + j -> tap = r>>4, ci = r&15, co = c.
-  bf16x8 Bf[3];
-#pragma unroll
-  for (int s = 0; s < 3; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      int r = 32 * s + 8 * h + j, tap = r >> 4, ci = r & 15;
-      float v = tap < K2 ? params[lay.w2 + c * (C * K2) + ci * K2 + tap] : 0.f;
-      Bf[s][j] = ecg::to_bf16(v);
-    }
   __syncthreads();
+  ECG_STAMP(1)
 
   // ---------------- phase 1: conv1 + bias + ReLU (VALU) into h1s (bf16) ------------------------
   uint32_t mask1 = 0u, mask2 = 0u;
+  {
+    float w1r[K1];
 #pragma unroll
-  for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
-    const int pair = w + pi * WAVES;
-    if (pair < NP) {
+    for (int k = 0; k < K1; ++k) w1r[k] = ps[lay.w1 + c * K1 + k];
+    const float b1r = ps[lay.b1 + c];
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const int t0 = 32 * pair + 16 * half;
+    for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
+      const int pair = w + pi * WAVES;
+      if (pair < NP) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int t = t0 + 4 * h + i;
-          float v = b1r;
+        for (int half = 0; half < 2; ++half) {
+          const int t0 = 32 * pair + 16 * half + 4 * h;
+          float xw[4 + K1 - 1];
 #pragma unroll
-          for (int k = 0; k < K1; ++k) v = fmaf(w1r[k], xs[t + k], v);
-          v = (t < L) ? fmaxf(v, 0.f) : 0.f;
-          __bf16 vb = ecg::to_bf16(v);
-          h1s[(t + 2) * C + c] = vb;
-          mask1 |= (ecg::from_bf16(vb) > 0.f ? 1u : 0u) << (pi * 8 + half * 4 + i);
+          for (int e = 0; e < 4 + K1 - 1; ++e) xw[e] = xs[t0 + e];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int t = t0 + i;
+            float v = b1r;
+#pragma unroll
+            for (int k = 0; k < K1; ++k) v = fmaf(w1r[k], xw[i + k], v);
+            v = (t < L) ? fmaxf(v, 0.f) : 0.f;
+            const __bf16 vb = ecg::to_bf16(v);
+            h1s[(t + 2) * C + c] = vb;
+            mask1 |= (ecg::from_bf16(vb) > 0.f ? 1u : 0u) << (pi * 8 + half * 4 + i);
+          }
         }
       }
     }
   }
   __syncthreads();
+  ECG_STAMP(2)
 
   // ---------------- phase 2: conv2 (MFMA) + bias + ReLU, mean-pool partials ---------------------
-  float pool = 0.f;
+  {
+    bf16x8 Bf[3];
 #pragma unroll
-  for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
-    const int pair = w + pi * WAVES;
-    if (pair < NP) {
+    for (int s = 0; s < 3; ++s) Bf[s] = *reinterpret_cast<const bf16x8*>(fragF + (s * 64 + lane) * 8);
+    const float b2r = ps[lay.b2 + c];
+    float pool = 0.f;
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const int t0 = 32 * pair + 16 * half;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
+      const int pair = w + pi * WAVES;
+      if (pair < NP) {
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          const int tap = 2 * s + (h >> 1);
-          const int r = t0 + (lane & 15) + tap - 2;  // h1 time index
-          const bf16x8 A = *reinterpret_cast<const bf16x8*>(h1s + (r + 2) * C + 8 * (h & 1));
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bf[s], acc, 0, 0, 0);
-        }
+        for (int half = 0; half < 2; ++half) {
+          const int t0 = 32 * pair + 16 * half;
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int t = t0 + 4 * h + i;
-          float v = fmaxf(acc[i] + b2r, 0.f);
-          if (t >= L) v = 0.f;
-          pool += v;
-          mask2 |= (v > 0.f ? 1u : 0u) << (pi * 8 + half * 4 + i);
+          for (int s = 0; s < 3; ++s) {
+            const int tap = 2 * s + (h >> 1);
+            const int r = t0 + (lane & 15) + tap - 2;  // h1 time index
+            const bf16x8 A = *reinterpret_cast<const bf16x8*>(h1s + (r + 2) * C + 8 * (h & 1));
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bf[s], acc, 0, 0, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int t = t0 + 4 * h + i;
+            float v = fmaxf(acc[i] + b2r, 0.f);
+            if (t >= L) v = 0.f;
+            pool += v;
+            mask2 |= (v > 0.f ? 1u : 0u) << (pi * 8 + half * 4 + i);
+          }
         }
       }
     }
+    pool = ecg::quarter_sum(pool);
+    if (lane < 16) red[RED_POOL + w * 16 + lane] = pool;
   }
-  pool = ecg::quarter_sum(pool);
-  if (lane < 16) red[RED_POOL + w * 16 + lane] = pool;
   __syncthreads();
+  ECG_STAMP(3)
 
   // ---------------- head: pooled -> logits -> CE -> dlogits, dWh, dbh, dpooled ----------------
   if (w == 0) {
-    float pooled = 0.f;
+    if (lane < 16) {
+      float pooled = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < WAVES; ++ww) pooled += red[RED_POOL + ww * 16 + c];
-    pooled *= (1.0f / (float)L);
-    // Broadcast the 16 pooled channels to every lane (all lanes active: no divergent shuffles).
+      for (int ww = 0; ww < WAVES; ++ww) pooled += red[RED_POOL + ww * 16 + lane];
+      red[RED_POOLED + lane] = pooled * (1.0f / (float)L);
+    }
+    // every lane picks up the 16 pooled channels (LDS broadcast reads; same-wave write -> read order)
     float pv[C];
 #pragma unroll
-    for (int co = 0; co < C; ++co) pv[co] = __shfl(pooled, co, 64);
+    for (int q4 = 0; q4 < C / 4; ++q4) {
+      const float4 v = reinterpret_cast<const float4*>(red + RED_POOLED)[q4];
+      pv[4 * q4] = v.x; pv[4 * q4 + 1] = v.y; pv[4 * q4 + 2] = v.z; pv[4 * q4 + 3] = v.w;
+    }
     // lane n (< nc) of each 16-lane group computes logit n
     const int n = c;
     float logit = -INFINITY;
     if (n < nc) {
-      logit = params[lay.bh + n];
+      logit = ps[lay.bh + n];
 #pragma unroll
-      for (int co = 0; co < C; ++co) logit = fmaf(params[lay.wh + n * C + co], pv[co], logit);
+      for (int co = 0; co < C; ++co) logit = fmaf(ps[lay.wh + n * C + co], pv[co], logit);
     }
     if (MODE == 1) {
       if (lane < nc) out[(long)b * out_stride + n] = logit;
@@ -226,11 +271,11 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
       float m = logit;
 #pragma unroll
       for (int off = 8; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
-      float e = (n < nc) ? __expf(logit - m) : 0.f;
+      const float e = (n < nc) ? __expf(logit - m) : 0.f;
       float ssum = e;
 #pragma unroll
       for (int off = 8; off >= 1; off >>= 1) ssum += __shfl_xor(ssum, off, 64);
-      const int y = Y[row];
+      const int y = ylab;
       const float logit_y = __shfl(logit, (lane & 48) + y, 64);
       const float loss = m + __logf(ssum) - logit_y;
       const float dlogit = (n < nc) ? (e / ssum - (n == y ? 1.f : 0.f)) * inv_B : 0.f;
@@ -243,147 +288,170 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
       if (lane == 0) srow[lay.P] = loss;
       // dpooled[co] = sum_n dlogit[n] * Wh[n][co]; lane co (< 16)
       float dp = 0.f;
-      for (int nn = 0; nn < nc; ++nn) dp = fmaf(__shfl(dlogit, nn, 64), params[lay.wh + nn * C + c], dp);
+      for (int nn = 0; nn < nc; ++nn) dp = fmaf(__shfl(dlogit, nn, 64), ps[lay.wh + nn * C + c], dp);
       if (lane < 16) red[RED_G + c] = dp * (1.0f / (float)L);
     }
   }
   if (MODE == 1) return;
   __syncthreads();
+  ECG_STAMP(4)
 
   // ---------------- phase 3: dh2 (= g * relu'), db2, conv2 wgrad (MFMA) ------------------------
-  const float g = red[RED_G + c];
-  float db2 = 0.f;
-  f32x4 accW[K2];
+  {
+    const float g = red[RED_G + c];
+    float db2 = 0.f;
+    f32x4 accW[K2];
 #pragma unroll
-  for (int k = 0; k < K2; ++k) accW[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < K2; ++k) accW[k] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
-    const int pair = w + pi * WAVES;
-    if (pair < NP) {
-      bf16x8 Adh;  // A[co][t] in the permuted k-order of the forward C layout
+    for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
+      const int pair = w + pi * WAVES;
+      if (pair < NP) {
+        bf16x8 Adh;  // A[co][t] in the permuted k-order of the forward C layout
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
+        for (int half = 0; half < 2; ++half) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int t = 32 * pair + 16 * half + 4 * h + i;
-          const bool on = (mask2 >> (pi * 8 + half * 4 + i)) & 1u;
-          const float d = on ? g : 0.f;
-          const __bf16 db = ecg::to_bf16(d);
-          dh2s[(t + 4) * C + c] = db;
-          db2 += d;
-          Adh[half * 4 + i] = db;
+          for (int i = 0; i < 4; ++i) {
+            const int t = 32 * pair + 16 * half + 4 * h + i;
+            const bool on = (mask2 >> (pi * 8 + half * 4 + i)) & 1u;
+            const float d = on ? g : 0.f;
+            const __bf16 db = ecg::to_bf16(d);
+            dh2s[(t + 4) * C + c] = db;
+            db2 += d;
+            Adh[half * 4 + i] = db;
+          }
+        }
+        const int t0 = 32 * pair;
+        const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
+#pragma unroll
+        for (int k = 0; k < K2; ++k) {
+          const int ra = t0 + 4 * h + k - 2 + q;  // h1 time index of row q of the first 4x16 block
+          const s16x4 lo = lds_tr16(h1s + (ra + 2) * C + p4);
+          const s16x4 hi = lds_tr16(h1s + (ra + 16 + 2) * C + p4);
+          accW[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Adh, cat44(lo, hi), accW[k], 0, 0, 0);
         }
       }
-      const int t0 = 32 * pair;
-      const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
-#pragma unroll
-      for (int k = 0; k < K2; ++k) {
-        const int ra = t0 + 4 * h + k - 2 + q;  // h1 time index of row q of the first 4x16 block
-        const s16x4 lo = lds_tr16(h1s + (ra + 2) * C + p4);
-        const s16x4 hi = lds_tr16(h1s + (ra + 16 + 2) * C + p4);
-        accW[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Adh, cat44(lo, hi), accW[k], 0, 0, 0);
-      }
     }
+    // this wave's partial dW2[co = 4h+i][ci = c][k] -> its own LDS slot (summed over waves later)
+    float* pw = red + red_dw2(WAVES) + w * 1280;
+#pragma unroll
+    for (int k = 0; k < K2; ++k)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pw[(4 * h + i) * (C * K2) + c * K2 + k] = accW[k][i];
+    db2 = ecg::quarter_sum(db2);
+    if (lane < 16) red[red_db2(WAVES) + w * 16 + c] = db2;
   }
-  // accW[k][i] = dW2[co = 4h+i][ci = c][k]
-#pragma unroll
-  for (int k = 0; k < K2; ++k)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) atomicAdd(&red[RED_DW2 + (4 * h + i) * (C * K2) + c * K2 + k], accW[k][i]);
-  db2 = ecg::quarter_sum(db2);
-  if (lane < 16) atomicAdd(&red[RED_DB2 + c], db2);
-  // conv2 dgrad B operand: B[r][ci], r = 32s + 8h + j -> tap k = r>>4, co = r&15, ci = c.
-  bf16x8 Bd[3];
-#pragma unroll
-  for (int s = 0; s < 3; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      int r = 32 * s + 8 * h + j, k = r >> 4, co = r & 15;
-      float v = k < K2 ? params[lay.w2 + co * (C * K2) + c * K2 + k] : 0.f;
-      Bd[s][j] = ecg::to_bf16(v);
-    }
   __syncthreads();
+  ECG_STAMP(5)
 
   // ---------------- phase 4: conv2 dgrad (MFMA) * relu'(h1), conv1 wgrad (VALU) ---------------
-  float dw1[K1 + 1];
+  {
+    bf16x8 Bd[3];
 #pragma unroll
-  for (int k = 0; k <= K1; ++k) dw1[k] = 0.f;
+    for (int s = 0; s < 3; ++s) Bd[s] = *reinterpret_cast<const bf16x8*>(fragD + (s * 64 + lane) * 8);
+    float dw1[K1 + 1];
 #pragma unroll
-  for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
-    const int pair = w + pi * WAVES;
-    if (pair < NP) {
+    for (int k = 0; k <= K1; ++k) dw1[k] = 0.f;
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const int t0 = 32 * pair + 16 * half;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
+      const int pair = w + pi * WAVES;
+      if (pair < NP) {
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          const int k = 2 * s + (h >> 1);
-          const int r = t0 + (lane & 15) - k + 2;  // dh2 time index
-          const bf16x8 A = *reinterpret_cast<const bf16x8*>(dh2s + (r + 4) * C + 8 * (h & 1));
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bd[s], acc, 0, 0, 0);
-        }
+        for (int half = 0; half < 2; ++half) {
+          const int t0 = 32 * pair + 16 * half;
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int t = t0 + 4 * h + i;
-          const bool on = (mask1 >> (pi * 8 + half * 4 + i)) & 1u;
-          const float d = on ? acc[i] : 0.f;
-          dw1[K1] += d;
+          for (int s = 0; s < 3; ++s) {
+            const int k = 2 * s + (h >> 1);
+            const int r = t0 + (lane & 15) - k + 2;  // dh2 time index
+            const bf16x8 A = *reinterpret_cast<const bf16x8*>(dh2s + (r + 4) * C + 8 * (h & 1));
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bd[s], acc, 0, 0, 0);
+          }
+          const int tb = t0 + 4 * h;
+          float xw[4 + K1 - 1];
 #pragma unroll
-          for (int k = 0; k < K1; ++k) dw1[k] = fmaf(d, xs[t + k], dw1[k]);
+          for (int e = 0; e < 4 + K1 - 1; ++e) xw[e] = xs[tb + e];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bool on = (mask1 >> (pi * 8 + half * 4 + i)) & 1u;
+            const float d = on ? acc[i] : 0.f;
+            dw1[K1] += d;
+#pragma unroll
+            for (int k = 0; k < K1; ++k) dw1[k] = fmaf(d, xw[i + k], dw1[k]);
+          }
         }
       }
     }
-  }
 #pragma unroll
-  for (int k = 0; k <= K1; ++k) {
-    float v = ecg::quarter_sum(dw1[k]);
-    if (lane < 16) atomicAdd(&red[RED_DW1 + c * 8 + k], v);
+    for (int k = 0; k <= K1; ++k) {
+      const float v = ecg::quarter_sum(dw1[k]);
+      if (lane < 16) red[red_dw1(WAVES) + w * 128 + c * 8 + k] = v;
+    }
   }
   __syncthreads();
+  ECG_STAMP(6)
 
-  // ---------------- phase 5: write this sample's gradient row ---------------------------------
+  // ---------------- phase 5: sum the per-wave partials, write this sample's gradient row -------
   float* srow = out + (long)b * out_stride;
   for (int i = tid; i < lay.wh; i += WAVES * 64) {
-    float v;
+    float v = 0.f;
     if (i < lay.b1) {
-      v = red[RED_DW1 + (i / K1) * 8 + (i % K1)];
+      const int o = red_dw1(WAVES) + (i / K1) * 8 + (i % K1);
+#pragma unroll
+      for (int ww = 0; ww < WAVES; ++ww) v += red[o + ww * 128];
     } else if (i < lay.w2) {
-      v = red[RED_DW1 + (i - lay.b1) * 8 + K1];
+      const int o = red_dw1(WAVES) + (i - lay.b1) * 8 + K1;
+#pragma unroll
+      for (int ww = 0; ww < WAVES; ++ww) v += red[o + ww * 128];
     } else if (i < lay.b2) {
-      v = red[RED_DW2 + (i - lay.w2)];
+      const int o = red_dw2(WAVES) + (i - lay.w2);
+#pragma unroll
+      for (int ww = 0; ww < WAVES; ++ww) v += red[o + ww * 1280];
     } else {
-      v = red[RED_DB2 + (i - lay.b2)];
+      const int o = red_db2(WAVES) + (i - lay.b2);
+#pragma unroll
+      for (int ww = 0; ww < WAVES; ++ww) v += red[o + ww * 16];
     }
     srow[i] = v;
   }
+  ECG_STAMP(7)
+  if (stamps && tid == 0) stamps[(long)b * 16 + 14] = __builtin_amdgcn_s_memrealtime();
+#undef ECG_STAMP
 }
 
 // Sum the per-sample gradient rows and apply SGD (+momentum, weight decay, nesterov) in place.
-// grid = ceil((P+1)/64) blocks of 256 threads; column P of the slab carries the per-sample loss.
-__global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
+// grid = ceil((P+1)/16) blocks of 256 threads: 16 columns x 16 row groups per block, each thread keeps 16
+// independent row loads in flight.  The slab was just written by CUs on every XCD, so this is a
+// latency/fabric-bound read of ~1.5 MB: spreading it over ~90 CUs (not 23) is what makes it fast.
+// Column P carries the per-sample loss (accumulated into loss_acc, never SGD-updated).
+constexpr int RED_COLS = 16;
+constexpr int RED_ROWG = 16;
+__global__ __launch_bounds__(RED_COLS * RED_ROWG) void slab_reduce_sgd_kernel(
     const float* __restrict__ slab, int G, int stride, int P,
     float* __restrict__ params, float* __restrict__ mom, float* __restrict__ grad_out,
     float* __restrict__ loss_acc, float lr, float momentum, float wd, int nesterov, int apply) {
-  __shared__ float part[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + lane;
+  __shared__ float part[RED_ROWG][RED_COLS + 1];
+  const int cl = threadIdx.x % RED_COLS, rg = threadIdx.x / RED_COLS;
+  const int col = blockIdx.x * RED_COLS + cl;
   float s = 0.f;
   if (col <= P) {
-    int r = w;
-    for (; r + 12 < G; r += 16) {
-      float a0 = slab[(long)r * stride + col];
-      float a1 = slab[(long)(r + 4) * stride + col];
-      float a2 = slab[(long)(r + 8) * stride + col];
-      float a3 = slab[(long)(r + 12) * stride + col];
-      s += (a0 + a1) + (a2 + a3);
+    const float* base = slab + col;
+    int r = rg;
+    for (; r + RED_ROWG * 15 < G; r += RED_ROWG * 16) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = base[(long)(r + RED_ROWG * j) * stride];
+#pragma unroll
+      for (int j = 0; j < 16; j += 2) s += v[j] + v[j + 1];
     }
-    for (; r < G; r += 4) s += slab[(long)r * stride + col];
+    for (; r < G; r += RED_ROWG) s += base[(long)r * stride];
   }
-  part[w][lane] = s;
+  part[rg][cl] = s;
   __syncthreads();
-  if (w == 0 && col <= P) {
-    float gsum = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+  if (rg == 0 && col <= P) {
+    float gsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < RED_ROWG; ++j) gsum += part[j][cl];
     if (col == P) {
       if (loss_acc) loss_acc[0] += gsum;
     } else {
@@ -402,29 +470,42 @@ __global__ __launch_bounds__(256) void slab_reduce_sgd_kernel(
   }
 }
 
+unsigned long long* g_stamps = nullptr;  // diagnostic phase stamps (ecg_tiny_set_stamps)
+
 template <int WAVES, int MODE>
 int launch_step(const float* X, int L, long ldx, const int* idx, const int* Y, const float* params, int nc,
                 float* out, int out_stride, int B, float inv_B, hipStream_t stream) {
-  const Smem sm = make_smem(L, WAVES);
+  const Smem sm = make_smem(L, WAVES, nc);
   auto kern = tiny_ecg_step_kernel<WAVES, MODE>;
   if (sm.bytes > 64 * 1024)
     ECG_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, sm.bytes));
   hipLaunchKernelGGL(kern, dim3(B), dim3(WAVES * 64), sm.bytes, stream, X, L, ldx, idx, Y, params, nc, out,
-                     out_stride, inv_B);
+                     out_stride, inv_B, g_stamps);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
 
+constexpr int kMaxLds = 160 * 1024;
+
+// 16 waves (one tile pair each at L=500) when the per-wave partial slots fit in LDS, else 8.
+// ECG_TINY_WAVES=8|16 overrides (tuning); the choice never changes results beyond fp32 summation order.
 int pick_waves(int L) {
   const int Lp = (L + 31) / 32 * 32;
-  return Lp <= 32 * 4 * 8 ? 8 : 16;  // 4 tile pairs per wave max
+  static int forced = -1;
+  if (forced < 0) {
+    const char* e = getenv("ECG_TINY_WAVES");
+    forced = e ? atoi(e) : 0;
+  }
+  const bool fit16 = Lp <= 32 * 4 * 16 && make_smem(L, 16).bytes <= kMaxLds;
+  if (forced == 16 && fit16) return 16;
+  if (forced == 8) return 8;
+  return (fit16 && Lp / 32 >= 16) ? 16 : 8;
 }
 
 int check_step_args(int L, int nc, int B, int out_stride, int mode) {
   if (L < 8 || B <= 0 || nc < 1 || nc > MAX_CLASSES) return ecg::kBadArg;
   const int Lp = (L + 31) / 32 * 32;
-  if (Lp > 32 * 4 * 16) return ecg::kTooLarge;  // > 2048 samples per window: use the op-by-op path
-  if (make_smem(L, 16).bytes > 160 * 1024) return ecg::kTooLarge;
+  if (Lp > 32 * 4 * 8 || make_smem(L, 8).bytes > kMaxLds) return ecg::kTooLarge;  // use the op-by-op path
   const Layout lay = make_layout(nc);
   if (mode == 0 && out_stride < lay.P + 1) return ecg::kBadArg;
   if (mode == 1 && out_stride < nc) return ecg::kBadArg;
@@ -448,8 +529,8 @@ int reduce_dispatch(const float* slab, int G, int stride, int P, float* params, 
                     hipStream_t stream) {
   if (G <= 0 || P <= 0 || stride < P + 1) return ecg::kBadArg;
   if (apply && (!params || (momentum != 0.f && !mom))) return ecg::kBadArg;
-  const int blocks = (P + 1 + 63) / 64;
-  hipLaunchKernelGGL(slab_reduce_sgd_kernel, dim3(blocks), dim3(256), 0, stream, slab, G, stride, P, params, mom,
+  const int blocks = (P + 1 + RED_COLS - 1) / RED_COLS;
+  hipLaunchKernelGGL(slab_reduce_sgd_kernel, dim3(blocks), dim3(RED_COLS * RED_ROWG), 0, stream, slab, G, stride, P, params, mom,
                      grad_out, loss_acc, lr, momentum, wd, nesterov, apply);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
@@ -465,6 +546,13 @@ struct RoundGraph {
 
 // ---------------------------------------------------------------------------- C ABI
 ECG_API int ecg_tiny_param_count(int nc) { return make_layout(nc).P; }
+
+// Diagnostic: when set, every fused-step workgroup b writes s_memtime at each phase boundary to
+// stamps[b*16 + k] (k = 0..8) and s_memrealtime at entry/exit to [b*16+15] / [b*16+14].
+ECG_API int ecg_tiny_set_stamps(unsigned long long* stamps) {
+  g_stamps = stamps;
+  return ecg::kOk;
+}
 
 ECG_API int ecg_tiny_smem_bytes(int L) { return make_smem(L, pick_waves(L)).bytes; }
 
