@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Module-1 locality benchmark CLI (reference Module_1/bench_locality.py, same flags) + A4 LABL + A5.
+
+    python bench_locality.py --dataset synthetic --batch-sizes 64 128 256 512 --iters 100
+Writes results/part1_locality_results.csv (+ part1_labl_results.csv) and, with --plots, the PNGs.
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import crossscale_ecg  # noqa: E402,F401
+from crossscale_ecg.bench.module1 import run_locality, measure_step, bench_labl  # noqa: E402,F401
+from crossscale_ecg.models.tiny_ecg import TinyECG as Tiny1D  # noqa: E402,F401
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dataset", choices=["mitbih", "synthetic"], default="synthetic")
+    ap.add_argument("--device", type=str, default=None)
+    ap.add_argument("--batch-sizes", nargs="+", type=int, default=[64, 128, 256, 512])
+    ap.add_argument("--iters", type=int, default=100)
+    ap.add_argument("--num-workers", type=int, default=4)
+    ap.add_argument("--shard-dir", default="data/shards")
+    ap.add_argument("--n-windows", type=int, default=20000)
+    ap.add_argument("--compute", choices=["torch", "fused"], default="torch")
+    ap.add_argument("--no-labl", action="store_true")
+    ap.add_argument("--no-normalize", action="store_true")
+    ap.add_argument("--results-dir", default="results")
+    ap.add_argument("--plots", action="store_true")
+    a = ap.parse_args(argv)
+    if a.dataset == "mitbih":
+        print("[WARN] MIT-BIH needs wfdb + network; falling back to synthetic shards.")
+    rows = run_locality(a.shard_dir, a.batch_sizes, a.iters, a.num_workers, a.device, a.compute, a.results_dir,
+                        a.n_windows, labl=not a.no_labl, normalize=not a.no_normalize)
+    if a.plots:
+        from crossscale_ecg.report.plots import plot_locality
+        plot_locality(os.path.join(a.results_dir, "part1_locality_results.csv"), a.results_dir)
+    return rows
+
+
+if __name__ == "__main__":
+    main()

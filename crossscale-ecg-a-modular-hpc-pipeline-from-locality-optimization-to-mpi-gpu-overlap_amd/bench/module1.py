@@ -1,0 +1,259 @@
+"""Module 1: data-locality benchmark (A0-A4) on MI355X.
+
+Reference: Module_1/bench_locality.py (A0-A3, ``measure_step``) and
+Module_1/train_ecg_labl(EXPERIMENTAL).py (A4 ``bench_labl``).  Configurations:
+
+  A0_baseline          random sampler, pageable host batches, blocking H2D
+  A1_contiguous        contiguous (sequential) sampler            <- the reference's A0 == A1 bug is fixed
+  A2_contig_pinned     + pinned host batches
+  A3_contig_pinned_nb  + non_blocking H2D
+  A4_LABL              C++ mmap reader -> hipHostMalloc slab ring (producer thread) -> hipMemcpyAsync on a
+                       copy stream, double-buffered against compute, event-fenced slab reuse, z-score
+  A5_GPU_RESIDENT      whole shard resident in HBM (the Module-3 path; no per-step H2D)
+
+Per-step breakdown (data_ms / h2d_ms / compute_ms) is measured like the reference (sync-bracketed
+wall-clock).  ``step_ms`` is the measured wall time per step; for A0-A3 it equals the sum of the parts
+(the parts are serialised by syncs, as in bench_locality.py:43-71), for A4 it is smaller because the
+next batch's fill and copy overlap the current batch's compute.
+``samples_per_s = (samples/iters) / (step_ms/1e3)`` (bench_locality.py:73-74).
+``compute`` is the reference eager step (TinyECG fwd/CE/bwd/SGD lr 1e-2) or, with ``compute="fused"``,
+the fused HIP step fed from the same device batch buffer.
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch.utils.data import DataLoader, RandomSampler, SequentialSampler
+
+from ..data.dataset import ShardDataset
+from ..data.shards import ensure_synthetic_shards, list_shards
+from ..models.tiny_ecg import TinyECG
+from ..utils.csvio import LOCALITY_COLUMNS, LABL_COLUMNS, write_csv
+
+CONFIGS = [
+    ("A0_baseline", False, False, False),
+    ("A1_contiguous", True, False, False),
+    ("A2_contig_pinned", True, True, False),
+    ("A3_contig_pinned_nb", True, True, True),
+]
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+class _Compute:
+    """One training step on a device batch x [B,1,L], y [B]."""
+
+    def __init__(self, dev, kind: str, B: int, L: int):
+        self.dev, self.kind = dev, kind
+        self.model = TinyECG().to(dev)
+        if kind == "fused":
+            from ..ops.fused_tiny import slab_stride
+            self.flat = self.model.flatten_parameters()
+            self.mom = torch.zeros_like(self.flat)
+            self.slab = torch.empty((B, slab_stride(2)), device=dev)
+            self.loss = torch.zeros(1, device=dev)
+            self.y32 = None
+        else:
+            self.opt = torch.optim.SGD(self.model.parameters(), lr=1e-2)
+
+    def __call__(self, x: torch.Tensor, y: torch.Tensor):
+        if self.kind == "fused":
+            from ..ops import _lib
+            x2 = x.reshape(x.shape[0], -1)
+            y32 = y.to(torch.int32)
+            st = _lib.kernels().ecg_tiny_train_step(x2.data_ptr(), x2.shape[1], x2.stride(0), None, y32.data_ptr(),
+                                                    self.flat.data_ptr(), self.mom.data_ptr(), 2,
+                                                    self.slab.data_ptr(), self.slab.shape[1], x2.shape[0],
+                                                    self.loss.data_ptr(), 1e-2, 0.0, 0.0, 0,
+                                                    _lib.stream_ptr(self.dev))
+            _lib.check(st, "ecg_tiny_train_step")
+            return
+        out = self.model(x)
+        loss = F.cross_entropy(out, y)
+        loss.backward()
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
+
+
+def measure_step(dl: DataLoader, device, non_blocking: bool, iters: int = 50, compute: str = "torch") -> Dict:
+    """Reference ``measure_step`` (bench_locality.py:23-76): 5 warm-up steps, then timed data/H2D/compute."""
+    dev = torch.device(device)
+    B = dl.batch_size
+    L = dl.dataset.x.shape[1]
+    step = _Compute(dev, compute, B, L)
+    it = iter(dl)
+
+    def nxt():
+        nonlocal it
+        try:
+            return next(it)
+        except StopIteration:
+            it = iter(dl)
+            return next(it)
+
+    for _ in range(5):
+        xc, yc = nxt()
+        step(xc.to(dev, non_blocking=non_blocking), yc.to(dev, non_blocking=non_blocking))
+    _sync(dev)
+    data_ms = h2d_ms = comp_ms = 0.0
+    total = 0
+    it = iter(dl)
+    t_all = time.perf_counter()
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        xc, yc = nxt()
+        t1 = time.perf_counter()
+        _sync(dev)
+        th0 = time.perf_counter()
+        x = xc.to(dev, non_blocking=non_blocking)
+        y = yc.to(dev, non_blocking=non_blocking)
+        _sync(dev)
+        th1 = time.perf_counter()
+        step(x, y)
+        _sync(dev)
+        t3 = time.perf_counter()
+        data_ms += (t1 - t0) * 1e3
+        h2d_ms += (th1 - th0) * 1e3
+        comp_ms += (t3 - th1) * 1e3
+        total += x.shape[0]
+    wall = (time.perf_counter() - t_all) * 1e3 / iters
+    sps = (total / iters) / (wall / 1e3)
+    return dict(data_ms=data_ms / iters, h2d_ms=h2d_ms / iters, compute_ms=comp_ms / iters, step_ms=wall,
+                samples_per_s=sps)
+
+
+def bench_labl(shard_paths: Sequence[str], batch_size: int, iters: int, normalize: bool, device,
+               compute: str = "torch", num_slots: int = 4) -> Dict:
+    """A4: native LABL prefetcher + copy-stream H2D double buffer (reference bench_labl, :23-94)."""
+    from ..ops.native_io import NativePrefetcher
+    dev = torch.device(device)
+    pf = NativePrefetcher(shard_paths, batch_size, num_slots=num_slots, normalize=normalize,
+                          pinned=dev.type == "cuda", loop=True)
+    L = pf.L
+    step = _Compute(dev, compute, batch_size, L)
+    y = torch.zeros(batch_size, dtype=torch.long, device=dev)  # labels allocated once (reference re-pinned per step)
+    bufs = [torch.empty((batch_size, 1, L), device=dev) for _ in range(2)]
+    copy = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+    main = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+    ready = [None, None]
+    consumed = [None, None]  # compute that last read bufs[k] (WAR fence for the next copy into it)
+    pf.start()
+
+    def stage(i):
+        """Fill-wait + async H2D of the next slab into bufs[i%2]; returns (n, wait_ms)."""
+        t0 = time.perf_counter()
+        r = pf.next_batch_cpu()
+        wait = (time.perf_counter() - t0) * 1e3
+        slot, view, _fill = r
+        n = view.shape[0]
+        if dev.type == "cuda":
+            if consumed[i % 2] is not None:
+                copy.wait_event(consumed[i % 2])  # WAR: the compute that read this buffer must be done
+            pf.h2d(slot, n, bufs[i % 2], copy)
+            ev = torch.cuda.Event()
+            ev.record(copy)
+            ready[i % 2] = ev
+        else:
+            bufs[i % 2][:n].copy_(view)
+            pf.recycle(slot)
+        return n, wait
+
+    try:
+        for i in range(5):  # warm-up
+            n, _ = stage(i)
+            if main is not None:
+                main.wait_event(ready[i % 2])
+            step(bufs[i % 2][:n], y[:n])
+            if main is not None:
+                consumed[i % 2] = torch.cuda.Event()
+                consumed[i % 2].record(main)
+        _sync(dev)
+        data_ms = h2d_ms = comp_ms = 0.0
+        total = 0
+        n_next, w = stage(0)
+        data_ms += w
+        t_all = time.perf_counter()
+        for i in range(iters):
+            n = n_next
+            if main is not None:
+                th = time.perf_counter()
+                main.wait_event(ready[i % 2])
+                h2d_ms += (time.perf_counter() - th) * 1e3
+            tc = time.perf_counter()
+            step(bufs[i % 2][:n], y[:n])  # enqueue compute of batch i
+            if main is not None:
+                consumed[i % 2] = torch.cuda.Event()
+                consumed[i % 2].record(main)
+            if i + 1 < iters:
+                n_next, w = stage(i + 1)  # fill + copy batch i+1 while batch i computes
+                data_ms += w
+            _sync(dev)
+            comp_ms += (time.perf_counter() - tc) * 1e3
+            total += n
+        wall = (time.perf_counter() - t_all) * 1e3 / iters
+    finally:
+        pf.close()
+    return dict(step_ms=wall, samples_per_s=(total / iters) / (wall / 1e3), data_ms=data_ms / iters,
+                h2d_ms=h2d_ms / iters, compute_ms=comp_ms / iters)
+
+
+def bench_gpu_resident(shard_paths, batch_size, iters, device, compute="torch") -> Dict:
+    from ..data.dataset import load_shards_to_gpu, make_gpu_batch_iter
+    dev = torch.device(device)
+    x, y = load_shards_to_gpu(shard_paths, dev)
+    it = make_gpu_batch_iter(x, y, batch_size)
+    step = _Compute(dev, compute, batch_size, x.shape[1])
+    for _ in range(5):
+        step(*next(it))
+    _sync(dev)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        step(*next(it))
+    _sync(dev)
+    wall = (time.perf_counter() - t0) * 1e3 / iters
+    return dict(step_ms=wall, samples_per_s=batch_size / (wall / 1e3), data_ms=0.0, h2d_ms=0.0, compute_ms=wall)
+
+
+def run_locality(shard_dir: str, batch_sizes: List[int], iters: int = 100, num_workers: int = 4,
+                 device: Optional[str] = None, compute: str = "torch", results_dir: str = "results",
+                 n_windows: int = 20000, labl: bool = True, normalize: bool = True) -> List[Dict]:
+    dev = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    paths = ensure_synthetic_shards(shard_dir, n_windows, shard_size=8192) if not list_shards(shard_dir) \
+        else list_shards(shard_dir)
+    ds = ShardDataset(paths)
+    rows, labl_rows = [], []
+    for bs in batch_sizes:
+        for name, contiguous, pin, nb in CONFIGS:
+            sampler = SequentialSampler(ds) if contiguous else RandomSampler(ds)
+            dl = DataLoader(ds, batch_size=bs, sampler=sampler, num_workers=num_workers,
+                            pin_memory=pin and dev.type == "cuda", drop_last=True,
+                            persistent_workers=num_workers > 0)
+            st = measure_step(dl, dev, non_blocking=nb, iters=iters, compute=compute)
+            row = dict(config=name, batch_size=bs, pin_memory=pin, contiguous=contiguous, non_blocking=nb, **st)
+            print(row, flush=True)
+            rows.append(row)
+        if labl:
+            st = bench_labl(paths, bs, iters, normalize, dev, compute=compute)
+            r = dict(config="A4_LABL", batch_size=bs, **st)
+            print(r, flush=True)
+            labl_rows.append(r)
+            rows.append(dict(config="A4_LABL", batch_size=bs, pin_memory=True, contiguous=True, non_blocking=True,
+                             **st))
+        if dev.type == "cuda":
+            st = bench_gpu_resident(paths, bs, iters, dev, compute=compute)
+            rows.append(dict(config="A5_GPU_RESIDENT", batch_size=bs, pin_memory=False, contiguous=False,
+                             non_blocking=False, **st))
+            print(rows[-1], flush=True)
+    os.makedirs(results_dir, exist_ok=True)
+    write_csv(os.path.join(results_dir, "part1_locality_results.csv"), rows, LOCALITY_COLUMNS)
+    if labl_rows:
+        write_csv(os.path.join(results_dir, "part1_labl_results.csv"), labl_rows, LABL_COLUMNS)
+    return rows

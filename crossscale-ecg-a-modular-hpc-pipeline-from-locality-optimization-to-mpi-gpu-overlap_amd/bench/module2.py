@@ -1,0 +1,244 @@
+"""Module 2: hand-written conv1d kernel vs PyTorch's native Conv1d.
+
+Reference: Module_2/benchmark_part_2.py (grid B in {64,128,256,512} x K in {3,5,7}, L=500, 15 trials of
+``time_once`` = 3 warm-up calls + 1 timed call, median/mean/pstdev/p95, ``speedup_med = torch/omp``) and
+Module_2/train_cpu_openmp.py (thread scaling at K=32).
+
+Two comparisons are produced:
+  * ``part2_hip_results.csv``    - HIP ``conv1d_batch_hip`` vs ``torch.nn.Conv1d`` on the MI355X (MIOpen).
+    Three timings per cell: ``*_call_ms`` = the reference's single call + device sync (host wall clock,
+    dominated by launch + sync latency), ``*_ms`` = back-to-back calls between syncs (host per-call cost,
+    the number the headline speedup uses), ``*_ev_ms`` = hipEvent device time per call.  Every cell is
+    also checked against an fp64 reference (``max_abs_err``), which the reference never did.
+  * ``part2_openmp_results.csv`` - the C++ OpenMP/AVX kernel (reference C ABI) vs CPU ``nn.Conv1d`` on the
+    host CPU: the reference's exact like-for-like experiment.
+"""
+from __future__ import annotations
+
+import os
+import statistics as stats
+import time
+from typing import Callable, Dict, List, Tuple
+
+import numpy as np
+import torch
+
+from ..ops.conv1d import conv1d_valid, run_omp_conv, conv1d_valid_reference
+from ..utils.csvio import PART2_COLUMNS, PART2_RAW_COLUMNS, PART2_SCALING_COLUMNS, safe_write_csv
+
+BATCH_SIZES = [64, 128, 256, 512]
+KERNEL_SIZES = [3, 5, 7]
+L = 500
+TRIALS = 15
+WARMUP_STEPS = 3
+
+
+def time_once(fn: Callable, warmup_steps: int = WARMUP_STEPS, sync: Callable = lambda: None) -> float:
+    """Reference semantics: warm-up calls, then ONE timed call (plus a device sync on GPUs)."""
+    for _ in range(warmup_steps):
+        fn()
+    sync()
+    t0 = time.perf_counter()
+    fn()
+    sync()
+    return (time.perf_counter() - t0) * 1e3
+
+
+def time_burst(fn: Callable, inner: int, sync: Callable) -> float:
+    for _ in range(WARMUP_STEPS):
+        fn()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(inner):
+        fn()
+    sync()
+    return (time.perf_counter() - t0) * 1e3 / inner
+
+
+def time_events(fn: Callable, inner: int) -> float:
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(WARMUP_STEPS):
+        fn()
+    a.record(s)
+    for _ in range(inner):
+        fn()
+    b.record(s)
+    b.synchronize()
+    return a.elapsed_time(b) / inner
+
+
+def _agg(prefix: str, xs: List[float]) -> Dict[str, float]:
+    return {f"{prefix}_median": float(stats.median(xs)), f"{prefix}_mean": float(stats.fmean(xs)),
+            f"{prefix}_std": float(stats.pstdev(xs)), f"{prefix}_p95": float(np.percentile(xs, 95))}
+
+
+def bench_pair_gpu(bs: int, K: int, rng: np.random.Generator, trials: int = TRIALS, inner: int = 50,
+                   device: str = "cuda") -> Tuple[Dict, List[Tuple[float, float]]]:
+    x_np = rng.normal(0, 1, size=(bs, L)).astype(np.float32)
+    w_np = rng.normal(0, 1, size=(K,)).astype(np.float32)
+    dev = torch.device(device)
+    xt = torch.from_numpy(x_np).to(dev)
+    xt4 = xt.unsqueeze(1)
+    wt = torch.from_numpy(w_np).to(dev)
+    conv = torch.nn.Conv1d(1, 1, K, bias=False).to(dev)
+    with torch.no_grad():
+        conv.weight.copy_(wt.view(1, 1, K))
+    out = torch.empty((bs, L - K + 1), device=dev)
+    sync = torch.cuda.synchronize
+
+    def torch_step():
+        with torch.no_grad():
+            conv(xt4)
+
+    def hip_step():
+        conv1d_valid(xt, wt, backend="hip", out=out)
+
+    hip_step()
+    sync()
+    ref = conv1d_valid_reference(x_np, w_np)
+    err = float(np.abs(out.cpu().numpy() - ref).max())
+    t_call, h_call, t_b, h_b, t_e, h_e = [], [], [], [], [], []
+    raw = []
+    for _ in range(trials):
+        tc, hc = time_once(torch_step, sync=sync), time_once(hip_step, sync=sync)
+        t_call.append(tc)
+        h_call.append(hc)
+        raw.append((tc, hc))
+        t_b.append(time_burst(torch_step, inner, sync))
+        h_b.append(time_burst(hip_step, inner, sync))
+        t_e.append(time_events(torch_step, inner))
+        h_e.append(time_events(hip_step, inner))
+    row = {"batch_size": bs, "kernel_size": K, "backend": "hip"}
+    row.update(_agg("torch_call_ms", t_call))
+    row.update(_agg("hip_call_ms", h_call))
+    row.update(_agg("torch_ms", t_b))
+    row.update(_agg("hip_ms", h_b))
+    row["torch_ev_ms"] = float(stats.median(t_e))
+    row["hip_ev_ms"] = float(stats.median(h_e))
+    row["torch_sps"] = bs / (row["torch_ms_median"] / 1e3)
+    row["hip_sps"] = bs / (row["hip_ms_median"] / 1e3)
+    row["speedup_med"] = row["torch_ms_median"] / row["hip_ms_median"]
+    row["speedup_call_med"] = row["torch_call_ms_median"] / row["hip_call_ms_median"]
+    row["speedup_ev"] = row["torch_ev_ms"] / row["hip_ev_ms"]
+    row["max_abs_err"] = err
+    return row, raw
+
+
+def bench_pair_cpu(bs: int, K: int, rng: np.random.Generator, nthreads: int, trials: int = TRIALS):
+    """Reference experiment on the host: native C++ kernel vs CPU torch nn.Conv1d."""
+    x_np = rng.normal(0, 1, size=(bs, L)).astype(np.float32)
+    w_np = rng.normal(0, 1, size=(K,)).astype(np.float32)
+    xt4 = torch.from_numpy(x_np).unsqueeze(1)
+    conv = torch.nn.Conv1d(1, 1, K, bias=False)
+    with torch.no_grad():
+        conv.weight[:] = torch.from_numpy(w_np).reshape(1, 1, K)
+    y = np.empty((bs, L - K + 1), np.float32)
+
+    def torch_step():
+        with torch.no_grad():
+            conv(xt4)
+
+    def omp_step():
+        run_omp_conv(x_np, w_np, nthreads, y)
+
+    omp_step()
+    err = float(np.abs(y - conv1d_valid_reference(x_np, w_np)).max())
+    tm, om = [], []
+    for _ in range(trials):
+        tm.append(time_once(torch_step))
+        om.append(time_once(omp_step))
+    row = {"batch_size": bs, "kernel_size": K, "nthreads": nthreads}
+    row.update(_agg("torch_ms", tm))
+    row.update(_agg("omp_ms", om))
+    row["torch_sps"] = bs / (row["torch_ms_median"] / 1e3)
+    row["omp_sps"] = bs / (row["omp_ms_median"] / 1e3)
+    row["speedup_med"] = row["torch_ms_median"] / row["omp_ms_median"]
+    row["max_abs_err"] = err
+    return row, list(zip(tm, om))
+
+
+HIP_COLUMNS = ["batch_size", "kernel_size", "backend", "torch_call_ms_median", "hip_call_ms_median",
+               "torch_ms_median", "torch_ms_mean", "torch_ms_std", "torch_ms_p95", "hip_ms_median", "hip_ms_mean",
+               "hip_ms_std", "hip_ms_p95", "torch_ev_ms", "hip_ev_ms", "torch_sps", "hip_sps", "speedup_med",
+               "speedup_call_med", "speedup_ev", "max_abs_err"]
+
+
+def run_part2(results_dir: str = "results", gpu: bool = True, cpu: bool = True, trials: int = TRIALS,
+              nthreads: int | None = None, batch_sizes=BATCH_SIZES, kernel_sizes=KERNEL_SIZES,
+              verbose: bool = True) -> Dict[str, List[Dict]]:
+    os.makedirs(results_dir, exist_ok=True)
+    out: Dict[str, List[Dict]] = {}
+    nthreads = nthreads or os.cpu_count() or 1
+    if gpu and torch.cuda.is_available():
+        rng = np.random.default_rng(1337)
+        rows, raw = [], []
+        for bs in batch_sizes:
+            for K in kernel_sizes:
+                row, r = bench_pair_gpu(bs, K, rng, trials)
+                rows.append(row)
+                raw += [{"batch_size": bs, "kernel_size": K, "trial": i, "torch_ms": a, "omp_ms": b}
+                        for i, (a, b) in enumerate(r)]
+                if verbose:
+                    print(f"[HIP] B={bs} K={K}: torch {row['torch_ms_median'] * 1e3:.1f} us  hip "
+                          f"{row['hip_ms_median'] * 1e3:.1f} us  speedup {row['speedup_med']:.2f}x "
+                          f"(single-call {row['speedup_call_med']:.2f}x, device {row['speedup_ev']:.2f}x) "
+                          f"err {row['max_abs_err']:.1e}", flush=True)
+        safe_write_csv(rows, os.path.join(results_dir, "part2_hip_results.csv"), HIP_COLUMNS)
+        safe_write_csv(raw, os.path.join(results_dir, "part2_hip_results_raw.csv"), PART2_RAW_COLUMNS)
+        out["hip"] = rows
+    if cpu:
+        rng = np.random.default_rng(1337)
+        torch.set_num_threads(nthreads)
+        rows, raw = [], []
+        for bs in batch_sizes:
+            for K in kernel_sizes:
+                row, r = bench_pair_cpu(bs, K, rng, nthreads, trials)
+                rows.append(row)
+                raw += [{"batch_size": bs, "kernel_size": K, "trial": i, "torch_ms": a, "omp_ms": b}
+                        for i, (a, b) in enumerate(r)]
+                if verbose:
+                    print(f"[CPU] B={bs} K={K}: torch {row['torch_ms_median']:.3f} ms  omp "
+                          f"{row['omp_ms_median']:.3f} ms  speedup {row['speedup_med']:.2f}x", flush=True)
+        safe_write_csv(rows, os.path.join(results_dir, "part2_openmp_results.csv"), PART2_COLUMNS + ["max_abs_err"])
+        safe_write_csv(raw, os.path.join(results_dir, "part2_openmp_results_raw.csv"), PART2_RAW_COLUMNS)
+        out["cpu"] = rows
+    return out
+
+
+def run_thread_scaling(results_dir: str = "results", threads=(1, 2, 4, 8, 16), batches=(64, 128, 256, 512),
+                       K: int = 32, iters: int = 50, warmup: int = 5) -> List[Dict]:
+    """Reference train_cpu_openmp.py: CPU kernel compute_ms / samples_per_s per (threads, batch) at K=32."""
+    rows = []
+    rng = np.random.default_rng(0)
+    for th in threads:
+        for bs in batches:
+            x = rng.normal(size=(bs, L)).astype(np.float32)
+            w = rng.normal(size=(K,)).astype(np.float32)
+            y = np.empty((bs, L - K + 1), np.float32)
+            for _ in range(warmup):
+                run_omp_conv(x, w, th, y)
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                run_omp_conv(x, w, th, y)
+            ms = (time.perf_counter() - t0) * 1e3 / iters
+            rows.append({"threads": th, "batch": bs, "compute_ms": ms, "samples_per_s": bs / (ms / 1e3)})
+    safe_write_csv(rows, os.path.join(results_dir, "part2_openmp_simd_results.csv"), PART2_SCALING_COLUMNS)
+    return rows
+
+
+def run_gpu_batch_scaling(results_dir: str = "results", batches=(64, 256, 1024, 4096, 16384, 65536), K: int = 7,
+                          inner: int = 50) -> List[Dict]:
+    """GPU analog of the thread sweep: device time and samples/s vs batch (how many windows fill 256 CUs)."""
+    rows = []
+    dev = torch.device("cuda")
+    for bs in batches:
+        x = torch.randn(bs, L, device=dev)
+        w = torch.randn(K, device=dev)
+        out = torch.empty(bs, L - K + 1, device=dev)
+        ms = time_events(lambda: conv1d_valid(x, w, backend="hip", out=out), inner)
+        rows.append({"batch": bs, "kernel_size": K, "device_ms": ms, "samples_per_s": bs / (ms / 1e3),
+                     "GBps": 2 * bs * L * 4 / (ms / 1e3) / 1e9})
+    safe_write_csv(rows, os.path.join(results_dir, "part2_hip_batch_scaling.csv"),
+                   ["batch", "kernel_size", "device_ms", "samples_per_s", "GBps"])
+    return rows

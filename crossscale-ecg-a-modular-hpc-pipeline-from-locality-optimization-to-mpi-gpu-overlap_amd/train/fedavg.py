@@ -1,0 +1,243 @@
+"""Federated averaging driver: one FL client per GPU (or per CPU process under gloo).
+
+Reference: TRUE_FL_M3/part3_fedavg_overlap_mpi_gpu.py:137-239 (``main``).  Per configuration (G0 fp32,
+G1 AMP) a fresh TinyECG + SGD(lr 1e-2, momentum 0.9); per round: broadcast the global model, run
+``local_steps`` local SGD steps on this client's GPU-resident shard, average the weights over clients.
+Every round emits a ``RoundStats`` row with the reference's columns (``samples_per_s = n / local_ms``,
+excluding comm) and MI355X columns (``comm_exposed_ms``, ``round_wall_ms``); rank 0 appends all rows to
+the results CSV and prints node-aggregate samples/s (sum over clients, wall time including comm).
+
+MI355X execution (vs the reference's host-staged per-tensor MPI calls and per-step sync):
+  * G1 local round = ONE native hipGraph replay of ``local_steps`` fused HIP steps (``ops.fused_tiny``);
+  * FedAvg = ONE RCCL ``all_reduce(AVG)`` of the flat fp32 weight buffer; broadcast = ONE RCCL broadcast;
+  * ``--overlap delayed``: the all-reduce runs on RCCL's stream under the next round (stale-by-one FedAvg);
+  * ``--sync none``: pseudo-federated independent clients; ``--sync ddp``: synchronous gradient DP;
+  * ``--drop-prob``: client dropout with sample-weighted averaging; ``--ckpt-every``/``--resume``.
+"""
+from __future__ import annotations
+
+import os
+import random
+import time
+from dataclasses import asdict
+from glob import glob
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..config import FedAvgConfig
+from ..data.dataset import load_shards_to_gpu
+from ..data.shards import assign_shards_evenly
+from ..models import build_model
+from ..parallel.env import DistContext, barrier
+from ..parallel.fedavg import (Communicator, broadcast_model, fedavg_allreduce, weighted_fedavg_, DelayedFedAvg,
+                               model_flat)
+from ..utils import profiling
+from ..utils.ckpt import ckpt_path, save_checkpoint, load_checkpoint, latest_checkpoint
+from ..utils.csvio import RoundStats, append_results, ROUND_COLUMNS
+from ..utils.log import RankLogger
+from .local import TorchLocalTrainer
+
+
+def set_basic_seeds(seed: int) -> None:
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(seed)
+
+
+def _sync(dev: torch.device):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def load_client_data(cfg: FedAvgConfig, ctx: DistContext):
+    """This client's windows on its device: shards (round-robin) or on-device synthetic data."""
+    dev = ctx.device
+    if cfg.synthetic_windows > 0 or not cfg.data_root:
+        n = cfg.synthetic_windows if cfg.synthetic_windows > 0 else cfg.max_windows
+        n = min(n, cfg.max_windows) if cfg.max_windows else n
+        g = torch.Generator(device=dev)
+        g.manual_seed(1337 + ctx.rank)
+        x = torch.randn((n, cfg.win_len), generator=g, device=dev)
+        if cfg.labels == "parity":
+            y = (x.mean(1) > 0).long()
+        else:
+            y = torch.zeros(n, dtype=torch.long, device=dev)
+        return x, y
+    paths = sorted(glob(os.path.join(cfg.data_root, "ecg_*.bin")))
+    if not paths:
+        raise RuntimeError(f"No ecg_*.bin files found in {cfg.data_root}")
+    mine = assign_shards_evenly(paths, ctx.world_size, ctx.rank)
+    return load_shards_to_gpu(mine, dev, max_windows=cfg.max_windows, labels=cfg.labels)
+
+
+def _amp(cfg: FedAvgConfig):
+    return {"bf16": torch.bfloat16, "fp16": torch.float16, "none": None}[cfg.amp_dtype]
+
+
+def make_trainer(cfg: FedAvgConfig, config_name: str, model, x, y, ctx: DistContext, backend: str):
+    seed = cfg.seed + 7919 * ctx.rank
+    if backend == "fused":
+        from ..ops.fused_tiny import FusedTinyTrainer
+        return FusedTinyTrainer(model, x, y, cfg.batch_size, cfg.local_steps, lr=cfg.lr, momentum=cfg.momentum,
+                                seed=seed)
+    amp = None if config_name == "G0" else _amp(cfg)
+    net = model
+    if cfg.sync == "ddp" and ctx.distributed:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        net = DDP(model, device_ids=[dev_index(ctx)] if ctx.device.type == "cuda" else None, bucket_cap_mb=4)
+    return TorchLocalTrainer(net, x, y, cfg.batch_size, lr=cfg.lr, momentum=cfg.momentum, amp_dtype=amp, seed=seed)
+
+
+def dev_index(ctx):
+    return ctx.device.index if ctx.device.index is not None else 0
+
+
+def pick_backend(cfg: FedAvgConfig, config_name: str, ctx: DistContext) -> str:
+    if cfg.kernel_backend == "torch" or ctx.device.type != "cuda":
+        return "torch"
+    fused_ok = (config_name == "G1" and cfg.amp_dtype == "bf16" and cfg.model == "tiny_ecg")
+    if cfg.kernel_backend == "fused":
+        if not fused_ok:
+            raise ValueError("the fused HIP step implements TinyECG with bf16 AMP (config G1, --amp-dtype bf16)")
+        return "fused"
+    return "fused" if fused_ok else "torch"
+
+
+def _ddp_fused_round(trainer, ctx: DistContext, n: int):
+    """Synchronous data parallel on the fused kernels: grads -> RCCL all-reduce(AVG) -> flat SGD per step."""
+    from ..ops import _lib
+    from ..ops.fused_tiny import tiny_step_grads
+    from ..ops.sgd import FlatSGD
+    from ..parallel.fedavg import allreduce_mean_
+    if not hasattr(trainer, "_ddp_opt"):
+        trainer._ddp_grad = torch.zeros_like(trainer.params)
+        trainer._ddp_opt = FlatSGD(trainer.params, trainer._ddp_grad, lr=trainer.lr, momentum=trainer.momentum)
+    trainer.loss_acc.zero_()
+    trainer._loss_steps = n
+    trainer.sampler.fill(trainer.idx_table[:n])
+    lib = _lib.kernels()
+    for s in range(n):
+        tiny_step_grads(trainer.params, trainer.x, trainer.y32, trainer.idx_table[s], trainer.B, trainer.nc,
+                        trainer.slab)
+        st = lib.ecg_slab_reduce_sgd(trainer.slab.data_ptr(), trainer.B, trainer.stride, trainer.P, None, None,
+                                     trainer._ddp_grad.data_ptr(), trainer.loss_acc.data_ptr(), 0.0, 0.0, 0.0, 0, 0,
+                                     _lib.stream_ptr(trainer.device))
+        _lib.check(st, "ecg_slab_reduce_sgd")
+        allreduce_mean_(trainer._ddp_grad, ctx)
+        trainer._ddp_opt.step()
+
+
+def run_fedavg(cfg: FedAvgConfig, ctx: DistContext) -> List[Dict]:
+    log = RankLogger(ctx.rank, cfg.jsonl, cfg.quiet)
+    comm = Communicator(ctx)
+    dev = ctx.device
+    torch.set_num_threads(max(1, min(4, os.cpu_count() or 1)))
+    x, y = load_client_data(cfg, ctx)
+    if x.shape[0] < cfg.batch_size:
+        raise RuntimeError(f"client {ctx.rank} has {x.shape[0]} windows < batch {cfg.batch_size}")
+    log.info(f"[fedavg] world={ctx.world_size} backend={ctx.backend} device={dev} windows/client={x.shape[0]} "
+             f"L={x.shape[1]} B={cfg.batch_size} rounds={cfg.rounds}x{cfg.local_steps} sync={cfg.sync} "
+             f"overlap={cfg.overlap}")
+    configs = ["G0", "G1"] if cfg.config == "both" else [cfg.config]
+    all_rows: List[Dict] = []
+    for cname in configs:
+        set_basic_seeds(cfg.seed + ctx.rank)
+        torch.manual_seed(cfg.seed)  # identical init on every client (the round-0 broadcast makes it exact)
+        model = build_model(cfg.model, cfg.num_classes).to(dev)
+        backend = pick_backend(cfg, cname, ctx)
+        flat = model.flatten_parameters() if hasattr(model, "flatten_parameters") else None
+        trainer = make_trainer(cfg, cname, model, x, y, ctx, backend)
+        start_round = 0
+        if cfg.resume:
+            p = latest_checkpoint(cfg.ckpt_dir, cname)
+            if p:
+                st = load_checkpoint(p)
+                model.load_state_dict(st["model"])
+                start_round = int(st["round"]) + 1
+                log.info(f"[fedavg] resumed {cname} from {p} at round {start_round}")
+        delayed = DelayedFedAvg(model_flat(model), ctx) if (cfg.overlap == "delayed" and cfg.sync == "fedavg") else None
+        rows = []
+        for r in range(start_round, cfg.rounds):
+            t_round0 = time.perf_counter()
+            # ---- broadcast the global model ------------------------------------------------
+            _sync(dev)
+            t_c0 = time.perf_counter()
+            if cfg.sync == "fedavg" and ctx.distributed and (r == start_round or cfg.bcast_every_round):
+                with profiling.range("bcast"):
+                    broadcast_model(comm, model)
+                _sync(dev)
+            t_c1 = time.perf_counter()
+            # ---- local steps -----------------------------------------------------------------
+            with profiling.range("local_round"):
+                if cfg.sync == "ddp" and backend == "fused" and ctx.distributed:
+                    _ddp_fused_round(trainer, ctx, cfg.local_steps)
+                else:
+                    trainer.run_round(cfg.local_steps)
+                _sync(dev)
+            t_l1 = time.perf_counter()
+            avg_loss = trainer.avg_loss()
+            n_samples = cfg.batch_size * cfg.local_steps
+            # ---- FedAvg ----------------------------------------------------------------------
+            _sync(dev)
+            t_c2 = time.perf_counter()
+            if cfg.sync == "fedavg" and ctx.distributed:
+                with profiling.range("fedavg"):
+                    if cfg.drop_prob > 0:
+                        rng = random.Random(cfg.seed * 1000003 + r * 8191 + ctx.rank)
+                        w = 0.0 if rng.random() < cfg.drop_prob else float(n_samples)
+                        weighted_fedavg_(model_flat(model), w, ctx)
+                    elif delayed is not None:
+                        delayed.boundary()
+                    else:
+                        fedavg_allreduce(comm, model)
+                _sync(dev)
+            t_c3 = time.perf_counter()
+            local_ms = (t_l1 - t_c1) * 1e3
+            comm_ms = ((t_c1 - t_c0) + (t_c3 - t_c2)) * 1e3
+            row = RoundStats(config=cname, world_size=ctx.world_size, rank=ctx.rank, round_idx=r,
+                             batch_size=cfg.batch_size, local_steps=cfg.local_steps, local_train_ms=local_ms,
+                             comm_ms=comm_ms, samples_per_s=n_samples / (local_ms / 1e3), avg_loss=avg_loss,
+                             comm_exposed_ms=comm_ms, round_wall_ms=(time.perf_counter() - t_round0) * 1e3,
+                             backend=backend, overlap=cfg.overlap if cfg.sync == "fedavg" else cfg.sync)
+            rows.append(asdict(row))
+            log.event("round", **asdict(row))
+            if cfg.ckpt_every and ctx.rank == 0 and (r + 1) % cfg.ckpt_every == 0:
+                mom = getattr(trainer, "mom", None)
+                save_checkpoint(ckpt_path(cfg.ckpt_dir, r, cname), r, model, mom, cname, asdict(cfg))
+        if delayed is not None:
+            delayed.finalize()
+            _sync(dev)
+        if hasattr(trainer, "close"):
+            trainer.close()
+        gathered = comm.gather(rows, root=0)
+        if ctx.rank == 0:
+            flat_rows = [row for rl in gathered for row in rl]
+            all_rows.extend(flat_rows)
+            if cfg.results_csv:
+                append_results(flat_rows, cfg.results_csv, ROUND_COLUMNS)
+            summarize(flat_rows, cname, ctx.world_size, log)
+        barrier(ctx)
+    return all_rows
+
+
+def summarize(rows: List[Dict], cname: str, world: int, log: RankLogger) -> Dict[str, float]:
+    if not rows:
+        return {}
+    rounds = sorted({r["round_idx"] for r in rows})
+    per_rank = float(np.mean([r["samples_per_s"] for r in rows]))
+    node = 0.0
+    for ri in rounds:
+        rr = [r for r in rows if r["round_idx"] == ri]
+        wall = max(r["round_wall_ms"] for r in rr) / 1e3
+        node += sum(r["batch_size"] * r["local_steps"] for r in rr) / wall
+    node /= len(rounds)
+    comm = float(np.mean([r["comm_ms"] for r in rows]))
+    local = float(np.mean([r["local_train_ms"] for r in rows]))
+    log.info(f"=== {cname} world={world}: per-rank samples/s (ref metric, excl. comm) {per_rank:,.0f} | "
+             f"node samples/s (incl. comm) {node:,.0f} | local_ms {local:.3f} comm_ms {comm:.3f} | "
+             f"final loss {rows[-1]['avg_loss']:.4f}")
+    return {"per_rank_sps": per_rank, "node_sps": node, "comm_ms": comm, "local_ms": local}

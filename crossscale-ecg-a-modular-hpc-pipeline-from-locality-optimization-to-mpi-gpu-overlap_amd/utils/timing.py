@@ -1,0 +1,63 @@
+"""Timers: host wall clock with device fences, and hipEvent-based per-stream timers.
+
+Reference timing is ``time.perf_counter()`` bracketed by ``torch.cuda.synchronize()``
+(bench_locality.py:44-66, part3_fedavg...py:188-211).  ``WallTimer`` reproduces that exactly;
+``StreamTimer`` measures work on one stream with hipEvents (no host sync inside the timed region) so
+copy/compute/comm overlap can be measured rather than assumed.
+"""
+from __future__ import annotations
+
+import time
+from contextlib import contextmanager
+from typing import Optional
+
+import torch
+
+
+def sync(device: Optional[torch.device]) -> None:
+    if device is not None and torch.device(device).type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+class WallTimer:
+    def __init__(self, device=None):
+        self.device = device
+        self.ms = 0.0
+
+    @contextmanager
+    def __call__(self, fence: bool = True):
+        if fence:
+            sync(self.device)
+        t0 = time.perf_counter()
+        yield self
+        if fence:
+            sync(self.device)
+        self.ms += (time.perf_counter() - t0) * 1e3
+
+
+class StreamTimer:
+    """Accumulates elapsed time of regions enqueued on a stream (read with ``elapsed_ms()``)."""
+
+    def __init__(self, stream: Optional[torch.cuda.Stream] = None):
+        self.stream = stream
+        self.pairs = []
+
+    @contextmanager
+    def region(self):
+        s = self.stream or torch.cuda.current_stream()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        yield
+        b.record(s)
+        self.pairs.append((a, b))
+
+    def elapsed_ms(self) -> float:
+        total = 0.0
+        for a, b in self.pairs:
+            b.synchronize()
+            total += a.elapsed_time(b)
+        return total
+
+    def reset(self):
+        self.pairs = []

@@ -1,0 +1,154 @@
+"""Multi-process FedAvg / collectives on CPU with gloo (world 2 and 4), launcher env shim, entry points."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import crossscale_ecg  # noqa: F401
+from crossscale_ecg.parallel import env as penv
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn_name, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    penv._CTX = None
+    torch.set_num_threads(1)
+    try:
+        ctx = penv.init_distributed(backend="gloo", prefer_gpu=False)
+        res = globals()[fn_name](ctx)
+        q.put((rank, "ok", res))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, "err", traceback.format_exc()))
+    finally:
+        penv.shutdown_distributed()
+
+
+def _run(world, fn_name):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, fn_name, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in range(world):
+        rank, status, res = q.get(timeout=240)
+        assert status == "ok", res
+        out[rank] = res
+    for p in ps:
+        p.join(timeout=60)
+    return out
+
+
+def case_fedavg_mean(ctx):
+    from crossscale_ecg.models.tiny_ecg import TinyECG
+    from crossscale_ecg.parallel.fedavg import Communicator, fedavg_allreduce, broadcast_model
+    torch.manual_seed(100 + ctx.rank)
+    m = TinyECG()
+    m.flatten_parameters()
+    before = m.flat.clone()
+    comm = Communicator(ctx)
+    allb = [torch.zeros_like(before) for _ in range(ctx.world_size)]
+    dist.all_gather(allb, before)
+    fedavg_allreduce(comm, m)
+    expect = torch.stack(allb).mean(0)
+    ok_mean = torch.allclose(m.flat, expect, atol=1e-6)
+    # broadcast from rank 0 of a perturbed model
+    with torch.no_grad():
+        m.flat.add_(ctx.rank)
+    broadcast_model(comm, m)
+    g = [torch.zeros_like(m.flat) for _ in range(ctx.world_size)]
+    dist.all_gather(g, m.flat)
+    ok_bcast = all(torch.equal(g[0], t) for t in g)
+    sd_ok = torch.equal(m.state_dict()["head.bias"], m.flat[1456:1458])
+    return ok_mean and ok_bcast and sd_ok
+
+
+def case_unflattened_model(ctx):
+    from crossscale_ecg.parallel.fedavg import Communicator, fedavg_allreduce
+    torch.manual_seed(ctx.rank)
+    m = torch.nn.Linear(3, 2)
+    w0 = m.weight.detach().clone()
+    g = [torch.zeros_like(w0) for _ in range(ctx.world_size)]
+    dist.all_gather(g, w0)
+    fedavg_allreduce(Communicator(ctx), m)
+    return torch.allclose(m.weight, torch.stack(g).mean(0), atol=1e-6)
+
+
+def case_weighted_and_dropout(ctx):
+    from crossscale_ecg.parallel.fedavg import weighted_fedavg_
+    flat = torch.full((8,), float(ctx.rank + 1))
+    w = 0.0 if ctx.rank == 0 else float(ctx.rank)
+    total = weighted_fedavg_(flat, w, ctx)
+    ws = [0.0] + [float(r) for r in range(1, ctx.world_size)]
+    expect = sum(wi * (r + 1) for r, wi in enumerate(ws)) / sum(ws)
+    return abs(total - sum(ws)) < 1e-6 and torch.allclose(flat, torch.full((8,), expect))
+
+
+def case_delayed_fedavg(ctx):
+    from crossscale_ecg.parallel.fedavg import DelayedFedAvg
+    flat = torch.full((4,), float(ctx.rank))
+    d = DelayedFedAvg(flat, ctx)
+    d.boundary()            # round 0 ends: start avg of w_0 = rank
+    flat.add_(10.0)         # round 1 local progress
+    d.boundary()            # wait: w <- w + (avg_0 - w_0) = rank + 10 + (mean - rank)
+    mean = (ctx.world_size - 1) / 2.0
+    ok1 = torch.allclose(flat, torch.full((4,), mean + 10.0))
+    d.finalize()
+    return ok1
+
+
+def case_communicator(ctx):
+    from crossscale_ecg.parallel.fedavg import Communicator, mpi_avg
+    c = Communicator(ctx)
+    rows = c.gather({"rank": ctx.rank}, root=0)
+    v = mpi_avg(c, float(ctx.rank))
+    c.Barrier()
+    ok = abs(v - (ctx.world_size - 1) / 2) < 1e-9
+    if ctx.rank == 0:
+        ok &= [r["rank"] for r in rows] == list(range(ctx.world_size))
+    return ok
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_fedavg_allreduce_and_broadcast(world):
+    assert all(_run(world, "case_fedavg_mean").values())
+
+
+def test_unflattened_model_path():
+    assert all(_run(2, "case_unflattened_model").values())
+
+
+def test_weighted_fedavg_with_dropped_client():
+    assert all(_run(3, "case_weighted_and_dropout").values())
+
+
+def test_delayed_overlap_semantics():
+    assert all(_run(2, "case_delayed_fedavg").values())
+
+
+def test_communicator_gather_and_avg():
+    assert all(_run(2, "case_communicator").values())
+
+
+def test_launcher_env_shim():
+    env = {"OMPI_COMM_WORLD_RANK": "3", "OMPI_COMM_WORLD_SIZE": "8", "OMPI_COMM_WORLD_LOCAL_RANK": "3"}
+    assert penv.apply_launcher_env_shim(env) == "OMPI"
+    assert (env["RANK"], env["WORLD_SIZE"], env["LOCAL_RANK"]) == ("3", "8", "3")
+    env = {"SLURM_PROCID": "1", "SLURM_NTASKS": "2", "SLURM_LOCALID": "0"}
+    assert penv.apply_launcher_env_shim(env) == "SLURM"
+    assert env["RANK"] == "1" and env["MASTER_ADDR"] == "127.0.0.1"
+    env = {"RANK": "0", "WORLD_SIZE": "1", "PMI_RANK": "5"}
+    assert penv.apply_launcher_env_shim(env) is None and env["RANK"] == "0"

@@ -1,0 +1,108 @@
+"""End-to-end entry points on CPU: shard_prep -> FedAvg (gloo world 2 via torchrun) / pseudo-FL / resume."""
+import csv
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(args, cwd, timeout=300):
+    env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run(args, cwd=cwd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:]
+    return r.stdout
+
+
+@pytest.fixture(scope="module")
+def shards(tmp_path_factory):
+    d = tmp_path_factory.mktemp("prep")
+    _run([sys.executable, os.path.join(ROOT, "shard_prep.py"), "--dataset", "synthetic", "--n-windows", "3000",
+          "--shard_size", "700", "--out-dir", str(d / "shards"), "--results-dir", str(d / "results")], cwd=str(d))
+    return d
+
+
+def test_fedavg_gloo_world2_csv_schema(shards):
+    d = shards
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+                os.path.join(ROOT, "part3_fedavg_overlap_mpi_gpu.py"), "--data-root", str(d / "shards"),
+                "--rounds", "2", "--local-steps", "2", "--batch-size", "32", "--config", "both",
+                "--max-windows", "500", "--results-csv", str(d / "results" / "fedavg_results.csv")], cwd=str(d))
+    assert "G1 world=2" in out
+    rows = list(csv.DictReader(open(d / "results" / "fedavg_results.csv")))
+    assert len(rows) == 2 * 2 * 2  # configs x ranks x rounds
+    ref_cols = ["config", "world_size", "rank", "round_idx", "batch_size", "local_steps", "local_train_ms",
+                "comm_ms", "samples_per_s", "avg_loss"]
+    assert list(rows[0].keys())[:10] == ref_cols
+    # FedAvg: after every round both clients hold identical weights -> identical next-round start;
+    # check the metric formula samples_per_s = n / local_ms
+    r0 = rows[0]
+    n = int(r0["batch_size"]) * int(r0["local_steps"])
+    assert abs(float(r0["samples_per_s"]) - n / (float(r0["local_train_ms"]) / 1e3)) < 1e-3 * float(r0["samples_per_s"])
+
+
+def test_fedavg_overlap_delayed_and_dropout(shards):
+    d = shards
+    for extra in (["--overlap", "delayed"], ["--drop-prob", "0.5"], ["--sync", "ddp"], ["--sync", "none"]):
+        _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+              "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+              os.path.join(ROOT, "part3_fedavg_overlap_mpi_gpu.py"), "--data-root", str(d / "shards"),
+              "--rounds", "2", "--local-steps", "2", "--batch-size", "32", "--config", "G1", "--max-windows", "300",
+              "--results-csv", str(d / "results" / "fedavg_ov.csv"), "--quiet", *extra], cwd=str(d))
+
+
+def test_checkpoint_and_resume(tmp_path):
+    ck = tmp_path / "ck"
+    args = [sys.executable, os.path.join(ROOT, "part3_fedavg_overlap_mpi_gpu.py"), "--synthetic-windows", "400",
+            "--batch-size", "32", "--local-steps", "2", "--config", "G1", "--ckpt-every", "1", "--ckpt-dir", str(ck),
+            "--results-csv", str(tmp_path / "r.csv"), "--quiet"]
+    _run(args + ["--rounds", "2"], cwd=str(tmp_path))
+    assert sorted(os.listdir(ck)) == ["fedavg_G1_round00000.pt", "fedavg_G1_round00001.pt"]
+    _run(args + ["--rounds", "4", "--resume"], cwd=str(tmp_path))
+    rows = list(csv.DictReader(open(tmp_path / "r.csv")))
+    assert [int(r["round_idx"]) for r in rows] == [0, 1, 2, 3]
+    import torch
+    import crossscale_ecg  # noqa: F401
+    from crossscale_ecg.utils.ckpt import load_checkpoint
+    from crossscale_ecg.models.tiny_ecg import TinyECG
+    st = load_checkpoint(str(ck / "fedavg_G1_round00003.pt"))
+    m = TinyECG()
+    m.load_state_dict(st["model"])
+    assert st["round"] == 3 and isinstance(st["momentum"], (torch.Tensor, type(None)))
+
+
+def test_pseudo_fl_entry(tmp_path):
+    out = _run([sys.executable, os.path.join(ROOT, "part3_mpi_gpu_train.py"), "--steps", "3", "--batch-size", "32",
+                "--synthetic-windows", "200", "--results-csv", str(tmp_path / "p.csv"), "--quiet"], cwd=str(tmp_path))
+    rows = list(csv.DictReader(open(tmp_path / "p.csv")))
+    assert list(rows[0].keys()) == ["config", "world_size", "rank", "batch_size", "steps", "data_ms", "h2d_ms",
+                                    "compute_ms", "step_ms", "samples_per_s"]
+    assert rows[0]["config"] == "G0_baseline_GPU_CACHE"
+
+
+def test_module_benches_cpu(tmp_path):
+    _run([sys.executable, os.path.join(ROOT, "benchmark_part_2.py"), "--no-gpu", "--trials", "2", "--results-dir",
+          str(tmp_path)], cwd=str(tmp_path))
+    rows = list(csv.DictReader(open(tmp_path / "part2_openmp_results.csv")))
+    assert len(rows) == 12 and float(rows[0]["max_abs_err"]) < 1e-4
+    _run([sys.executable, os.path.join(ROOT, "bench_locality.py"), "--batch-sizes", "32", "--iters", "3",
+          "--num-workers", "0", "--n-windows", "600", "--shard-dir", str(tmp_path / "sh"), "--results-dir",
+          str(tmp_path)], cwd=str(tmp_path))
+    rows = list(csv.DictReader(open(tmp_path / "part1_locality_results.csv")))
+    assert [r["config"] for r in rows] == ["A0_baseline", "A1_contiguous", "A2_contig_pinned",
+                                           "A3_contig_pinned_nb", "A4_LABL"]
+    _run([sys.executable, os.path.join(ROOT, "plot_results.py"), "--results-dir", str(tmp_path)], cwd=str(tmp_path))
+    assert os.path.exists(tmp_path / "throughput_vs_batch.png")
