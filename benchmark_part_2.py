@@ -14,7 +14,9 @@ from crossscale_ecg.bench.module2 import (run_part2, time_once, BATCH_SIZES, KER
                                           WARMUP_STEPS, run_gpu_batch_scaling)
 from crossscale_ecg.ops.conv1d import run_omp_conv  # noqa: E402,F401
 
-NTHREADS = os.cpu_count()
+from crossscale_ecg.utils import usable_cpus  # noqa: E402
+
+NTHREADS = usable_cpus()
 
 
 def main(argv=None):

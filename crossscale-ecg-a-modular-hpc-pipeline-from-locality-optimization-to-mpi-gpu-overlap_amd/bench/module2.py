@@ -24,6 +24,7 @@ import numpy as np
 import torch
 
 from ..ops.conv1d import conv1d_valid, run_omp_conv, conv1d_valid_reference
+from ..utils import usable_cpus
 from ..utils.csvio import PART2_COLUMNS, PART2_RAW_COLUMNS, PART2_SCALING_COLUMNS, safe_write_csv
 
 BATCH_SIZES = [64, 128, 256, 512]
@@ -169,7 +170,7 @@ def run_part2(results_dir: str = "results", gpu: bool = True, cpu: bool = True, 
               verbose: bool = True) -> Dict[str, List[Dict]]:
     os.makedirs(results_dir, exist_ok=True)
     out: Dict[str, List[Dict]] = {}
-    nthreads = nthreads or os.cpu_count() or 1
+    nthreads = nthreads or usable_cpus()
     if gpu and torch.cuda.is_available():
         rng = np.random.default_rng(1337)
         rows, raw = [], []

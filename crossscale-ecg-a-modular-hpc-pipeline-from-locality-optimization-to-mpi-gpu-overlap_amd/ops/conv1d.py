@@ -18,6 +18,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
+from ..utils import usable_cpus
 
 
 def _as_2d(x: torch.Tensor) -> torch.Tensor:
@@ -87,7 +88,7 @@ def run_omp_conv(x_np: np.ndarray, w_np: np.ndarray, nthreads: int | None = None
         raise ValueError("bad output buffer")
     fp = C.POINTER(C.c_float)
     _lib.cpu_lib().conv1d_batch_omp_simd(x_np.ctypes.data_as(fp), w_np.ctypes.data_as(fp), y_np.ctypes.data_as(fp),
-                                        batch, L, K, int(nthreads or os.cpu_count() or 1))
+                                        batch, L, K, int(nthreads or usable_cpus()))
     return y_np
 
 

@@ -33,7 +33,7 @@ from ..models import build_model
 from ..parallel.env import DistContext, barrier
 from ..parallel.fedavg import (Communicator, broadcast_model, fedavg_allreduce, weighted_fedavg_, DelayedFedAvg,
                                model_flat)
-from ..utils import profiling
+from ..utils import profiling, usable_cpus
 from ..utils.ckpt import ckpt_path, save_checkpoint, load_checkpoint, latest_checkpoint
 from ..utils.csvio import RoundStats, append_results, ROUND_COLUMNS
 from ..utils.log import RankLogger
@@ -135,7 +135,7 @@ def run_fedavg(cfg: FedAvgConfig, ctx: DistContext) -> List[Dict]:
     log = RankLogger(ctx.rank, cfg.jsonl, cfg.quiet)
     comm = Communicator(ctx)
     dev = ctx.device
-    torch.set_num_threads(max(1, min(4, os.cpu_count() or 1)))
+    torch.set_num_threads(max(1, min(4, usable_cpus())))
     x, y = load_client_data(cfg, ctx)
     if x.shape[0] < cfg.batch_size:
         raise RuntimeError(f"client {ctx.rank} has {x.shape[0]} windows < batch {cfg.batch_size}")

@@ -31,12 +31,17 @@ def _world_size() -> int:
 
 
 def run_baseline_gpu(model, batch_iter: Iterator, device, steps: int, rank: int, batch_size: int,
-                     lr: float = 1e-2, log_every: int = 10) -> BenchStats:
+                     lr: float = 1e-2, log_every: int = 10, warmup: int = 5) -> BenchStats:
     """G0: fp32, default stream, no overlap, sync every step (reference semantics)."""
     device = torch.device(device)
     model = model.to(device)
     opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=0.9)
     model.train()
+    for _ in range(warmup):  # untimed: MIOpen solver search / allocator warm-up (not in the reference)
+        x, y = next(batch_iter)
+        F.cross_entropy(model(x), y).backward()
+        opt.zero_grad(set_to_none=True)
+    _sync(device)
     data_ms = compute_ms = step_ms = 0.0
     n_samples = n_steps = 0
     while n_steps < steps:
@@ -63,7 +68,7 @@ def run_baseline_gpu(model, batch_iter: Iterator, device, steps: int, rank: int,
 
 
 def run_overlap_gpu(model, batch_iter: Iterator, device, steps: int, rank: int, batch_size: int,
-                    lr: float = 1e-2, amp_dtype=torch.bfloat16, log_every: int = 10) -> BenchStats:
+                    lr: float = 1e-2, amp_dtype=torch.bfloat16, log_every: int = 10, warmup: int = 5) -> BenchStats:
     """G1: AMP (bf16 by default) + lookahead: batch i+1's device gather is enqueued on a side stream while
     batch i computes on the main stream (reference did the lookahead in Python only)."""
     device = torch.device(device)
@@ -75,6 +80,13 @@ def run_overlap_gpu(model, batch_iter: Iterator, device, steps: int, rank: int, 
     side = torch.cuda.Stream(device)
     main = torch.cuda.current_stream(device)
     model.train()
+    for _ in range(warmup):  # untimed warm-up (MIOpen bf16 solver search)
+        x, y = next(batch_iter)
+        with torch.autocast("cuda", dtype=amp_dtype):
+            loss = F.cross_entropy(model(x), y)
+        loss.backward()
+        opt.zero_grad(set_to_none=True)
+    _sync(device)
     data_ms = compute_ms = step_ms = 0.0
     n_samples = n_steps = 0
     t_d0 = time.perf_counter()

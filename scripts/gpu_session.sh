@@ -30,6 +30,20 @@ for s in $STEPS; do
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 500 --warmup 100 ;;
+    modules)
+      R=gpurun_out/results
+      mkdir -p $R
+      run module2 600 python benchmark_part_2.py --results-dir $R --batch-scaling
+      run module1 900 python bench_locality.py --batch-sizes 64 128 256 512 --iters 100 --num-workers 4 \
+        --shard-dir /tmp/ecg_shards --results-dir $R
+      run module1_fused 600 python bench_locality.py --batch-sizes 256 --iters 100 --num-workers 4 --compute fused \
+        --shard-dir /tmp/ecg_shards --results-dir $R/fused_compute
+      run pseudo_fl 600 python part3_mpi_gpu_train.py --steps 200 --synthetic-windows 20000 \
+        --results-csv $R/part3_mpi_cuda_results.csv --quiet
+      run fedavg1 600 python part3_fedavg_overlap_mpi_gpu.py --synthetic-windows 20000 --rounds 5 \
+        --local-steps 50 --config both --results-csv $R/fedavg_results_w1.csv
+      run plots 300 python plot_results.py --results-dir $R
+      ;;
     prof)
       export TMPDIR=/tmp
       run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
