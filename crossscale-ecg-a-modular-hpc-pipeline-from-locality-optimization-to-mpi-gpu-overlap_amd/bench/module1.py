@@ -60,7 +60,10 @@ class _Compute:
             self.mom = torch.zeros_like(self.flat)
             self.slab = torch.empty((B, slab_stride(2)), device=dev)
             self.loss = torch.zeros(1, device=dev)
-            self.y32 = None
+            from ..ops import _lib
+            lib = _lib.kernels()
+            self.ctl = torch.zeros(lib.ecg_tiny_ctl_ints(), dtype=torch.int32, device=dev)
+            self.gslab = torch.empty((lib.ecg_tiny_gslab_rows(), slab_stride(2)), device=dev)
         else:
             self.opt = torch.optim.SGD(self.model.parameters(), lr=1e-2)
 
@@ -72,7 +75,7 @@ class _Compute:
             st = _lib.kernels().ecg_tiny_train_step(x2.data_ptr(), x2.shape[1], x2.stride(0), None, y32.data_ptr(),
                                                     self.flat.data_ptr(), self.mom.data_ptr(), 2,
                                                     self.slab.data_ptr(), self.slab.shape[1], x2.shape[0],
-                                                    self.loss.data_ptr(), 1e-2, 0.0, 0.0, 0,
+                                                    self.loss.data_ptr(), 1e-2, 0.0, 0.0, 0, None, None,
                                                     _lib.stream_ptr(self.dev))
             _lib.check(st, "ecg_tiny_train_step")
             return

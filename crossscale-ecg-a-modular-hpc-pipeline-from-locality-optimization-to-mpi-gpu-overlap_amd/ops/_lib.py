@@ -65,9 +65,13 @@ def _bind_kernels(lib: C.CDLL) -> None:
     _sig(lib, "ecg_tiny_step_grads", [vp, i32, i64, vp, vp, vp, i32, vp, i32, i32, f32, vp])
     _sig(lib, "ecg_tiny_forward", [vp, i32, i64, vp, vp, i32, vp, i32, vp])
     _sig(lib, "ecg_slab_reduce_sgd", [vp, i32, i32, i32, vp, vp, vp, vp, f32, f32, f32, i32, i32, vp])
-    _sig(lib, "ecg_tiny_train_step", [vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, vp, f32, f32, f32, i32, vp])
+    _sig(lib, "ecg_tiny_train_step", [vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, vp, f32, f32, f32, i32,
+                                      vp, vp, vp])
     _sig(lib, "ecg_round_graph_create", [C.POINTER(vp), vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, i32, vp,
-                                         f32, f32, f32, i32])
+                                         f32, f32, f32, i32, vp, vp])
+    _sig(lib, "ecg_tiny_ctl_ints", [])
+    _sig(lib, "ecg_tiny_gslab_rows", [])
+    _sig(lib, "ecg_tiny_set_stamps", [vp])
     _sig(lib, "ecg_round_graph_launch", [vp, vp])
     _sig(lib, "ecg_round_graph_destroy", [vp])
     _sig(lib, "conv1d_batch_hip", [vp, vp, vp, i32, i32, i32, vp])

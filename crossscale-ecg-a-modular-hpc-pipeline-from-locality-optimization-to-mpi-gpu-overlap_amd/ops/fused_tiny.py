@@ -103,7 +103,8 @@ class FusedTinyTrainer:
 
     def __init__(self, model: TinyECG, x_gpu: torch.Tensor, y_gpu: torch.Tensor, batch_size: int,
                  steps_per_round: int, lr: float = 1e-2, momentum: float = 0.9, weight_decay: float = 0.0,
-                 nesterov: bool = False, seed: Optional[int] = None, use_graph: bool = True):
+                 nesterov: bool = False, seed: Optional[int] = None, use_graph: bool = True,
+                 single_launch: bool = False):
         self.device = x_gpu.device
         self.model = model
         self.nc = model.num_classes
@@ -127,6 +128,12 @@ class FusedTinyTrainer:
         self._graphs = {}  # n_steps -> native hipGraphExec handle
         self.steps_done = 0
         lib = _lib.kernels()
+        # single-launch steps: arrival counters (zero on entry, reset by the kernel) + group partial rows.
+        # Measured on MI355X (profiles/r1_fused_step_v3): the in-kernel write-through reduction tree costs
+        # ~7 us of hand-off latency vs ~5.5 us for slab-reduce kernel + boundary, so two launches is the default.
+        self.single_launch = bool(single_launch)
+        self.ctl = torch.zeros(lib.ecg_tiny_ctl_ints(), dtype=torch.int32, device=self.device)
+        self.gslab = torch.empty((lib.ecg_tiny_gslab_rows(), self.stride), dtype=torch.float32, device=self.device)
         smem = lib.ecg_tiny_smem_bytes(self.x.shape[1])
         if smem > 160 * 1024:
             raise ValueError(f"window length {self.x.shape[1]} too long for the fused kernel ({smem} B LDS)")
@@ -143,7 +150,7 @@ class FusedTinyTrainer:
                                         self.idx_table.data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
                                         self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
                                         n, self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd,
-                                        int(self.nesterov))
+                                        int(self.nesterov), *self._fuse_ptrs())
         _lib.check(st, "ecg_round_graph_create")
         self._graphs[n] = g
         return g
@@ -161,13 +168,16 @@ class FusedTinyTrainer:
             pass
 
     # ------------------------------------------------------------------ execution
+    def _fuse_ptrs(self):
+        return (self.ctl.data_ptr(), self.gslab.data_ptr()) if self.single_launch else (None, None)
+
     def _eager_step(self, s: int):
         lib = _lib.kernels()
         st = lib.ecg_tiny_train_step(self.x.data_ptr(), self.x.shape[1], self.x.stride(0),
                                      self.idx_table[s].data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
                                      self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
                                      self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd, int(self.nesterov),
-                                     _lib.stream_ptr(self.device))
+                                     *self._fuse_ptrs(), _lib.stream_ptr(self.device))
         _lib.check(st, "ecg_tiny_train_step")
 
     def run_round(self, n_steps: Optional[int] = None, reset_loss: bool = True) -> None:

@@ -50,13 +50,46 @@ struct Smem {
 
 // red region (floats): per-wave partials are written with plain stores and summed after a barrier
 // (deterministic; no LDS float atomics).
-constexpr int RED_G = 0;                            // [16] dL/dh2 scale per channel (dpooled / L)
-constexpr int RED_POOLED = 16;                      // [16] pooled features
-constexpr int RED_POOL = 32;                        // [WAVES][16] pooled partials
-__host__ __device__ constexpr int red_dw2(int waves) { return RED_POOL + waves * 16; }       // [WAVES][1280]
-__host__ __device__ constexpr int red_dw1(int waves) { return red_dw2(waves) + waves * 1280; }  // [WAVES][16][8]
-__host__ __device__ constexpr int red_db2(int waves) { return red_dw1(waves) + waves * 128; }   // [WAVES][16]
-__host__ __device__ constexpr int red_floats(int waves) { return red_db2(waves) + waves * 16; }
+constexpr int RED_G = 0;       // [16] dL/dh2 scale per channel (dpooled / L), written by the head
+constexpr int RED_POOLED = 16; // [16] pooled features
+constexpr int RED_FLAG = 32;   // [16] broadcast slot for the last-arriver decision (ints)
+constexpr int RED_POOL = 48;   // [WAVES][16] pooled partials
+
+// In-kernel cross-sample reduction + SGD (one launch per training step).  Deterministic two-level
+// last-arriver tree: the G per-sample rows are summed by NG <= 16 group reducers (group g = b % NG, i.e.
+// one XCD-affine group under round-robin dispatch; correctness never depends on placement), then by the
+// last group reducer, which applies SGD.  Publication follows the agent-scope release -> ticket ->
+// acquire protocol; counters are zero on entry and reset by the final reducer.
+constexpr int kMaxGroups = 16;
+struct FusedOpt {
+  int* ctl;          // [kMaxGroups + 1] arrival counters (nullptr: no in-kernel reduction, slab only)
+  float* gslab;      // [kMaxGroups][out_stride] group partial rows
+  float* params;     // flat fp32 params updated in place by the final reducer
+  float* mom;        // momentum buffer
+  float* loss_acc;   // += sum of per-sample losses
+  float lr, momentum, wd;
+  int nesterov;
+  int G;             // number of workgroups (= batch)
+};
+// conv2 wgrad work split: 5 taps x msplit(WAVES) pair ranges, one (tap, range) per wave 1.. (wave 0 runs the head)
+__host__ __device__ constexpr int msplit(int waves) { return (waves - 1) / 5 < 1 ? 1 : (waves - 1) / 5; }
+__host__ __device__ constexpr int red_cnt(int waves) { return RED_POOL + waves * 16; }      // [WAVES][16] relu'(h2) counts
+__host__ __device__ constexpr int red_m(int waves) { return red_cnt(waves) + waves * 16; }  // [msplit][16*16*5] M partials
+__host__ __device__ constexpr int red_dw1(int waves) { return red_m(waves) + msplit(waves) * 1280; }  // [WAVES][16][8]
+__host__ __device__ constexpr int red_head(int waves) { return red_dw1(waves) + waves * 128; }  // dWh, dbh, loss
+__host__ __device__ constexpr int red_floats(int waves) { return red_head(waves) + 288; }
+
+// Write-through (sc1) global accesses for data handed between workgroups inside one launch: the
+// stores need no release fence and the sc1 loads need no acquire fence (MI355X guide, Guideline 16 R1).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, int idx, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, idx * 4, 0, 16);
+}
+__device__ __forceinline__ float ld_wt(__amdgpu_buffer_rsrc_t r, int idx) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, idx * 4, 0, 16));
+}
 
 __host__ __device__ inline Smem make_smem(int L, int waves, int nc = MAX_CLASSES) {
   Smem s;
@@ -87,6 +120,14 @@ __device__ __forceinline__ s16x4 lds_tr16(const __bf16* p) {
 }
 
 // MODE 0: full training step (grads -> slab row).  MODE 1: forward only (logits -> out [B, nc]).
+//
+// Backward algebra used (h2 = relu(conv2(h1)), pooled = mean_t h2, g[co] = dL/dpooled[co] / L):
+//   dh2[t][co]       = g[co] * m[t][co]          with m = relu'(h2) in {0, 1} (exact in bf16)
+//   dW2[co][ci][k]   = g[co] * M[co][ci][k],     M = sum_t m[t][co] h1[t+k-2][ci]   (needs no g)
+//   db2[co]          = g[co] * sum_t m[t][co]
+//   dh1[t][ci]       = sum_{co,k} m[t-k+2][co] * (g[co] w2[co][ci][k])   (g folded into the B operand)
+// so the M MFMAs of waves 1.. run concurrently with the head on wave 0, and every MFMA operand that
+// carries activation gradients is the exact 0/1 mask.
 template <int WAVES, int MODE>
 __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     const float* __restrict__ X, int L, long ldx,        // dataset windows [N, ldx], window length L
@@ -94,7 +135,8 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     const int* __restrict__ Y,                           // [N] int32 labels (unused in MODE 1)
     const float* __restrict__ params, int nc,            // flat fp32 params
     float* __restrict__ out, int out_stride,             // MODE0: slab [B][out_stride]; MODE1: logits
-    float inv_B, unsigned long long* __restrict__ stamps) {  // stamps: diagnostic phase clock (nullptr = off)
+    float inv_B, unsigned long long* __restrict__ stamps,   // stamps: diagnostic phase clock (nullptr = off)
+    FusedOpt opt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const Smem sm = make_smem(L, WAVES, nc);
   const Layout lay = make_layout(nc);
@@ -102,8 +144,8 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
   const int NP = Lp / 32;  // tile pairs (32 time steps each)
 
   float* xs = reinterpret_cast<float*>(smem + sm.xs_off);
-  __bf16* h1s = reinterpret_cast<__bf16*>(smem + sm.h1_off);    // row (t+2), 16 channels
-  __bf16* dh2s = reinterpret_cast<__bf16*>(smem + sm.dh2_off);  // row (t+4), 16 channels
+  __bf16* h1s = reinterpret_cast<__bf16*>(smem + sm.h1_off);    // row (t+2): h1[t][ci]
+  __bf16* ms = reinterpret_cast<__bf16*>(smem + sm.dh2_off);    // row (t+4): m[t][co] = relu'(h2) in {0,1}
   float* ps = reinterpret_cast<float*>(smem + sm.ps_off);       // fp32 copy of the flat params
   __bf16* fragF = reinterpret_cast<__bf16*>(smem + sm.frag_off); // [3][64][8] conv2 fwd B operand
   __bf16* fragD = fragF + 3 * 64 * 8;                            // [3][64][8] conv2 dgrad B operand
@@ -121,8 +163,18 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
   ECG_STAMP(0)
 
   // ---------------- phase 0: stage params + x into LDS, zero halos ------------------------------
-  // params: coalesced 16-B loads of the whole (tiny) parameter vector; every later weight access is LDS.
+  int ylab = 0;
   {
+    const long row = idx ? (long)idx[b] : (long)b;
+    if (MODE == 0) ylab = Y[row];  // label prefetched with the window (used by the head)
+    const float* xrow = X + row * ldx;
+    for (int i = tid; i < Lp + 16; i += WAVES * 64) {
+      const int t = i - 3;
+      xs[i] = (t >= 0 && t < L) ? xrow[t] : 0.f;
+    }
+  }
+  {
+    // params: coalesced 16-B loads of the whole (tiny) parameter vector; every later weight access is LDS.
     const int P4 = lay.P >> 2;
     for (int i = tid; i < P4; i += WAVES * 64)
       reinterpret_cast<float4*>(ps)[i] = reinterpret_cast<const float4*>(params)[i];
@@ -143,33 +195,23 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
       (which ? fragD : fragF)[(2 * 64 + l) * 8 + j] = ecg::to_bf16(0.f);
     }
   }
-  int ylab = 0;
   {
-    const long row = idx ? (long)idx[b] : (long)b;
-    if (MODE == 0) ylab = Y[row];  // label prefetched with the window (used by the head)
-    const float* xrow = X + row * ldx;
-    for (int i = tid; i < Lp + 16; i += WAVES * 64) {
-      const int t = i - 3;
-      xs[i] = (t >= 0 && t < L) ? xrow[t] : 0.f;
-    }
-  }
-  {
-    // h1 halo rows: index 0,1 (t=-2,-1) and [Lp+2, Lp+8) ; dh2 halo rows: [0,4) and [Lp+4, Lp+8)
+    // h1 halo rows: index 0,1 (t=-2,-1) and [Lp+2, Lp+8) ; mask halo rows: [0,4) and [Lp+4, Lp+8)
     uint32_t* h1w = reinterpret_cast<uint32_t*>(h1s);
-    uint32_t* dhw = reinterpret_cast<uint32_t*>(dh2s);
+    uint32_t* mw = reinterpret_cast<uint32_t*>(ms);
     for (int i = tid; i < 8 * 8; i += WAVES * 64) {  // 8 rows x 8 dwords each
       const int r = i >> 3, d = i & 7;
       const int hr = r < 2 ? r : Lp + 2 + (r - 2);
       h1w[hr * 8 + d] = 0u;
       const int dr = r < 4 ? r : Lp + 4 + (r - 4);
-      dhw[dr * 8 + d] = 0u;
+      mw[dr * 8 + d] = 0u;
     }
   }
   __syncthreads();
   ECG_STAMP(1)
 
   // ---------------- phase 1: conv1 + bias + ReLU (VALU) into h1s (bf16) ------------------------
-  uint32_t mask1 = 0u, mask2 = 0u;
+  uint32_t mask1 = 0u;
   {
     float w1r[K1];
 #pragma unroll
@@ -182,9 +224,12 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
           const int t0 = 32 * pair + 16 * half + 4 * h;
-          float xw[4 + K1 - 1];
+          float xw[12];
 #pragma unroll
-          for (int e = 0; e < 4 + K1 - 1; ++e) xw[e] = xs[t0 + e];
+          for (int q4 = 0; q4 < 3; ++q4) {
+            const float4 v = reinterpret_cast<const float4*>(xs + t0)[q4];
+            xw[4 * q4] = v.x; xw[4 * q4 + 1] = v.y; xw[4 * q4 + 2] = v.z; xw[4 * q4 + 3] = v.w;
+          }
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int t = t0 + i;
@@ -203,13 +248,14 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
   __syncthreads();
   ECG_STAMP(2)
 
-  // ---------------- phase 2: conv2 (MFMA) + bias + ReLU, mean-pool partials ---------------------
+  // ---------------- phase 2: conv2 (MFMA) + bias + ReLU -> pool partials, mask m -> LDS ---------
   {
     bf16x8 Bf[3];
 #pragma unroll
     for (int s = 0; s < 3; ++s) Bf[s] = *reinterpret_cast<const bf16x8*>(fragF + (s * 64 + lane) * 8);
     const float b2r = ps[lay.b2 + c];
-    float pool = 0.f;
+    float pool = 0.f, cnt = 0.f;
+    const __bf16 one = ecg::to_bf16(1.f), zero = ecg::to_bf16(0.f);
 #pragma unroll
     for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
       const int pair = w + pi * WAVES;
@@ -231,18 +277,24 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
             float v = fmaxf(acc[i] + b2r, 0.f);
             if (t >= L) v = 0.f;
             pool += v;
-            mask2 |= (v > 0.f ? 1u : 0u) << (pi * 8 + half * 4 + i);
+            const bool on = v > 0.f;
+            cnt += on ? 1.f : 0.f;
+            ms[(t + 4) * C + c] = on ? one : zero;
           }
         }
       }
     }
     pool = ecg::quarter_sum(pool);
-    if (lane < 16) red[RED_POOL + w * 16 + lane] = pool;
+    cnt = ecg::quarter_sum(cnt);
+    if (lane < 16) {
+      red[RED_POOL + w * 16 + lane] = pool;
+      red[red_cnt(WAVES) + w * 16 + lane] = cnt;
+    }
   }
   __syncthreads();
   ECG_STAMP(3)
 
-  // ---------------- head: pooled -> logits -> CE -> dlogits, dWh, dbh, dpooled ----------------
+  // ---------------- phase 3: wave 0 = head;  waves 1.. = M (mask-weighted conv2 wgrad, MFMA) ------
   if (w == 0) {
     if (lane < 16) {
       float pooled = 0.f;
@@ -279,76 +331,59 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
       const float logit_y = __shfl(logit, (lane & 48) + y, 64);
       const float loss = m + __logf(ssum) - logit_y;
       const float dlogit = (n < nc) ? (e / ssum - (n == y ? 1.f : 0.f)) * inv_B : 0.f;
-      float* srow = out + (long)b * out_stride;
+      float* hg = red + red_head(WAVES);  // [wh, P] of this sample's row, stored with the rest in phase 5
       if (lane < nc) {
 #pragma unroll
-        for (int co = 0; co < C; ++co) srow[lay.wh + n * C + co] = dlogit * pv[co];
-        srow[lay.bh + n] = dlogit;
+        for (int co = 0; co < C; ++co) hg[n * C + co] = dlogit * pv[co];
+        hg[nc * C + n] = dlogit;
       }
-      if (lane == 0) srow[lay.P] = loss;
+      if (lane == 0) hg[nc * C + nc] = loss;
       // dpooled[co] = sum_n dlogit[n] * Wh[n][co]; lane co (< 16)
       float dp = 0.f;
       for (int nn = 0; nn < nc; ++nn) dp = fmaf(__shfl(dlogit, nn, 64), ps[lay.wh + nn * C + c], dp);
       if (lane < 16) red[RED_G + c] = dp * (1.0f / (float)L);
     }
+  } else if (MODE == 0 && w <= 5 * msplit(WAVES)) {
+    // work item (tap k, pair range part): M_k[co][ci] = sum_t m[t][co] * h1[t+k-2][ci]
+    constexpr int S = msplit(WAVES);
+    const int item = w - 1, k = item / S, part = item % S;
+    const int per = (NP + S - 1) / S;
+    const int p0 = part * per, p1 = p0 + per < NP ? p0 + per : NP;
+    const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int pair = p0; pair < p1; ++pair) {
+      const int ta = 32 * pair + 8 * h + q;  // time of row q of this lane-quarter's first 4x16 block
+      // A[co][t] (lane: co = l&15, t = 32*pair + 8h + j): transposing reads of the [t][co] mask image
+      const bf16x8 A = cat44(lds_tr16(ms + (ta + 4) * C + p4), lds_tr16(ms + (ta + 4 + 4) * C + p4));
+      // B[t][ci] = h1[t + k - 2][ci]
+      const bf16x8 Bm = cat44(lds_tr16(h1s + (ta + k - 2 + 2) * C + p4), lds_tr16(h1s + (ta + k - 2 + 4 + 2) * C + p4));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bm, acc, 0, 0, 0);
+    }
+    // acc[i] = M_k[co = 4h+i][ci = c]
+    float* pm = red + red_m(WAVES) + part * 1280;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pm[(4 * h + i) * (C * K2) + c * K2 + k] = acc[i];
   }
   if (MODE == 1) return;
   __syncthreads();
   ECG_STAMP(4)
 
-  // ---------------- phase 3: dh2 (= g * relu'), db2, conv2 wgrad (MFMA) ------------------------
+  // ---------------- phase 4: conv2 dgrad (MFMA, A = mask, B = g-scaled w2) * relu'(h1), conv1 wgrad
   {
-    const float g = red[RED_G + c];
-    float db2 = 0.f;
-    f32x4 accW[K2];
+    // B[r][ci] = g[co] * w2[co][ci][k], r = 32s + 8h + j -> k = r>>4, co = r&15 = 8(h&1) + j
+    float gq[8];
 #pragma unroll
-    for (int k = 0; k < K2; ++k) accW[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
-      const int pair = w + pi * WAVES;
-      if (pair < NP) {
-        bf16x8 Adh;  // A[co][t] in the permuted k-order of the forward C layout
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int t = 32 * pair + 16 * half + 4 * h + i;
-            const bool on = (mask2 >> (pi * 8 + half * 4 + i)) & 1u;
-            const float d = on ? g : 0.f;
-            const __bf16 db = ecg::to_bf16(d);
-            dh2s[(t + 4) * C + c] = db;
-            db2 += d;
-            Adh[half * 4 + i] = db;
-          }
-        }
-        const int t0 = 32 * pair;
-        const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
-#pragma unroll
-        for (int k = 0; k < K2; ++k) {
-          const int ra = t0 + 4 * h + k - 2 + q;  // h1 time index of row q of the first 4x16 block
-          const s16x4 lo = lds_tr16(h1s + (ra + 2) * C + p4);
-          const s16x4 hi = lds_tr16(h1s + (ra + 16 + 2) * C + p4);
-          accW[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Adh, cat44(lo, hi), accW[k], 0, 0, 0);
-        }
-      }
+    for (int q2 = 0; q2 < 2; ++q2) {
+      const float4 v = reinterpret_cast<const float4*>(red + RED_G + 8 * (h & 1))[q2];
+      gq[4 * q2] = v.x; gq[4 * q2 + 1] = v.y; gq[4 * q2 + 2] = v.z; gq[4 * q2 + 3] = v.w;
     }
-    // this wave's partial dW2[co = 4h+i][ci = c][k] -> its own LDS slot (summed over waves later)
-    float* pw = red + red_dw2(WAVES) + w * 1280;
-#pragma unroll
-    for (int k = 0; k < K2; ++k)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) pw[(4 * h + i) * (C * K2) + c * K2 + k] = accW[k][i];
-    db2 = ecg::quarter_sum(db2);
-    if (lane < 16) red[red_db2(WAVES) + w * 16 + c] = db2;
-  }
-  __syncthreads();
-  ECG_STAMP(5)
-
-  // ---------------- phase 4: conv2 dgrad (MFMA) * relu'(h1), conv1 wgrad (VALU) ---------------
-  {
     bf16x8 Bd[3];
 #pragma unroll
-    for (int s = 0; s < 3; ++s) Bd[s] = *reinterpret_cast<const bf16x8*>(fragD + (s * 64 + lane) * 8);
+    for (int s = 0; s < 3; ++s) {
+      const bf16x8 raw = *reinterpret_cast<const bf16x8*>(fragD + (s * 64 + lane) * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Bd[s][j] = ecg::to_bf16(ecg::from_bf16(raw[j]) * gq[j]);
+    }
     float dw1[K1 + 1];
 #pragma unroll
     for (int k = 0; k <= K1; ++k) dw1[k] = 0.f;
@@ -363,14 +398,17 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
 #pragma unroll
           for (int s = 0; s < 3; ++s) {
             const int k = 2 * s + (h >> 1);
-            const int r = t0 + (lane & 15) - k + 2;  // dh2 time index
-            const bf16x8 A = *reinterpret_cast<const bf16x8*>(dh2s + (r + 4) * C + 8 * (h & 1));
+            const int r = t0 + (lane & 15) - k + 2;  // mask time index
+            const bf16x8 A = *reinterpret_cast<const bf16x8*>(ms + (r + 4) * C + 8 * (h & 1));
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bd[s], acc, 0, 0, 0);
           }
           const int tb = t0 + 4 * h;
-          float xw[4 + K1 - 1];
+          float xw[12];
 #pragma unroll
-          for (int e = 0; e < 4 + K1 - 1; ++e) xw[e] = xs[tb + e];
+          for (int q4 = 0; q4 < 3; ++q4) {
+            const float4 v = reinterpret_cast<const float4*>(xs + tb)[q4];
+            xw[4 * q4] = v.x; xw[4 * q4 + 1] = v.y; xw[4 * q4 + 2] = v.z; xw[4 * q4 + 3] = v.w;
+          }
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const bool on = (mask1 >> (pi * 8 + half * 4 + i)) & 1u;
@@ -389,13 +427,16 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     }
   }
   __syncthreads();
-  ECG_STAMP(6)
+  ECG_STAMP(5)
 
-  // ---------------- phase 5: sum the per-wave partials, write this sample's gradient row -------
-  float* srow = out + (long)b * out_stride;
-  for (int i = tid; i < lay.wh; i += WAVES * 64) {
+  // ---------------- phase 5: combine partials, scale by g, write this sample's gradient row -----
+  const __amdgpu_buffer_rsrc_t slab_r = make_rsrc(out, (long)gridDim.x * out_stride * 4);
+  const int rowbase = b * out_stride;
+  for (int i = tid; i <= lay.P; i += WAVES * 64) {
     float v = 0.f;
-    if (i < lay.b1) {
+    if (i >= lay.wh) {
+      v = red[red_head(WAVES) + (i - lay.wh)];
+    } else if (i < lay.b1) {
       const int o = red_dw1(WAVES) + (i / K1) * 8 + (i % K1);
 #pragma unroll
       for (int ww = 0; ww < WAVES; ++ww) v += red[o + ww * 128];
@@ -404,18 +445,120 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
 #pragma unroll
       for (int ww = 0; ww < WAVES; ++ww) v += red[o + ww * 128];
     } else if (i < lay.b2) {
-      const int o = red_dw2(WAVES) + (i - lay.w2);
+      const int e = i - lay.w2;
 #pragma unroll
-      for (int ww = 0; ww < WAVES; ++ww) v += red[o + ww * 1280];
+      for (int part = 0; part < msplit(WAVES); ++part) v += red[red_m(WAVES) + part * 1280 + e];
+      v *= red[RED_G + e / (C * K2)];
     } else {
-      const int o = red_db2(WAVES) + (i - lay.b2);
+      const int co = i - lay.b2;
 #pragma unroll
-      for (int ww = 0; ww < WAVES; ++ww) v += red[o + ww * 16];
+      for (int ww = 0; ww < WAVES; ++ww) v += red[red_cnt(WAVES) + ww * 16 + co];
+      v *= red[RED_G + co];
     }
-    srow[i] = v;
+    st_wt(slab_r, rowbase + i, v);
   }
-  ECG_STAMP(7)
+  ECG_STAMP(6)
   if (stamps && tid == 0) stamps[(long)b * 16 + 14] = __builtin_amdgcn_s_memrealtime();
+  if (opt.ctl != nullptr) {
+    // ---------------- phase 6: two-level deterministic cross-sample reduction + SGD --------------
+    int* flag = reinterpret_cast<int*>(red + RED_FLAG);
+    const int G = opt.G;
+    const int NG = G < kMaxGroups ? G : kMaxGroups;
+    const int g = b % NG;
+    const int members = (G - 1 - g) / NG + 1;  // rows b' < G with b' % NG == g
+    const int ncols = lay.P + 1;               // gradient + loss column
+    // Hand-off protocol (guide Guideline 16, R1 form): rows are stored write-through (sc1) by every
+    // wave and drained (vmcnt(0)) before the barrier; ONE lane then takes a relaxed agent-scope ticket.
+    // Reducers read the handed-off rows ONLY with sc1 loads, so neither a release nor an acquire fence
+    // (each ~1-2 us at agent scope) is needed.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const int t = __hip_atomic_fetch_add(&opt.ctl[g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = (t == members - 1);
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    // group reducer: sum the group's rows in a fixed order (bitwise reproducible)
+    const __amdgpu_buffer_rsrc_t g_r = make_rsrc(opt.gslab, (long)kMaxGroups * out_stride * 4);
+    // (no per-element "load or zero" selects inside the unrolled block: hipcc would serialise them)
+    constexpr int NT = WAVES * 64;
+    constexpr int CPT = (1 + C * K1 + C + C * C * K2 + C + MAX_CLASSES * C + MAX_CLASSES + NT - 1) / NT;
+    if (members == 16) {
+      // fast path (B = 256): every thread issues all CPT x 16 row loads before the first add -> one round trip
+      float v[CPT][16];
+#pragma unroll
+      for (int cc = 0; cc < CPT; ++cc) {
+        const int col = min(tid + cc * NT, ncols - 1);  // clamped: no branches around the loads
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[cc][u] = ld_wt(slab_r, (g + u * NG) * out_stride + col);
+      }
+#pragma unroll
+      for (int cc = 0; cc < CPT; ++cc) {
+        float sum = 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; u += 2) sum += v[cc][u] + v[cc][u + 1];
+        if (tid + cc * NT < ncols) st_wt(g_r, g * out_stride + tid + cc * NT, sum);
+      }
+    }
+    for (int i = members == 16 ? ncols : tid; i < ncols; i += WAVES * 64) {
+      float sum = 0.f;
+      int m = 0;
+      for (; m + 8 <= members; m += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = ld_wt(slab_r, (g + (m + u) * NG) * out_stride + i);
+        sum += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+      }
+      for (; m < members; ++m) sum += ld_wt(slab_r, (g + m * NG) * out_stride + i);
+      st_wt(g_r, g * out_stride + i, sum);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const int t = __hip_atomic_fetch_add(&opt.ctl[kMaxGroups], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[1] = (t == NG - 1);
+    }
+    __syncthreads();
+    if (!flag[1]) return;
+    // final reducer: sum the NG group rows, SGD(+momentum) on the flat master weights, reset counters
+    float gv[CPT][kMaxGroups];
+    if (NG == kMaxGroups) {
+#pragma unroll
+      for (int cc = 0; cc < CPT; ++cc) {
+        const int col = min(tid + cc * NT, ncols - 1);
+#pragma unroll
+        for (int u = 0; u < kMaxGroups; ++u) gv[cc][u] = ld_wt(g_r, u * out_stride + col);
+      }
+    }
+#pragma unroll
+    for (int cc = 0; cc < CPT; ++cc) {
+      const int i = tid + cc * NT;
+      if (i >= ncols) continue;
+      float sum = 0.f;
+      if (NG == kMaxGroups) {
+#pragma unroll
+        for (int u = 0; u < kMaxGroups; u += 2) sum += gv[cc][u] + gv[cc][u + 1];
+      } else {
+        for (int m = 0; m < NG; ++m) sum += ld_wt(g_r, m * out_stride + i);
+      }
+      if (i == lay.P) {
+        if (opt.loss_acc) opt.loss_acc[0] += sum;
+      } else {
+        const float p = opt.params[i];
+        float d = sum + opt.wd * p;
+        if (opt.momentum != 0.f) {
+          const float bm = opt.momentum * opt.mom[i] + d;
+          opt.mom[i] = bm;
+          d = opt.nesterov ? d + opt.momentum * bm : bm;
+        }
+        opt.params[i] = p - opt.lr * d;
+      }
+    }
+    if (tid <= kMaxGroups) __hip_atomic_store(&opt.ctl[tid], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ECG_STAMP(7)
+    if (stamps && tid == 0) stamps[(long)b * 16 + 13] = __builtin_amdgcn_s_memrealtime();
+  }
 #undef ECG_STAMP
 }
 
@@ -474,13 +617,13 @@ unsigned long long* g_stamps = nullptr;  // diagnostic phase stamps (ecg_tiny_se
 
 template <int WAVES, int MODE>
 int launch_step(const float* X, int L, long ldx, const int* idx, const int* Y, const float* params, int nc,
-                float* out, int out_stride, int B, float inv_B, hipStream_t stream) {
+                float* out, int out_stride, int B, float inv_B, const FusedOpt& opt, hipStream_t stream) {
   const Smem sm = make_smem(L, WAVES, nc);
   auto kern = tiny_ecg_step_kernel<WAVES, MODE>;
   if (sm.bytes > 64 * 1024)
     ECG_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, sm.bytes));
   hipLaunchKernelGGL(kern, dim3(B), dim3(WAVES * 64), sm.bytes, stream, X, L, ldx, idx, Y, params, nc, out,
-                     out_stride, inv_B, g_stamps);
+                     out_stride, inv_B, g_stamps, opt);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
@@ -513,15 +656,21 @@ int check_step_args(int L, int nc, int B, int out_stride, int mode) {
 }
 
 int step_dispatch(int mode, const float* X, int L, long ldx, const int* idx, const int* Y, const float* params,
-                  int nc, float* out, int out_stride, int B, float inv_B, hipStream_t stream) {
+                  int nc, float* out, int out_stride, int B, float inv_B, const FusedOpt& opt, hipStream_t stream) {
   int st = check_step_args(L, nc, B, out_stride, mode);
   if (st) return st;
+  if (opt.ctl && (!opt.gslab || !opt.params || (opt.momentum != 0.f && !opt.mom) || opt.G != B)) return ecg::kBadArg;
   const int waves = pick_waves(L);
   if (mode == 0)
-    return waves == 8 ? launch_step<8, 0>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, stream)
-                      : launch_step<16, 0>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, stream);
-  return waves == 8 ? launch_step<8, 1>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, stream)
-                    : launch_step<16, 1>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, stream);
+    return waves == 8 ? launch_step<8, 0>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream)
+                      : launch_step<16, 0>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream);
+  return waves == 8 ? launch_step<8, 1>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream)
+                    : launch_step<16, 1>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream);
+}
+
+FusedOpt no_fuse() {
+  FusedOpt o{};
+  return o;
 }
 
 int reduce_dispatch(const float* slab, int G, int stride, int P, float* params, float* mom, float* grad_out,
@@ -560,14 +709,19 @@ ECG_API int ecg_tiny_smem_bytes(int L) { return make_smem(L, pick_waves(L)).byte
 ECG_API int ecg_tiny_step_grads(const float* X, int L, long ldx, const int* idx, const int* Y,
                                 const float* params, int nc, float* slab, int slab_stride, int B, float inv_B,
                                 hipStream_t stream) {
-  return step_dispatch(0, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, inv_B, stream);
+  return step_dispatch(0, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, inv_B, no_fuse(), stream);
 }
 
 // Inference: logits[B][nc] for windows X[idx[b]].
 ECG_API int ecg_tiny_forward(const float* X, int L, long ldx, const int* idx, const float* params, int nc,
                              float* logits, int B, hipStream_t stream) {
-  return step_dispatch(1, X, L, ldx, idx, nullptr, params, nc, logits, nc, B, 0.f, stream);
+  return step_dispatch(1, X, L, ldx, idx, nullptr, params, nc, logits, nc, B, 0.f, no_fuse(), stream);
 }
+
+// Size of the control block (int32 counters, must be zero before the first fused step) and of the
+// group-partial buffer (floats) needed by the single-launch step.
+ECG_API int ecg_tiny_ctl_ints(void) { return kMaxGroups + 1; }
+ECG_API int ecg_tiny_gslab_rows(void) { return kMaxGroups; }
 
 ECG_API int ecg_slab_reduce_sgd(const float* slab, int G, int stride, int P, float* params, float* mom,
                                 float* grad_out, float* loss_acc, float lr, float momentum, float wd, int nesterov,
@@ -576,11 +730,17 @@ ECG_API int ecg_slab_reduce_sgd(const float* slab, int G, int stride, int P, flo
                          stream);
 }
 
-// Full step = grads + reduce/SGD (two launches on ``stream``).
+// Full training step.  With ``ctl``/``gslab`` (see ecg_tiny_ctl_ints) it is ONE launch: per-sample
+// gradients, the in-kernel deterministic reduction tree and SGD.  Without them it is two launches
+// (gradient slab, then slab_reduce_sgd_kernel).
 ECG_API int ecg_tiny_train_step(const float* X, int L, long ldx, const int* idx, const int* Y, float* params,
                                 float* mom, int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr,
-                                float momentum, float wd, int nesterov, hipStream_t stream) {
-  int st = step_dispatch(0, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, stream);
+                                float momentum, float wd, int nesterov, int* ctl, float* gslab, hipStream_t stream) {
+  if (ctl) {
+    FusedOpt o{ctl, gslab, params, mom, loss_acc, lr, momentum, wd, nesterov, B};
+    return step_dispatch(0, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, o, stream);
+  }
+  int st = step_dispatch(0, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, no_fuse(), stream);
   if (st) return st;
   return reduce_dispatch(slab, B, slab_stride, make_layout(nc).P, params, mom, nullptr, loss_acc, lr, momentum, wd,
                          nesterov, 1, stream);
@@ -591,7 +751,7 @@ ECG_API int ecg_tiny_train_step(const float* X, int L, long ldx, const int* idx,
 ECG_API int ecg_round_graph_create(void** handle, const float* X, int L, long ldx, const int* idx_table,
                                    const int* Y, float* params, float* mom, int nc, float* slab, int slab_stride,
                                    int B, int steps, float* loss_acc, float lr, float momentum, float wd,
-                                   int nesterov) {
+                                   int nesterov, int* ctl, float* gslab) {
   if (!handle || steps <= 0) return ecg::kBadArg;
   int st = check_step_args(L, nc, B, slab_stride, 0);
   if (st) return st;
@@ -607,7 +767,7 @@ ECG_API int ecg_round_graph_create(void** handle, const float* X, int L, long ld
   }
   for (int s = 0; s < steps && st == 0; ++s)
     st = ecg_tiny_train_step(X, L, ldx, idx_table + (long)s * B, Y, params, mom, nc, slab, slab_stride, B, loss_acc,
-                             lr, momentum, wd, nesterov, cap);
+                             lr, momentum, wd, nesterov, ctl, gslab, cap);
   e = hipStreamEndCapture(cap, &rg->graph);
   (void)hipStreamDestroy(cap);
   if (st != 0 || e != hipSuccess) {
