@@ -61,14 +61,14 @@ def _sig(lib, name, argtypes, restype=i32):
 
 def _bind_kernels(lib: C.CDLL) -> None:
     _sig(lib, "ecg_tiny_param_count", [i32])
-    _sig(lib, "ecg_tiny_smem_bytes", [i32])
-    _sig(lib, "ecg_tiny_step_grads", [vp, i32, i64, vp, vp, vp, i32, vp, i32, i32, f32, vp])
-    _sig(lib, "ecg_tiny_forward", [vp, i32, i64, vp, vp, i32, vp, i32, vp])
+    _sig(lib, "ecg_tiny_smem_bytes", [i32, i32])
+    _sig(lib, "ecg_tiny_step_grads", [vp, i32, i64, vp, vp, vp, i32, vp, i32, i32, f32, i32, vp])
+    _sig(lib, "ecg_tiny_forward", [vp, i32, i64, vp, vp, i32, vp, i32, i32, vp])
     _sig(lib, "ecg_slab_reduce_sgd", [vp, i32, i32, i32, vp, vp, vp, vp, f32, f32, f32, i32, i32, vp])
     _sig(lib, "ecg_tiny_train_step", [vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, vp, f32, f32, f32, i32,
-                                      vp, vp, vp])
+                                      vp, vp, i32, vp])
     _sig(lib, "ecg_round_graph_create", [C.POINTER(vp), vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, i32, vp,
-                                         f32, f32, f32, i32, vp, vp])
+                                         f32, f32, f32, i32, vp, vp, i32])
     _sig(lib, "ecg_tiny_ctl_ints", [])
     _sig(lib, "ecg_tiny_gslab_rows", [])
     _sig(lib, "ecg_tiny_set_stamps", [vp])

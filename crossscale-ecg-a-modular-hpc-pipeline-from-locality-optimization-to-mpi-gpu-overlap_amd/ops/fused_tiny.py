@@ -22,6 +22,15 @@ from ..models.tiny_ecg import TinyECG, num_params
 from ..data.dataset import DeviceIndexSampler
 
 
+PRECISION = {"bf16": 0, "fp32": 1}
+
+
+def prec_id(precision: str) -> int:
+    if precision not in PRECISION:
+        raise ValueError(f"precision must be one of {list(PRECISION)}, got {precision!r}")
+    return PRECISION[precision]
+
+
 def slab_stride(num_classes: int) -> int:
     return (num_params(num_classes) + 1 + 63) // 64 * 64
 
@@ -50,7 +59,7 @@ def labels_int32(y: torch.Tensor, num_classes: int) -> torch.Tensor:
 
 
 def tiny_forward(flat_params: torch.Tensor, x: torch.Tensor, idx: Optional[torch.Tensor], batch: int,
-                 num_classes: int = 2) -> torch.Tensor:
+                 num_classes: int = 2, precision: str = "bf16") -> torch.Tensor:
     """Logits [batch, C] of TinyECG for windows ``x[idx[b]]`` (or ``x[b]`` when idx is None)."""
     _check_dataset(x, None, num_classes)
     if idx is not None:
@@ -60,13 +69,14 @@ def tiny_forward(flat_params: torch.Tensor, x: torch.Tensor, idx: Optional[torch
     out = torch.empty((batch, num_classes), dtype=torch.float32, device=x.device)
     lib = _lib.kernels()
     st = lib.ecg_tiny_forward(x.data_ptr(), x.shape[1], x.stride(0), _lib.ptr(idx), flat_params.data_ptr(),
-                              num_classes, out.data_ptr(), batch, _lib.stream_ptr(x.device))
+                              num_classes, out.data_ptr(), batch, prec_id(precision), _lib.stream_ptr(x.device))
     _lib.check(st, "ecg_tiny_forward")
     return out
 
 
 def tiny_step_grads(flat_params: torch.Tensor, x: torch.Tensor, y32: torch.Tensor, idx: Optional[torch.Tensor],
-                    batch: int, num_classes: int = 2, slab: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    batch: int, num_classes: int = 2, slab: Optional[torch.Tensor] = None,
+                    precision: str = "bf16") -> torch.Tensor:
     """Per-sample gradient slab [batch, stride] (loss in column P) of one fused step (no update)."""
     _check_dataset(x, y32, num_classes)
     if idx is not None:
@@ -77,7 +87,7 @@ def tiny_step_grads(flat_params: torch.Tensor, x: torch.Tensor, y32: torch.Tenso
     lib = _lib.kernels()
     st = lib.ecg_tiny_step_grads(x.data_ptr(), x.shape[1], x.stride(0), _lib.ptr(idx), y32.data_ptr(),
                                  flat_params.data_ptr(), num_classes, slab.data_ptr(), stride, batch,
-                                 1.0 / batch, _lib.stream_ptr(x.device))
+                                 1.0 / batch, prec_id(precision), _lib.stream_ptr(x.device))
     _lib.check(st, "ecg_tiny_step_grads")
     return slab
 
@@ -104,8 +114,10 @@ class FusedTinyTrainer:
     def __init__(self, model: TinyECG, x_gpu: torch.Tensor, y_gpu: torch.Tensor, batch_size: int,
                  steps_per_round: int, lr: float = 1e-2, momentum: float = 0.9, weight_decay: float = 0.0,
                  nesterov: bool = False, seed: Optional[int] = None, use_graph: bool = True,
-                 single_launch: bool = False):
+                 single_launch: bool = False, precision: str = "bf16"):
         self.device = x_gpu.device
+        self.precision = precision
+        self.prec = prec_id(precision)
         self.model = model
         self.nc = model.num_classes
         self.params = model.flat if model.flat is not None else model.flatten_parameters()
@@ -134,7 +146,7 @@ class FusedTinyTrainer:
         self.single_launch = bool(single_launch)
         self.ctl = torch.zeros(lib.ecg_tiny_ctl_ints(), dtype=torch.int32, device=self.device)
         self.gslab = torch.empty((lib.ecg_tiny_gslab_rows(), self.stride), dtype=torch.float32, device=self.device)
-        smem = lib.ecg_tiny_smem_bytes(self.x.shape[1])
+        smem = lib.ecg_tiny_smem_bytes(self.x.shape[1], self.prec)
         if smem > 160 * 1024:
             raise ValueError(f"window length {self.x.shape[1]} too long for the fused kernel ({smem} B LDS)")
 
@@ -150,7 +162,7 @@ class FusedTinyTrainer:
                                         self.idx_table.data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
                                         self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
                                         n, self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd,
-                                        int(self.nesterov), *self._fuse_ptrs())
+                                        int(self.nesterov), *self._fuse_ptrs(), self.prec)
         _lib.check(st, "ecg_round_graph_create")
         self._graphs[n] = g
         return g
@@ -177,7 +189,7 @@ class FusedTinyTrainer:
                                      self.idx_table[s].data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
                                      self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
                                      self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd, int(self.nesterov),
-                                     *self._fuse_ptrs(), _lib.stream_ptr(self.device))
+                                     *self._fuse_ptrs(), self.prec, _lib.stream_ptr(self.device))
         _lib.check(st, "ecg_tiny_train_step")
 
     def run_round(self, n_steps: Optional[int] = None, reset_loss: bool = True) -> None:

@@ -82,8 +82,9 @@ def make_trainer(cfg: FedAvgConfig, config_name: str, model, x, y, ctx: DistCont
     seed = cfg.seed + 7919 * ctx.rank
     if backend == "fused":
         from ..ops.fused_tiny import FusedTinyTrainer
+        prec = "bf16" if (config_name == "G1" and cfg.amp_dtype == "bf16") else "fp32"
         return FusedTinyTrainer(model, x, y, cfg.batch_size, cfg.local_steps, lr=cfg.lr, momentum=cfg.momentum,
-                                seed=seed)
+                                seed=seed, precision=prec)
     amp = None if config_name == "G0" else _amp(cfg)
     net = model
     if cfg.sync == "ddp" and ctx.distributed:
@@ -99,10 +100,12 @@ def dev_index(ctx):
 def pick_backend(cfg: FedAvgConfig, config_name: str, ctx: DistContext) -> str:
     if cfg.kernel_backend == "torch" or ctx.device.type != "cuda":
         return "torch"
-    fused_ok = (config_name == "G1" and cfg.amp_dtype == "bf16" and cfg.model == "tiny_ecg")
+    # fused HIP step: TinyECG in fp32 (G0, or G1 with --amp-dtype none) or bf16 AMP (G1); fp16 AMP keeps the
+    # reference's GradScaler path on eager PyTorch
+    fused_ok = cfg.model == "tiny_ecg" and (config_name == "G0" or cfg.amp_dtype in ("bf16", "none"))
     if cfg.kernel_backend == "fused":
         if not fused_ok:
-            raise ValueError("the fused HIP step implements TinyECG with bf16 AMP (config G1, --amp-dtype bf16)")
+            raise ValueError("the fused HIP step implements TinyECG in fp32 or bf16 (not --amp-dtype fp16)")
         return "fused"
     return "fused" if fused_ok else "torch"
 
@@ -122,7 +125,7 @@ def _ddp_fused_round(trainer, ctx: DistContext, n: int):
     lib = _lib.kernels()
     for s in range(n):
         tiny_step_grads(trainer.params, trainer.x, trainer.y32, trainer.idx_table[s], trainer.B, trainer.nc,
-                        trainer.slab)
+                        trainer.slab, precision=trainer.precision)
         st = lib.ecg_slab_reduce_sgd(trainer.slab.data_ptr(), trainer.B, trainer.stride, trainer.P, None, None,
                                      trainer._ddp_grad.data_ptr(), trainer.loss_acc.data_ptr(), 0.0, 0.0, 0.0, 0, 0,
                                      _lib.stream_ptr(trainer.device))

@@ -17,6 +17,7 @@
 #include "../include/ecg_common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -91,18 +92,22 @@ __device__ __forceinline__ float ld_wt(__amdgpu_buffer_rsrc_t r, int idx) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, idx * 4, 0, 16));
 }
 
-__host__ __device__ inline Smem make_smem(int L, int waves, int nc = MAX_CLASSES) {
+// fp32 path: v_mfma_f32_16x16x4_f32 (exact f32 products, K = 80 = 20 k-steps of 4, no padding)
+constexpr int F32_KSTEPS = C * K2 / 4;
+
+__host__ __device__ inline Smem make_smem(int L, int waves, int nc = MAX_CLASSES, bool f32 = false) {
   Smem s;
   s.Lp = (L + 31) / 32 * 32;
   s.xs_off = 0;
   const int xs_bytes = ((s.Lp + 16) * 4 + 15) / 16 * 16;
   s.h1_off = s.xs_off + xs_bytes;
-  const int act_bytes = (s.Lp + 8) * C * 2;  // bf16 [Lp+8][16]
+  const int act_bytes = (s.Lp + 8) * C * (f32 ? 4 : 2);  // [Lp+8][16] in the activation type
   s.dh2_off = s.h1_off + act_bytes;
   s.ps_off = s.dh2_off + act_bytes;
   const int ps_bytes = ((make_layout(nc).P) * 4 + 15) / 16 * 16;
-  s.frag_off = s.ps_off + ps_bytes;  // bf16 MFMA B fragments of conv2: [2 (fwd, dgrad)][3][64 lanes][8]
-  s.red_off = s.frag_off + 2 * 3 * 64 * 16;
+  // conv2 MFMA B fragments in lane order, fwd + dgrad: bf16 [2][3][64][8] or fp32 [2][20][64]
+  s.frag_off = s.ps_off + ps_bytes;
+  s.red_off = s.frag_off + (f32 ? 2 * F32_KSTEPS * 64 * 4 : 2 * 3 * 64 * 16);
   s.bytes = s.red_off + (red_floats(waves) * 4 + 15) / 16 * 16;
   return s;
 }
@@ -128,7 +133,7 @@ __device__ __forceinline__ s16x4 lds_tr16(const __bf16* p) {
 //   dh1[t][ci]       = sum_{co,k} m[t-k+2][co] * (g[co] w2[co][ci][k])   (g folded into the B operand)
 // so the M MFMAs of waves 1.. run concurrently with the head on wave 0, and every MFMA operand that
 // carries activation gradients is the exact 0/1 mask.
-template <int WAVES, int MODE>
+template <int WAVES, int MODE, bool F32>
 __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     const float* __restrict__ X, int L, long ldx,        // dataset windows [N, ldx], window length L
     const int* __restrict__ idx,                         // [B] rows of X for this step (nullptr: b)
@@ -138,17 +143,20 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     float inv_B, unsigned long long* __restrict__ stamps,   // stamps: diagnostic phase clock (nullptr = off)
     FusedOpt opt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const Smem sm = make_smem(L, WAVES, nc);
+  using AT = std::conditional_t<F32, float, __bf16>;  // activation / MFMA operand type
+  const Smem sm = make_smem(L, WAVES, nc, F32);
   const Layout lay = make_layout(nc);
   const int Lp = sm.Lp;
   const int NP = Lp / 32;  // tile pairs (32 time steps each)
 
   float* xs = reinterpret_cast<float*>(smem + sm.xs_off);
-  __bf16* h1s = reinterpret_cast<__bf16*>(smem + sm.h1_off);    // row (t+2): h1[t][ci]
-  __bf16* ms = reinterpret_cast<__bf16*>(smem + sm.dh2_off);    // row (t+4): m[t][co] = relu'(h2) in {0,1}
+  AT* h1s = reinterpret_cast<AT*>(smem + sm.h1_off);    // row (t+2): h1[t][ci]
+  AT* ms = reinterpret_cast<AT*>(smem + sm.dh2_off);    // row (t+4): m[t][co] = relu'(h2) in {0,1}
   float* ps = reinterpret_cast<float*>(smem + sm.ps_off);       // fp32 copy of the flat params
   __bf16* fragF = reinterpret_cast<__bf16*>(smem + sm.frag_off); // [3][64][8] conv2 fwd B operand
   __bf16* fragD = fragF + 3 * 64 * 8;                            // [3][64][8] conv2 dgrad B operand
+  float* fragF32 = reinterpret_cast<float*>(smem + sm.frag_off);  // fp32 path: [20][64] fwd B operand
+  float* fragD32 = fragF32 + F32_KSTEPS * 64;                     // fp32 path: [20][64] dgrad B operand
   float* red = reinterpret_cast<float*>(smem + sm.red_off);
 
   const int tid = threadIdx.x;
@@ -184,27 +192,36 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     // element (r, col) lives at frag[s = r>>5][lane = 16*((r&31)>>3) + col][j = r&7].
     for (int e = tid; e < C * C * K2; e += WAVES * 64) {
       const int co = e / (C * K2), ci = (e / K2) % C, k = e % K2;
-      const __bf16 v = ecg::to_bf16(params[lay.w2 + e]);
       const int rf = 16 * k + ci, rd = 16 * k + co;
-      fragF[((rf >> 5) * 64 + 16 * ((rf & 31) >> 3) + co) * 8 + (rf & 7)] = v;
-      fragD[((rd >> 5) * 64 + 16 * ((rd & 31) >> 3) + ci) * 8 + (rd & 7)] = v;
+      if constexpr (F32) {
+        // 16x16x4 f32 operand: element (r, col) at frag[s = r>>2][lane = 16*(r&3) + col]
+        const float v = params[lay.w2 + e];
+        fragF32[(rf >> 2) * 64 + 16 * (rf & 3) + co] = v;
+        fragD32[(rd >> 2) * 64 + 16 * (rd & 3) + ci] = v;
+      } else {
+        const __bf16 v = ecg::to_bf16(params[lay.w2 + e]);
+        fragF[((rf >> 5) * 64 + 16 * ((rf & 31) >> 3) + co) * 8 + (rf & 7)] = v;
+        fragD[((rd >> 5) * 64 + 16 * ((rd & 31) >> 3) + ci) * 8 + (rd & 7)] = v;
+      }
     }
-    // r in [80, 96) (the 6th, padding tap) is zero: s = 2, lane quarters 2 and 3
-    for (int e = tid; e < 2 * 32 * 8; e += WAVES * 64) {
-      const int which = e >> 8, l = 32 + ((e >> 3) & 31), j = e & 7;
-      (which ? fragD : fragF)[(2 * 64 + l) * 8 + j] = ecg::to_bf16(0.f);
-    }
+    // bf16: r in [80, 96) (the 6th, padding tap) is zero: s = 2, lane quarters 2 and 3
+    if constexpr (!F32)
+      for (int e = tid; e < 2 * 32 * 8; e += WAVES * 64) {
+        const int which = e >> 8, l = 32 + ((e >> 3) & 31), j = e & 7;
+        (which ? fragD : fragF)[(2 * 64 + l) * 8 + j] = ecg::to_bf16(0.f);
+      }
   }
   {
     // h1 halo rows: index 0,1 (t=-2,-1) and [Lp+2, Lp+8) ; mask halo rows: [0,4) and [Lp+4, Lp+8)
+    constexpr int DW = C * (int)sizeof(AT) / 4;  // dwords per activation row
     uint32_t* h1w = reinterpret_cast<uint32_t*>(h1s);
     uint32_t* mw = reinterpret_cast<uint32_t*>(ms);
-    for (int i = tid; i < 8 * 8; i += WAVES * 64) {  // 8 rows x 8 dwords each
-      const int r = i >> 3, d = i & 7;
+    for (int i = tid; i < 8 * DW; i += WAVES * 64) {  // 8 rows
+      const int r = i / DW, d = i % DW;
       const int hr = r < 2 ? r : Lp + 2 + (r - 2);
-      h1w[hr * 8 + d] = 0u;
+      h1w[hr * DW + d] = 0u;
       const int dr = r < 4 ? r : Lp + 4 + (r - 4);
-      mw[dr * 8 + d] = 0u;
+      mw[dr * DW + d] = 0u;
     }
   }
   __syncthreads();
@@ -237,9 +254,9 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
 #pragma unroll
             for (int k = 0; k < K1; ++k) v = fmaf(w1r[k], xw[i + k], v);
             v = (t < L) ? fmaxf(v, 0.f) : 0.f;
-            const __bf16 vb = ecg::to_bf16(v);
+            const AT vb = (AT)v;
             h1s[(t + 2) * C + c] = vb;
-            mask1 |= (ecg::from_bf16(vb) > 0.f ? 1u : 0u) << (pi * 8 + half * 4 + i);
+            mask1 |= ((float)vb > 0.f ? 1u : 0u) << (pi * 8 + half * 4 + i);
           }
         }
       }
@@ -251,11 +268,16 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
   // ---------------- phase 2: conv2 (MFMA) + bias + ReLU -> pool partials, mask m -> LDS ---------
   {
     bf16x8 Bf[3];
+    float Wf[F32_KSTEPS];
+    if constexpr (F32) {
 #pragma unroll
-    for (int s = 0; s < 3; ++s) Bf[s] = *reinterpret_cast<const bf16x8*>(fragF + (s * 64 + lane) * 8);
+      for (int s = 0; s < F32_KSTEPS; ++s) Wf[s] = fragF32[s * 64 + lane];
+    } else {
+#pragma unroll
+      for (int s = 0; s < 3; ++s) Bf[s] = *reinterpret_cast<const bf16x8*>(fragF + (s * 64 + lane) * 8);
+    }
     const float b2r = ps[lay.b2 + c];
     float pool = 0.f, cnt = 0.f;
-    const __bf16 one = ecg::to_bf16(1.f), zero = ecg::to_bf16(0.f);
 #pragma unroll
     for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
       const int pair = w + pi * WAVES;
@@ -264,12 +286,22 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
         for (int half = 0; half < 2; ++half) {
           const int t0 = 32 * pair + 16 * half;
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (F32) {
+            // 16x16x4 f32: lane holds A[t0 + (l&15)][r = 4s + h], r = 16*tap + ci
 #pragma unroll
-          for (int s = 0; s < 3; ++s) {
-            const int tap = 2 * s + (h >> 1);
-            const int r = t0 + (lane & 15) + tap - 2;  // h1 time index
-            const bf16x8 A = *reinterpret_cast<const bf16x8*>(h1s + (r + 2) * C + 8 * (h & 1));
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bf[s], acc, 0, 0, 0);
+            for (int s = 0; s < F32_KSTEPS; ++s) {
+              const int r = 4 * s + h, tap = r >> 4, ci = r & 15;
+              const float a = h1s[(t0 + (lane & 15) + tap - 2 + 2) * C + ci];
+              acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Wf[s], acc, 0, 0, 0);
+            }
+          } else {
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+              const int tap = 2 * s + (h >> 1);
+              const int r = t0 + (lane & 15) + tap - 2;  // h1 time index
+              const bf16x8 A = *reinterpret_cast<const bf16x8*>(h1s + (r + 2) * C + 8 * (h & 1));
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bf[s], acc, 0, 0, 0);
+            }
           }
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -279,7 +311,7 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
             pool += v;
             const bool on = v > 0.f;
             cnt += on ? 1.f : 0.f;
-            ms[(t + 4) * C + c] = on ? one : zero;
+            ms[(t + 4) * C + c] = (AT)(on ? 1.f : 0.f);
           }
         }
       }
@@ -349,15 +381,29 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     const int item = w - 1, k = item / S, part = item % S;
     const int per = (NP + S - 1) / S;
     const int p0 = part * per, p1 = p0 + per < NP ? p0 + per : NP;
-    const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int pair = p0; pair < p1; ++pair) {
-      const int ta = 32 * pair + 8 * h + q;  // time of row q of this lane-quarter's first 4x16 block
-      // A[co][t] (lane: co = l&15, t = 32*pair + 8h + j): transposing reads of the [t][co] mask image
-      const bf16x8 A = cat44(lds_tr16(ms + (ta + 4) * C + p4), lds_tr16(ms + (ta + 4 + 4) * C + p4));
-      // B[t][ci] = h1[t + k - 2][ci]
-      const bf16x8 Bm = cat44(lds_tr16(h1s + (ta + k - 2 + 2) * C + p4), lds_tr16(h1s + (ta + k - 2 + 4 + 2) * C + p4));
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bm, acc, 0, 0, 0);
+    if constexpr (F32) {
+      // 16x16x4 f32: lane holds A[co = l&15][t = 4s + h] and B[t][ci = l&15]
+      for (int pair = p0; pair < p1; ++pair) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const int t = 32 * pair + 4 * s + h;
+          const float a = ms[(t + 4) * C + (lane & 15)];
+          const float bb = h1s[(t + k - 2 + 2) * C + (lane & 15)];
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb, acc, 0, 0, 0);
+        }
+      }
+    } else {
+      const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
+      for (int pair = p0; pair < p1; ++pair) {
+        const int ta = 32 * pair + 8 * h + q;  // time of row q of this lane-quarter's first 4x16 block
+        // A[co][t] (lane: co = l&15, t = 32*pair + 8h + j): transposing reads of the [t][co] mask image
+        const bf16x8 A = cat44(lds_tr16(ms + (ta + 4) * C + p4), lds_tr16(ms + (ta + 4 + 4) * C + p4));
+        // B[t][ci] = h1[t + k - 2][ci]
+        const bf16x8 Bm =
+            cat44(lds_tr16(h1s + (ta + k - 2 + 2) * C + p4), lds_tr16(h1s + (ta + k - 2 + 4 + 2) * C + p4));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bm, acc, 0, 0, 0);
+      }
     }
     // acc[i] = M_k[co = 4h+i][ci = c]
     float* pm = red + red_m(WAVES) + part * 1280;
@@ -378,11 +424,18 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
       gq[4 * q2] = v.x; gq[4 * q2 + 1] = v.y; gq[4 * q2 + 2] = v.z; gq[4 * q2 + 3] = v.w;
     }
     bf16x8 Bd[3];
+    float Wd[F32_KSTEPS];
+    if constexpr (F32) {
+      // 16x16x4 f32: B[r][ci], r = 4s + h = 16k + co
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const bf16x8 raw = *reinterpret_cast<const bf16x8*>(fragD + (s * 64 + lane) * 8);
+      for (int s = 0; s < F32_KSTEPS; ++s) Wd[s] = fragD32[s * 64 + lane] * red[RED_G + ((4 * s + h) & 15)];
+    } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) Bd[s][j] = ecg::to_bf16(ecg::from_bf16(raw[j]) * gq[j]);
+      for (int s = 0; s < 3; ++s) {
+        const bf16x8 raw = *reinterpret_cast<const bf16x8*>(fragD + (s * 64 + lane) * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Bd[s][j] = ecg::to_bf16(ecg::from_bf16(raw[j]) * gq[j]);
+      }
     }
     float dw1[K1 + 1];
 #pragma unroll
@@ -395,12 +448,21 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
         for (int half = 0; half < 2; ++half) {
           const int t0 = 32 * pair + 16 * half;
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (F32) {
 #pragma unroll
-          for (int s = 0; s < 3; ++s) {
-            const int k = 2 * s + (h >> 1);
-            const int r = t0 + (lane & 15) - k + 2;  // mask time index
-            const bf16x8 A = *reinterpret_cast<const bf16x8*>(ms + (r + 4) * C + 8 * (h & 1));
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bd[s], acc, 0, 0, 0);
+            for (int s = 0; s < F32_KSTEPS; ++s) {
+              const int r = 4 * s + h, k = r >> 4, co = r & 15;
+              const float a = ms[(t0 + (lane & 15) - k + 2 + 4) * C + co];
+              acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Wd[s], acc, 0, 0, 0);
+            }
+          } else {
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+              const int k = 2 * s + (h >> 1);
+              const int r = t0 + (lane & 15) - k + 2;  // mask time index
+              const bf16x8 A = *reinterpret_cast<const bf16x8*>(ms + (r + 4) * C + 8 * (h & 1));
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bd[s], acc, 0, 0, 0);
+            }
           }
           const int tb = t0 + 4 * h;
           float xw[12];
@@ -615,11 +677,11 @@ __global__ __launch_bounds__(RED_COLS * RED_ROWG) void slab_reduce_sgd_kernel(
 
 unsigned long long* g_stamps = nullptr;  // diagnostic phase stamps (ecg_tiny_set_stamps)
 
-template <int WAVES, int MODE>
+template <int WAVES, int MODE, bool F32>
 int launch_step(const float* X, int L, long ldx, const int* idx, const int* Y, const float* params, int nc,
                 float* out, int out_stride, int B, float inv_B, const FusedOpt& opt, hipStream_t stream) {
-  const Smem sm = make_smem(L, WAVES, nc);
-  auto kern = tiny_ecg_step_kernel<WAVES, MODE>;
+  const Smem sm = make_smem(L, WAVES, nc, F32);
+  auto kern = tiny_ecg_step_kernel<WAVES, MODE, F32>;
   if (sm.bytes > 64 * 1024)
     ECG_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, sm.bytes));
   hipLaunchKernelGGL(kern, dim3(B), dim3(WAVES * 64), sm.bytes, stream, X, L, ldx, idx, Y, params, nc, out,
@@ -632,40 +694,53 @@ constexpr int kMaxLds = 160 * 1024;
 
 // 16 waves (one tile pair each at L=500) when the per-wave partial slots fit in LDS, else 8.
 // ECG_TINY_WAVES=8|16 overrides (tuning); the choice never changes results beyond fp32 summation order.
-int pick_waves(int L) {
+// bf16: 8 waves measured fastest at L=500 (profiles/r1_fused_step_v3); fp32: 16 waves (4x more MFMA
+// instructions per tile on v_mfma_f32_16x16x4_f32, so the extra waves pay).
+int pick_waves(int L, bool f32) {
   const int Lp = (L + 31) / 32 * 32;
   static int forced = -1;
   if (forced < 0) {
     const char* e = getenv("ECG_TINY_WAVES");
     forced = e ? atoi(e) : 0;
   }
-  const bool fit16 = Lp <= 32 * 4 * 16 && make_smem(L, 16).bytes <= kMaxLds;
+  const bool fit16 = Lp <= 32 * 4 * 16 && make_smem(L, 16, MAX_CLASSES, f32).bytes <= kMaxLds;
   if (forced == 16 && fit16) return 16;
   if (forced == 8) return 8;
-  return (fit16 && Lp / 32 >= 16) ? 16 : 8;
+  return (f32 && fit16 && Lp / 32 >= 16) ? 16 : 8;
 }
 
-int check_step_args(int L, int nc, int B, int out_stride, int mode) {
+int check_step_args(int L, int nc, int B, int out_stride, int mode, bool f32 = false) {
   if (L < 8 || B <= 0 || nc < 1 || nc > MAX_CLASSES) return ecg::kBadArg;
   const int Lp = (L + 31) / 32 * 32;
-  if (Lp > 32 * 4 * 8 || make_smem(L, 8).bytes > kMaxLds) return ecg::kTooLarge;  // use the op-by-op path
+  if (Lp > 32 * 4 * 8 || make_smem(L, 8, MAX_CLASSES, f32).bytes > kMaxLds) return ecg::kTooLarge;  // op-by-op path
   const Layout lay = make_layout(nc);
   if (mode == 0 && out_stride < lay.P + 1) return ecg::kBadArg;
   if (mode == 1 && out_stride < nc) return ecg::kBadArg;
   return ecg::kOk;
 }
 
-int step_dispatch(int mode, const float* X, int L, long ldx, const int* idx, const int* Y, const float* params,
+template <bool F32>
+int dispatch_prec(int mode, const float* X, int L, long ldx, const int* idx, const int* Y, const float* params,
                   int nc, float* out, int out_stride, int B, float inv_B, const FusedOpt& opt, hipStream_t stream) {
-  int st = check_step_args(L, nc, B, out_stride, mode);
+  const int waves = pick_waves(L, F32);
+  if (mode == 0)
+    return waves == 8
+               ? launch_step<8, 0, F32>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream)
+               : launch_step<16, 0, F32>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream);
+  return waves == 8 ? launch_step<8, 1, F32>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream)
+                    : launch_step<16, 1, F32>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream);
+}
+
+// prec: 0 = bf16 MFMA operands (AMP), 1 = fp32 (exact f32 MFMA)
+int step_dispatch(int mode, int prec, const float* X, int L, long ldx, const int* idx, const int* Y,
+                  const float* params, int nc, float* out, int out_stride, int B, float inv_B, const FusedOpt& opt,
+                  hipStream_t stream) {
+  if (prec != 0 && prec != 1) return ecg::kBadArg;
+  int st = check_step_args(L, nc, B, out_stride, mode, prec == 1);
   if (st) return st;
   if (opt.ctl && (!opt.gslab || !opt.params || (opt.momentum != 0.f && !opt.mom) || opt.G != B)) return ecg::kBadArg;
-  const int waves = pick_waves(L);
-  if (mode == 0)
-    return waves == 8 ? launch_step<8, 0>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream)
-                      : launch_step<16, 0>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream);
-  return waves == 8 ? launch_step<8, 1>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream)
-                    : launch_step<16, 1>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream);
+  return prec == 1 ? dispatch_prec<true>(mode, X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream)
+                   : dispatch_prec<false>(mode, X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream);
 }
 
 FusedOpt no_fuse() {
@@ -703,19 +778,21 @@ ECG_API int ecg_tiny_set_stamps(unsigned long long* stamps) {
   return ecg::kOk;
 }
 
-ECG_API int ecg_tiny_smem_bytes(int L) { return make_smem(L, pick_waves(L)).bytes; }
+ECG_API int ecg_tiny_smem_bytes(int L, int prec) {
+  return make_smem(L, pick_waves(L, prec == 1), MAX_CLASSES, prec == 1).bytes;
+}
 
 // One fused training step's gradient pass: writes slab[B][slab_stride] (grads + loss at column P).
 ECG_API int ecg_tiny_step_grads(const float* X, int L, long ldx, const int* idx, const int* Y,
                                 const float* params, int nc, float* slab, int slab_stride, int B, float inv_B,
-                                hipStream_t stream) {
-  return step_dispatch(0, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, inv_B, no_fuse(), stream);
+                                int prec, hipStream_t stream) {
+  return step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, inv_B, no_fuse(), stream);
 }
 
 // Inference: logits[B][nc] for windows X[idx[b]].
 ECG_API int ecg_tiny_forward(const float* X, int L, long ldx, const int* idx, const float* params, int nc,
-                             float* logits, int B, hipStream_t stream) {
-  return step_dispatch(1, X, L, ldx, idx, nullptr, params, nc, logits, nc, B, 0.f, no_fuse(), stream);
+                             float* logits, int B, int prec, hipStream_t stream) {
+  return step_dispatch(1, prec, X, L, ldx, idx, nullptr, params, nc, logits, nc, B, 0.f, no_fuse(), stream);
 }
 
 // Size of the control block (int32 counters, must be zero before the first fused step) and of the
@@ -735,12 +812,14 @@ ECG_API int ecg_slab_reduce_sgd(const float* slab, int G, int stride, int P, flo
 // (gradient slab, then slab_reduce_sgd_kernel).
 ECG_API int ecg_tiny_train_step(const float* X, int L, long ldx, const int* idx, const int* Y, float* params,
                                 float* mom, int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr,
-                                float momentum, float wd, int nesterov, int* ctl, float* gslab, hipStream_t stream) {
+                                float momentum, float wd, int nesterov, int* ctl, float* gslab, int prec,
+                                hipStream_t stream) {
   if (ctl) {
     FusedOpt o{ctl, gslab, params, mom, loss_acc, lr, momentum, wd, nesterov, B};
-    return step_dispatch(0, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, o, stream);
+    return step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, o, stream);
   }
-  int st = step_dispatch(0, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, no_fuse(), stream);
+  int st = step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, no_fuse(),
+                         stream);
   if (st) return st;
   return reduce_dispatch(slab, B, slab_stride, make_layout(nc).P, params, mom, nullptr, loss_acc, lr, momentum, wd,
                          nesterov, 1, stream);
@@ -751,9 +830,9 @@ ECG_API int ecg_tiny_train_step(const float* X, int L, long ldx, const int* idx,
 ECG_API int ecg_round_graph_create(void** handle, const float* X, int L, long ldx, const int* idx_table,
                                    const int* Y, float* params, float* mom, int nc, float* slab, int slab_stride,
                                    int B, int steps, float* loss_acc, float lr, float momentum, float wd,
-                                   int nesterov, int* ctl, float* gslab) {
+                                   int nesterov, int* ctl, float* gslab, int prec) {
   if (!handle || steps <= 0) return ecg::kBadArg;
-  int st = check_step_args(L, nc, B, slab_stride, 0);
+  int st = check_step_args(L, nc, B, slab_stride, 0, prec == 1);
   if (st) return st;
   hipStream_t cap;
   ECG_HIP_CHECK(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
@@ -767,7 +846,7 @@ ECG_API int ecg_round_graph_create(void** handle, const float* X, int L, long ld
   }
   for (int s = 0; s < steps && st == 0; ++s)
     st = ecg_tiny_train_step(X, L, ldx, idx_table + (long)s * B, Y, params, mom, nc, slab, slab_stride, B, loss_acc,
-                             lr, momentum, wd, nesterov, ctl, gslab, cap);
+                             lr, momentum, wd, nesterov, ctl, gslab, prec, cap);
   e = hipStreamEndCapture(cap, &rg->graph);
   (void)hipStreamDestroy(cap);
   if (st != 0 || e != hipSuccess) {
