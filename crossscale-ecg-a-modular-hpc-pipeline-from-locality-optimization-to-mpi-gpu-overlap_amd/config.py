@@ -18,7 +18,7 @@ class FedAvgConfig:
     max_windows: int = 30000
     config: str = "both"  # G0 | G1 | both
     # ---- MI355X additions ----
-    kernel_backend: str = "auto"  # auto | fused | torch
+    kernel_backend: str = "auto"  # auto | fused | hip | torch  (hip = MFMA conv kernels for ResNet1D)
     amp_dtype: str = "bf16"  # bf16 | fp16 | none  (dtype of the G1 configuration)
     overlap: str = "none"  # none | delayed
     sync: str = "fedavg"  # fedavg | none | ddp

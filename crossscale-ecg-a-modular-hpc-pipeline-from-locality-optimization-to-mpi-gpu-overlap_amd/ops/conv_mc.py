@@ -1,0 +1,113 @@
+"""Multi-channel conv1d on MFMA (csrc/kernels/conv1d_mc.hip) as a differentiable op, channels-last.
+
+``conv1d_nlc(x, weight, bias, stride, padding)``: x [B, L, C_in] bf16 (NLC), weight [C_out, C_in, K] (the
+nn.Conv1d parameter, fp32 master), bias [C_out] or None -> y [B, L_out, C_out] bf16.
+  forward    = ecg_conv1d_nlc_fwd (implicit GEMM, bias fused)
+  grad input = ecg_conv1d_nlc_fwd on dy with input dilation ``stride``, flipped taps, pad K-1-p
+  grad weight= ecg_conv1d_nlc_wgrad (split-K fp32 partials, summed in a fixed order -> deterministic)
+  grad bias  = sum of dy over (B, L)
+Constraints: C_in % 64 == 0 and C_out % 64 == 0 (``supported()``); callers fall back to MIOpen otherwise.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+
+def supported(c_in: int, c_out: int) -> bool:
+    return c_in % 64 == 0 and c_out % 64 == 0
+
+
+def out_len(L: int, K: int, stride: int, pad: int) -> int:
+    return (L + 2 * pad - K) // stride + 1
+
+
+def _bind(lib):
+    if getattr(lib, "_conv_mc_bound", False):
+        return
+    vp, i32 = _lib.vp, _lib.i32
+    _lib._sig(lib, "ecg_conv1d_nlc_fwd", [vp, vp, vp, vp] + [i32] * 10 + [vp])
+    _lib._sig(lib, "ecg_conv1d_nlc_wgrad", [vp, vp, vp] + [i32] * 9 + [vp])
+    lib._conv_mc_bound = True
+
+
+def _lib_k():
+    lib = _lib.kernels()
+    _bind(lib)
+    return lib
+
+
+def fwd_raw(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor], stride: int, pad: int,
+            L_out: int, in_dil: int = 1, relu: bool = False) -> torch.Tensor:
+    """x [B, Lin, Cin] bf16, w_t [Cout, K, Cin] bf16 -> y [B, L_out, Cout] bf16."""
+    B, Lin, Cin = x.shape
+    Cout, K, Cin2 = w_t.shape
+    if Cin2 != Cin or x.dtype != torch.bfloat16 or w_t.dtype != torch.bfloat16:
+        raise ValueError("conv1d_nlc: bf16 x [B,L,Cin] and w [Cout,K,Cin] required")
+    if not (x.is_contiguous() and w_t.is_contiguous()):
+        raise ValueError("conv1d_nlc: contiguous operands required")
+    if not supported(Cin, Cout):
+        raise ValueError(f"conv1d_nlc needs C_in, C_out multiples of 64 (got {Cin}, {Cout})")
+    y = torch.empty((B, L_out, Cout), dtype=torch.bfloat16, device=x.device)
+    b = None if bias is None else bias.float().contiguous()
+    st = _lib_k().ecg_conv1d_nlc_fwd(x.data_ptr(), w_t.data_ptr(), _lib.ptr(b), y.data_ptr(), B, Lin, Cin, L_out, Cout,
+                                     K, stride, pad, in_dil, int(relu), _lib.stream_ptr(x.device))
+    _lib.check(st, "ecg_conv1d_nlc_fwd")
+    return y
+
+
+def wgrad_raw(dy: torch.Tensor, x: torch.Tensor, K: int, stride: int, pad: int,
+              splits: Optional[int] = None) -> torch.Tensor:
+    """dw [Cout, K, Cin] fp32 from dy [B, Lout, Cout] and x [B, Lin, Cin] (bf16)."""
+    B, Lout, Cout = dy.shape
+    _, Lin, Cin = x.shape
+    R = B * Lout
+    chunks = (R + 63) // 64
+    tiles = (Cout // 64) * (K * Cin // 64)
+    if splits is None:  # aim for ~2 workgroups per CU, at least 4 r-chunks per workgroup
+        splits = max(1, min(chunks // 4 if chunks >= 4 else 1, max(1, 512 // max(1, tiles))))
+    part = torch.empty((splits, Cout, K * Cin), dtype=torch.float32, device=dy.device)
+    st = _lib_k().ecg_conv1d_nlc_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr(), splits, B, Lin, Cin, Lout, Cout, K,
+                                       stride, pad, _lib.stream_ptr(dy.device))
+    _lib.check(st, "ecg_conv1d_nlc_wgrad")
+    return part.sum(0).view(Cout, K, Cin)
+
+
+class Conv1dNLC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride: int, pad: int):
+        Cout, Cin, K = weight.shape
+        L_out = out_len(x.shape[1], K, stride, pad)
+        w_t = weight.detach().permute(0, 2, 1).to(torch.bfloat16).contiguous()  # [Cout, K, Cin]
+        xb = x.to(torch.bfloat16).contiguous()
+        y = fwd_raw(xb, w_t, bias.detach() if bias is not None else None, stride, pad, L_out)
+        ctx.save_for_backward(xb, weight)
+        ctx.has_bias = bias is not None
+        ctx.stride, ctx.pad = stride, pad
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, weight = ctx.saved_tensors
+        Cout, Cin, K = weight.shape
+        dyb = dy.to(torch.bfloat16).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            # dx[u] = sum_k' w[K-1-k'] * dil_s(dy)[u + k' - (K-1-p)]
+            w_d = weight.detach().flip(2).permute(1, 2, 0).to(torch.bfloat16).contiguous()  # [Cin, K, Cout]
+            dx = fwd_raw(dyb, w_d, None, 1, K - 1 - ctx.pad, xb.shape[1], in_dil=ctx.stride)
+        if ctx.needs_input_grad[1]:
+            dw = wgrad_raw(dyb, xb, K, ctx.stride, ctx.pad).permute(0, 2, 1).contiguous().to(weight.dtype)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy.float().sum(dim=(0, 1)).to(weight.dtype)
+        return dx, dw, db, None, None
+
+
+def conv1d_nlc(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None, stride: int = 1,
+               padding: int = 0) -> torch.Tensor:
+    if padding > weight.shape[2] - 1:
+        raise ValueError("padding must be < kernel size (data-grad uses pad K-1-p)")
+    return Conv1dNLC.apply(x, weight, bias, stride, padding)

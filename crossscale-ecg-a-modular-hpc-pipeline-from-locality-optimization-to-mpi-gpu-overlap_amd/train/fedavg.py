@@ -100,6 +100,11 @@ def dev_index(ctx):
 def pick_backend(cfg: FedAvgConfig, config_name: str, ctx: DistContext) -> str:
     if cfg.kernel_backend == "torch" or ctx.device.type != "cuda":
         return "torch"
+    if cfg.model.startswith("resnet"):
+        if cfg.kernel_backend == "fused":
+            raise ValueError("the fused HIP step implements TinyECG only; use --kernel-backend hip for ResNet1D")
+        # the MFMA conv kernels compute in bf16: G1 with bf16 AMP only; G0 keeps fp32 semantics on MIOpen
+        return "hip" if (config_name == "G1" and cfg.amp_dtype == "bf16") else "torch"
     # fused HIP step: TinyECG in fp32 (G0, or G1 with --amp-dtype none) or bf16 AMP (G1); fp16 AMP keeps the
     # reference's GradScaler path on eager PyTorch
     fused_ok = cfg.model == "tiny_ecg" and (config_name == "G0" or cfg.amp_dtype in ("bf16", "none"))
@@ -152,6 +157,8 @@ def run_fedavg(cfg: FedAvgConfig, ctx: DistContext) -> List[Dict]:
         torch.manual_seed(cfg.seed)  # identical init on every client (the round-0 broadcast makes it exact)
         model = build_model(cfg.model, cfg.num_classes).to(dev)
         backend = pick_backend(cfg, cname, ctx)
+        if hasattr(model, "backend"):  # ResNet1D: MFMA channels-last convs on the GPU unless --kernel-backend torch
+            model.backend = "hip" if backend == "hip" else "torch"
         flat = model.flatten_parameters() if hasattr(model, "flatten_parameters") else None
         trainer = make_trainer(cfg, cname, model, x, y, ctx, backend)
         start_round = 0

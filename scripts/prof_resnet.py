@@ -1,0 +1,13 @@
+#!/usr/bin/env python3
+"""Run a few ResNet1D-34 training steps on one backend (for rocprofv3 --kernel-trace --stats)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import crossscale_ecg  # noqa: E402,F401
+from crossscale_ecg.bench.resnet import train_throughput  # noqa: E402
+
+if __name__ == "__main__":
+    be = sys.argv[1] if len(sys.argv) > 1 else "hip"
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+    print(be, B, train_throughput(be, B=B, steps=10))

@@ -1,0 +1,83 @@
+"""MFMA multi-channel conv1d (channels-last) vs plain PyTorch fp32 F.conv1d: forward, dgrad, wgrad, bias."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import crossscale_ecg  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+CASES = [  # B, L, Cin, Cout, K, stride, pad
+    (4, 125, 64, 64, 3, 1, 1),
+    (3, 125, 64, 128, 3, 2, 1),
+    (2, 63, 128, 128, 3, 1, 1),
+    (5, 33, 128, 256, 1, 2, 0),
+    (2, 16, 512, 512, 3, 1, 1),
+    (3, 70, 64, 192, 5, 1, 2),
+    (2, 32, 256, 512, 3, 2, 1),  # (L+2p-K) % stride != 0: last input row only reached by one tap
+    (3, 32, 256, 512, 1, 2, 0),
+    (2, 9, 64, 64, 3, 2, 1),
+]
+
+
+def _rel(a, b):
+    return (a.float() - b.float()).norm().item() / (b.float().norm().item() + 1e-12)
+
+
+@pytest.mark.parametrize("B,L,Cin,Cout,K,s,p", CASES)
+def test_conv1d_nlc_forward_backward(B, L, Cin, Cout, K, s, p):
+    from crossscale_ecg.ops.conv_mc import conv1d_nlc
+    torch.manual_seed(0)
+    x = torch.randn(B, L, Cin, device=DEV).bfloat16().requires_grad_(True)
+    w = (torch.randn(Cout, Cin, K, device=DEV) / (Cin * K) ** 0.5).requires_grad_(True)
+    b = torch.randn(Cout, device=DEV).requires_grad_(True)
+    y = conv1d_nlc(x, w, b, s, p)
+    # fp32 reference on the same bf16-rounded inputs
+    xr = x.detach().float().transpose(1, 2).requires_grad_(True)
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    yr = F.conv1d(xr, wr, br, stride=s, padding=p)
+    assert y.shape == (B, yr.shape[2], Cout)
+    assert _rel(y.transpose(1, 2), yr) < 1e-2
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    y.backward(g.transpose(1, 2).bfloat16())
+    torch.cuda.synchronize()
+    assert _rel(x.grad.transpose(1, 2), xr.grad) < 2e-2
+    assert _rel(w.grad, wr.grad) < 2e-2
+    assert _rel(b.grad, br.grad) < 1e-2
+
+
+def _grads(m, x, y, amp=False):
+    m.zero_grad(set_to_none=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        F.cross_entropy(m(x), y).backward()
+    torch.cuda.synchronize()
+    return {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+
+
+def test_resnet1d_hip_backend_matches_torch():
+    """The hip backend (bf16 NLC MFMA convs) vs the fp32 torch model.  A random-init deep net in train-mode BN
+    amplifies bf16 rounding (torch's own bf16 autocast is ~30% off fp32 in the early-layer grads at B=8), so
+    the bound is relative to the autocast error of the same batch, plus an absolute cap."""
+    from crossscale_ecg.models.resnet1d import resnet1d18
+    torch.manual_seed(0)
+    m = resnet1d18(backend="torch").to(DEV)
+    x = torch.randn(16, 1, 500, device=DEV)
+    y = torch.randint(0, 2, (16,), device=DEV)
+    m.eval()
+    with torch.no_grad():
+        a = m(x)
+        m.backend = "hip"
+        b = m(x)
+    assert _rel(b, a) < 5e-2
+    m.train()
+    m.backend = "torch"
+    g32 = _grads(m, x, y)
+    gam = _grads(m, x, y, amp=True)
+    m.backend = "hip"
+    ghp = _grads(m, x, y)
+    for n in g32:
+        e_amp, e_hip = _rel(gam[n], g32[n]), _rel(ghp[n], g32[n])
+        assert e_hip < 1.5 * e_amp + 0.05 and e_hip < 0.6, (n, e_hip, e_amp)
