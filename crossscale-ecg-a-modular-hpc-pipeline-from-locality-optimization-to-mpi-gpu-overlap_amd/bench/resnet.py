@@ -86,3 +86,24 @@ def train_throughput(backend: str, B: int = 256, L: int = 500, steps: int = 20, 
         step()
     torch.cuda.synchronize()
     return B * steps / (time.perf_counter() - t0)
+
+
+def engine_throughput(B: int = 256, L: int = 500, steps: int = 20, warmup: int = 3, depth: int = 34,
+                      use_graph: bool = True, dev="cuda") -> float:
+    """Samples/s of the native step engine (ops.resnet_engine): fwd + bwd + SGD per step, bf16, one hipGraph."""
+    from ..models.resnet1d import resnet1d18
+    from ..ops.resnet_engine import ResNetStepEngine
+    torch.manual_seed(0)
+    m = (resnet1d34 if depth == 34 else resnet1d18)().to(dev)
+    eng = ResNetStepEngine(m, B, L, lr=1e-2, momentum=0.9, use_graph=use_graph)
+    eng.set_batch(torch.randn(B, 1, L, device=dev), torch.randint(0, 2, (B,), device=dev))
+    for _ in range(warmup):
+        eng.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    eng.close()
+    return B * steps / dt

@@ -1,0 +1,430 @@
+"""Native ResNet1D training step: the whole forward + backward + SGD step as ONE encoded launch plan
+(csrc/kernels/resnet_nlc.hip), replayed eagerly by the C++ plan executor or captured into a single hipGraph.
+
+BASELINE.json config 5 (ResNet1D-34 stress, bf16, large batch).  Design (MI355X-first, see the .hip header):
+
+* one flat fp32 buffer holds every parameter (then the BN running statistics) - ``parallel.flat`` - so FedAvg
+  is one RCCL all-reduce, DDP one bucketed all-reduce per backward segment, SGD one kernel;
+* activations are channels-last bf16 ``[B, L, C]`` resident in HBM for the whole step (no NCL<->NLC
+  transposes, no MIOpen), all shapes fixed at construction so every pointer is baked into the plan;
+* every conv is an MFMA implicit GEMM (conv1d_mc.hip) whose epilogue also emits the BatchNorm statistics;
+  BN apply / backward passes are fused with ReLU and the residual;
+* backward is laid out in ``segments`` (head+layer4, layer3, layer2, layer1+stem).  The gradients of a
+  segment form one contiguous range of the flat grad buffer, so with ``grad_sync`` each range is all-reduced
+  on a side stream while the next segment's graph runs (the DDP overlap of SURVEY §2 C29 / §7 step 8).
+
+The reference has no ResNet; parity is against PyTorch's own fp32 ResNet1D (tests/test_resnet_engine_gpu.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import struct
+from typing import Callable, Dict, List, Optional, Tuple
+
+import torch
+
+from . import _lib
+from ..models.resnet1d import ResNet1D
+
+OP_WORDS = 32
+OP = dict(CONV_FWD=1, CONV_WGRAD=2, REDUCE_WGRAD=3, BN_FIN=4, BN_ACT=5, BN_BWD_REDUCE=6, BN_BWD_APPLY=7,
+          STEM_FWD=8, STEM_POOL=9, STEM_BWD_REDUCE=10, STEM_WGRAD=11, REDUCE_SUM=12, WEIGHT_PREP=13, HEAD=14,
+          HEAD_REDUCE=15, SGD=16)
+
+
+def _f(x: float) -> int:
+    return struct.unpack("<q", struct.pack("<d", float(x)))[0]
+
+
+def _bind(lib):
+    if getattr(lib, "_plan_bound", False):
+        return
+    vp, i32 = _lib.vp, _lib.i32
+    _lib._sig(lib, "ecg_plan_run", [vp, i32, ctypes.POINTER(ctypes.c_int), vp])
+    _lib._sig(lib, "ecg_plan_graph_create", [ctypes.POINTER(ctypes.c_void_p), vp, i32, ctypes.POINTER(ctypes.c_int)])
+    _lib._sig(lib, "ecg_plan_graph_launch", [vp, vp])
+    _lib._sig(lib, "ecg_plan_graph_destroy", [vp])
+    _lib._sig(lib, "ecg_plan_op_words", [])
+    _lib._sig(lib, "ecg_plan_wentry_bytes", [])
+    _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles", [ctypes.c_long, i32])
+    lib._plan_bound = True
+    if lib.ecg_plan_op_words() != OP_WORDS or lib.ecg_plan_wentry_bytes() != 40:
+        raise _lib.NativeError("resnet plan ABI mismatch (rebuild csrc)")
+
+
+def _out_len(L: int, K: int, s: int, p: int) -> int:
+    return (L + 2 * p - K) // s + 1
+
+
+class _BN:
+    """Per-BatchNorm device state: saved mean / rstd / scale / shift (fwd) and c1 / c2 (bwd)."""
+
+    def __init__(self, bn: torch.nn.BatchNorm1d, dev):
+        C = bn.num_features
+        self.bn, self.C = bn, C
+        self.buf = torch.zeros(6, C, dtype=torch.float32, device=dev)
+        self.mean, self.rstd, self.scale, self.shift, self.c1, self.c2 = (self.buf[i] for i in range(6))
+
+
+class ResNetStepEngine:
+    """Fixed-shape training step for a :class:`ResNet1D` (any depth, BasicBlocks, channels multiple of 64).
+
+    ``set_batch(x, y)`` copies a batch into the static input buffers; ``step()`` runs forward, backward and
+    SGD; ``forward_backward()`` skips the SGD (tests, DDP).  ``grad_sync(flat_range_tensor)`` - if given -
+    is called for each backward segment's gradient range in order (DDP all-reduce hook).
+    """
+
+    def __init__(self, model: ResNet1D, batch_size: int, seq_len: int = 500, lr: float = 1e-2,
+                 momentum: float = 0.9, weight_decay: float = 0.0, nesterov: bool = False, use_graph: bool = True,
+                 grad_sync: Optional[Callable[[torch.Tensor], None]] = None):
+        dev = next(model.parameters()).device
+        if dev.type != "cuda":
+            raise RuntimeError("ResNetStepEngine needs a GPU (HIP kernels)")
+        self.lib = _lib.kernels()
+        _bind(self.lib)
+        self.model, self.dev, self.B, self.L = model, dev, int(batch_size), int(seq_len)
+        self.lr, self.momentum, self.wd, self.nesterov = lr, momentum, weight_decay, nesterov
+        self.use_graph, self.grad_sync = use_graph, grad_sync
+        if model._space is None:
+            model.flatten_parameters()
+        self.space = model._space
+        self.flat = self.space.flat
+        self.grad = self.space.grad_buffer()
+        self.mom = torch.zeros_like(self.grad)
+        self.loss_acc = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._steps_since_sync = 0
+        self._loss_steps = 0
+        self._keep: List[torch.Tensor] = []
+        self._graphs: Dict[str, int] = {}
+        self._build()
+
+    # ------------------------------------------------------------------------------------------ allocation
+    def _t(self, *shape, dtype=torch.bfloat16) -> torch.Tensor:
+        t = torch.empty(*shape, dtype=dtype, device=self.dev)
+        self._keep.append(t)
+        return t
+
+    def _gptr(self, p: torch.Tensor) -> int:
+        """Address of parameter ``p``'s gradient inside the flat grad buffer."""
+        return self.grad.data_ptr() + 4 * self.space.offset_of(p)
+
+    # ------------------------------------------------------------------------------------------ plan build
+    def _build(self):
+        m, B, L, dev = self.model, self.B, self.L, self.dev
+        c0 = m.conv1
+        if c0.in_channels != 1 or c0.out_channels != 64 or c0.kernel_size[0] > 8:
+            raise ValueError("engine stem expects Conv1d(1, 64, k<=8)")
+        blocks = [blk for st in (m.layer1, m.layer2, m.layer3, m.layer4) for blk in st]
+        Ks, Ss, Ps = c0.kernel_size[0], c0.stride[0], c0.padding[0]
+        Lz = _out_len(L, Ks, Ss, Ps)
+        mp = m.maxpool
+        if (mp.kernel_size, mp.stride, mp.padding) != (3, 2, 1):
+            raise ValueError("engine stem expects MaxPool1d(3, 2, 1)")
+        Lp = _out_len(Lz, 3, 2, 1)
+        self.Lz, self.Lp = Lz, Lp
+
+        # ---- shapes per block
+        shapes = []
+        Lc, Cc = Lp, 64
+        for blk in blocks:
+            s = blk.conv1.stride[0]
+            Co = blk.conv1.out_channels
+            if Cc % 64 or Co % 64:
+                raise ValueError("engine convs need channels % 64 == 0")
+            Lo = _out_len(Lc, 3, s, 1)
+            shapes.append((Lc, Cc, Lo, Co, s))
+            Lc, Cc = Lo, Co
+        self.Lf, self.Cf = Lc, Cc
+        ncls = m.fc.out_features
+        maxel = max([B * Lz * 64] + [B * max(a[0] * a[1], a[2] * a[3]) for a in shapes])
+
+        # ---- static inputs and activations
+        self.x = self._t(B, L, dtype=torch.float32)
+        self.y = self._t(B, dtype=torch.int32)
+        self.z0 = self._t(B, Lz, 64)
+        self.h0 = self._t(B, Lp, 64)
+        acts = []
+        for (Li, Ci, Lo, Co, s), blk in zip(shapes, blocks):
+            a = dict(z1=self._t(B, Lo, Co), a1=self._t(B, Lo, Co), z2=self._t(B, Lo, Co), out=self._t(B, Lo, Co))
+            if blk.downsample is not None:
+                a["zd"] = self._t(B, Lo, Co)
+            acts.append(a)
+        # backward scratch (reused block to block: the plan is stream-ordered)
+        gA, gB = self._t(maxel), self._t(maxel)  # ping-pong: grad wrt block output / block input
+        dz2, ga1, dz1, dzd, tmp = (self._t(maxel) for _ in range(5))
+        dz0 = self._t(B, Lz, 64)
+        # BN states
+        bn0 = _BN(m.bn1, dev)
+        bns = [(_BN(b.bn1, dev), _BN(b.bn2, dev), _BN(b.downsample[1], dev) if b.downsample is not None else None)
+               for b in blocks]
+        self._bn_states = [bn0] + [x for t in bns for x in t if x is not None]
+        # stats / partial buffers (stream-ordered reuse)
+        max_T = max((B * Lz + 63) // 64, max((B * a[2] + 63) // 64 for a in shapes))
+        stats = self._t(2 * max_T * 512, dtype=torch.float32)
+        chunk_for = lambda C: (256 // (C // 8)) * 16  # noqa: E731  rows per reduce block
+        max_Tb = max((B * Lz + chunk_for(64) - 1) // chunk_for(64),
+                     max((B * a[2] + chunk_for(a[3]) - 1) // chunk_for(a[3]) for a in shapes))
+        bpart = self._t(3 * max_Tb * 512, dtype=torch.float32)
+        fin_scratch = self._t(1024 * 2 * 512, dtype=torch.float64)
+        tickets = torch.zeros(64, dtype=torch.int32, device=dev)
+        self._keep.append(tickets)
+
+        # ---- wgrad split plan + workspace
+        def wsplits(R, Cout, K, Cin):
+            # ~512 workgroups, >= 8 row chunks each, <= 64 partial slices (the reduce reads S x |dW|)
+            chunks = (R + 63) // 64
+            tiles = (Cout // 64) * (K * Cin // 64)
+            return max(1, min(64, max(1, chunks // 8), max(1, 512 // tiles)))
+
+        ws_need = 0
+        for (Li, Ci, Lo, Co, s), blk in zip(shapes, blocks):
+            R = B * Lo
+            ws_need = max(ws_need, wsplits(R, Co, 3, Ci) * Co * 3 * Ci, wsplits(R, Co, 3, Co) * Co * 3 * Co)
+            if blk.downsample is not None:
+                ws_need = max(ws_need, wsplits(R, Co, 1, Ci) * Co * Ci)
+        stem_chunk = max(256, -(-(B * Lz) // 1024 + 3) // 4 * 4)  # <= ~1024 partial slices
+        stem_blocks = (B * Lz + stem_chunk - 1) // stem_chunk
+        Gb = max(1, min(64, B // 64))
+        ws_need = max(ws_need, stem_blocks * 64 * Ks, Gb * (ncls * self.Cf + ncls + 1))
+        ws = self._t(ws_need, dtype=torch.float32)
+
+        # ---- bf16 weight arena (fwd + flipped dgrad layouts) and prep table
+        convs = []
+        for blk in blocks:
+            convs += [blk.conv1, blk.conv2] + ([blk.downsample[0]] if blk.downsample is not None else [])
+        total = sum(c.weight.numel() for c in convs)
+        self.warena = self._t(2 * total)
+        entries, off, block0 = [], 0, 0
+        self._wf, self._wb = {}, {}
+        for c in convs:
+            n = c.weight.numel()
+            self._wf[id(c)] = self.warena.data_ptr() + 2 * off
+            self._wb[id(c)] = self.warena.data_ptr() + 2 * (total + off)
+            entries.append(struct.pack("<qqqiiii", self.space.offset_of(c.weight), off, total + off, c.out_channels,
+                                       c.in_channels, c.kernel_size[0], block0))
+            off += n
+            block0 += (n + 255) // 256
+        tab = torch.tensor(list(b"".join(entries)), dtype=torch.uint8).to(dev)
+        self._keep.append(tab)
+        wprep_blocks = block0
+
+        ops: List[List[int]] = []
+        self._segments: List[Tuple[int, int, int, int]] = []  # (op_begin, op_end, grad_lo, grad_hi) elements
+
+        def op(kind, *args):
+            w = [OP[kind]] + [int(a) for a in args]
+            assert len(w) <= OP_WORDS, kind
+            ops.append(w + [0] * (OP_WORDS - len(w)))
+
+        P = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+        eps, bnm = m.bn1.eps, (m.bn1.momentum if m.bn1.momentum is not None else 0.1)
+
+        def fin_fwd(st: _BN, T, n):
+            G = max(1, min(128, T // 64))
+            bn = st.bn
+            op("BN_FIN", stats.data_ptr(), stats.data_ptr() + 4 * T * st.C, T, st.C, 0, P(fin_scratch),
+               P(tickets), _f(n), _f(eps), _f(bnm), P(bn.weight), P(bn.bias), P(st.mean), P(st.rstd), P(st.scale),
+               P(st.shift), P(bn.running_mean), P(bn.running_var), 0, 0, 0, 0, G)
+
+        def fin_bwd(st: _BN, T, n, statB):
+            G = max(1, min(128, T // 64))
+            bn = st.bn
+            op("BN_FIN", bpart.data_ptr(), bpart.data_ptr() + 4 * statB * T * st.C, T, st.C, 1, P(fin_scratch),
+               P(tickets), _f(n), _f(eps), _f(bnm), P(bn.weight), P(bn.bias), 0, 0, 0, 0, 0, 0,
+               self._gptr(bn.weight), self._gptr(bn.bias), P(st.c1), P(st.c2), G)
+
+        def conv(x, Lin, Cin, w_ptr, y, Lout, Cout, K, s, p, dil=1, st=None, add=None, add_mask=None):
+            op("CONV_FWD", P(x), w_ptr, 0, P(y), P(st), P(add), P(add_mask), B, Lin, Cin, Lout, Cout, K, s, p, dil, 0)
+
+        def wgrad(dy, x, Lin, Cin, Lout, Cout, K, s, p, weight):
+            S = wsplits(B * Lout, Cout, K, Cin)
+            op("CONV_WGRAD", P(dy), P(x), P(ws), S, B, Lin, Cin, Lout, Cout, K, s, p)
+            op("REDUCE_WGRAD", P(ws), S, Cout, K, Cin, self._gptr(weight))
+
+        # =============================== forward
+        op("WEIGHT_PREP", P(tab), len(convs), wprep_blocks, P(self.flat), P(self.warena))
+        T0 = (B * Lz + 63) // 64
+        op("STEM_FWD", P(self.x), P(c0.weight), P(self.z0), P(stats), B, L, Lz, Ks, Ss, Ps)
+        fin_fwd(bn0, T0, B * Lz)
+        op("STEM_POOL", P(self.z0), P(bn0.scale), P(bn0.shift), P(self.h0), B, Lz, Lp, 64)
+        xin = self.h0
+        for (Li, Ci, Lo, Co, s), blk, a, (b1, b2, bd) in zip(shapes, blocks, acts, bns):
+            T = self.lib.ecg_conv1d_nlc_fwd_stat_tiles(B * Lo, Co)  # rows of the epilogue's BN partials
+            conv(xin, Li, Ci, self._wf[id(blk.conv1)], a["z1"], Lo, Co, 3, s, 1, st=stats)
+            fin_fwd(b1, T, B * Lo)
+            op("BN_ACT", 0, P(a["z1"]), P(b1.scale), P(b1.shift), 0, 0, 0, P(a["a1"]), B * Lo, Co)
+            conv(a["a1"], Lo, Co, self._wf[id(blk.conv2)], a["z2"], Lo, Co, 3, 1, 1, st=stats)
+            fin_fwd(b2, T, B * Lo)
+            if bd is not None:
+                conv(xin, Li, Ci, self._wf[id(blk.downsample[0])], a["zd"], Lo, Co, 1, s, 0, st=stats)
+                fin_fwd(bd, T, B * Lo)
+                op("BN_ACT", 2, P(a["z2"]), P(b2.scale), P(b2.shift), P(a["zd"]), P(bd.scale), P(bd.shift),
+                   P(a["out"]), B * Lo, Co)
+            else:
+                op("BN_ACT", 1, P(a["z2"]), P(b2.scale), P(b2.shift), P(xin), 0, 0, P(a["out"]), B * Lo, Co)
+            a["in"] = xin
+            xin = a["out"]
+
+        # =============================== head (loss + dlogits + dW/db)
+        seg_begin = len(ops)
+        gbuf = self._t(B, ncls, dtype=torch.float32)
+        fbuf = self._t(B, self.Cf, dtype=torch.float32)
+        lbuf = self._t(B, dtype=torch.float32)
+        gcur = gA
+        op("HEAD", P(xin), P(m.fc.weight), P(m.fc.bias), P(self.y), P(gcur), P(gbuf), P(fbuf), P(lbuf), B, self.Lf,
+           self.Cf, ncls, 0)
+        op("HEAD_REDUCE", P(gbuf), P(fbuf), P(lbuf), P(ws), B, self.Cf, ncls, Gb)
+        if self.space.offset_of(m.fc.bias) != self.space.offset_of(m.fc.weight) + ncls * self.Cf:
+            raise RuntimeError("fc.weight / fc.bias not adjacent in the flat buffer")
+        op("REDUCE_SUM", P(ws), Gb, ncls * self.Cf + ncls + 1, self._gptr(m.fc.weight), ncls * self.Cf + ncls,
+           P(self.loss_acc))
+
+        # =============================== backward through the blocks (segments per stage)
+        stage_of = []
+        for si, st in enumerate((m.layer1, m.layer2, m.layer3, m.layer4)):
+            stage_of += [si] * len(st)
+        nxt = gB
+        seg_hi = self.space.param_numel
+        for bi in range(len(blocks) - 1, -1, -1):
+            (Li, Ci, Lo, Co, s), blk, a, (b1, b2, bd) = shapes[bi], blocks[bi], acts[bi], bns[bi]
+            R = B * Lo
+            ch = chunk_for(Co)
+            Tb = (R + ch - 1) // ch
+            gy, din = gcur, nxt
+            ns = 3 if bd is not None else 2
+            op("BN_BWD_REDUCE", ns, P(gy), P(a["out"]), P(a["z2"]), P(b2.mean), P(b2.rstd),
+               P(a.get("zd")), P(bd.mean) if bd else 0, P(bd.rstd) if bd else 0, P(bpart), R, Co, ch)
+            fin_bwd(b2, Tb, R, 1)
+            if bd is not None:
+                fin_bwd(bd, Tb, R, 2)
+            op("BN_BWD_APPLY", 1 if bd is not None else 0, P(gy), P(a["out"]), P(a["z2"]), P(b2.mean), P(b2.rstd),
+               P(b2.scale), P(b2.c1), P(b2.c2), P(dz2), P(a.get("zd")), P(bd.mean) if bd else 0,
+               P(bd.rstd) if bd else 0, P(bd.scale) if bd else 0, P(bd.c2) if bd else 0, P(dzd), R, Co)
+            wgrad(dz2, a["a1"], Lo, Co, Lo, Co, 3, 1, 1, blk.conv2.weight)
+            conv(dz2, Lo, Co, self._wb[id(blk.conv2)], ga1, Lo, Co, 3, 1, 1)  # dgrad conv2 (stride 1, pad 1)
+            op("BN_BWD_REDUCE", 2, P(ga1), P(a["a1"]), P(a["z1"]), P(b1.mean), P(b1.rstd), 0, 0, 0, P(bpart), R, Co,
+               ch)
+            fin_bwd(b1, Tb, R, 1)
+            op("BN_BWD_APPLY", 0, P(ga1), P(a["a1"]), P(a["z1"]), P(b1.mean), P(b1.rstd), P(b1.scale), P(b1.c1),
+               P(b1.c2), P(dz1), 0, 0, 0, 0, 0, 0, R, Co)
+            wgrad(dz1, a["in"], Li, Ci, Lo, Co, 3, s, 1, blk.conv1.weight)
+            if bd is not None:
+                wgrad(dzd, a["in"], Li, Ci, Lo, Co, 1, s, 0, blk.downsample[0].weight)
+                conv(dzd, Lo, Co, self._wb[id(blk.downsample[0])], tmp, Li, Ci, 1, 1, 0, dil=s)
+                conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=tmp)
+            else:
+                conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=gy, add_mask=a["out"])
+            gcur, nxt = din, gy
+            if bi == 0 or stage_of[bi - 1] != stage_of[bi]:  # stage boundary: close a grad segment
+                if stage_of[bi] == 0:
+                    break  # layer1 joins the stem segment
+                lo = min(self.space.offset_of(p) for p in blocks[bi].parameters())
+                self._segments.append((seg_begin, len(ops), lo, seg_hi))
+                seg_begin, seg_hi = len(ops), lo
+
+        # =============================== stem backward
+        Tb0 = (B * Lz + chunk_for(64) - 1) // chunk_for(64)
+        op("STEM_BWD_REDUCE", P(gcur), P(self.z0), P(bn0.scale), P(bn0.shift), P(bn0.mean), P(bn0.rstd), P(dz0),
+           P(bpart), B, Lz, Lp, 64, chunk_for(64))
+        fin_bwd(bn0, Tb0, B * Lz, 1)
+        op("STEM_WGRAD", P(dz0), P(self.z0), P(bn0.mean), P(bn0.rstd), P(bn0.scale), P(bn0.c1), P(bn0.c2),
+           P(self.x), P(ws), B, L, Lz, Ks, Ss, Ps, stem_chunk)
+        op("REDUCE_SUM", P(ws), stem_blocks, 64 * Ks, self._gptr(c0.weight), 64 * Ks, 0)
+        self._segments.append((seg_begin, len(ops), 0, seg_hi))
+        self._fb_end = len(ops)
+        # =============================== optimizer
+        op("SGD", P(self.flat), P(self.grad), P(self.mom), self.space.param_numel, _f(self.lr), _f(self.momentum),
+           _f(self.wd), int(self.nesterov))
+        self.ops = torch.tensor(ops, dtype=torch.int64)
+        self.n_ops = len(ops)
+        # grad segments must tile [0, param_numel) back to front
+        hi = self.space.param_numel
+        for (_, _, lo, h) in self._segments:
+            assert h == hi, (self._segments, hi)
+            hi = lo
+        assert hi == 0
+
+    # ------------------------------------------------------------------------------------------ execution
+    def _ops_ptr(self, begin: int) -> int:
+        return self.ops.data_ptr() + 8 * OP_WORDS * begin
+
+    def _run(self, begin: int, end: int):
+        bad = ctypes.c_int(-1)
+        st = self.lib.ecg_plan_run(self._ops_ptr(begin), end - begin, ctypes.byref(bad), _lib.stream_ptr(self.dev))
+        if st:
+            raise _lib.NativeError(f"resnet plan op {begin + bad.value} (kind {int(self.ops[begin + bad.value, 0])}) "
+                                   f"failed with status {st}")
+
+    def _graph(self, key: str, begin: int, end: int) -> int:
+        h = self._graphs.get(key)
+        if h is None:
+            hp = ctypes.c_void_p()
+            bad = ctypes.c_int(-1)
+            st = self.lib.ecg_plan_graph_create(ctypes.byref(hp), self._ops_ptr(begin), end - begin,
+                                                ctypes.byref(bad))
+            if st:
+                raise _lib.NativeError(f"resnet plan graph capture failed (status {st}, op {begin + bad.value})")
+            h = self._graphs[key] = hp.value
+        return h
+
+    def _exec(self, key: str, begin: int, end: int):
+        if self.use_graph:
+            st = self.lib.ecg_plan_graph_launch(self._graph(key, begin, end), _lib.stream_ptr(self.dev))
+            _lib.check(st, "ecg_plan_graph_launch")
+        else:
+            self._run(begin, end)
+
+    def set_batch(self, x: torch.Tensor, y: torch.Tensor) -> None:
+        self.x.copy_(x.reshape(self.B, self.L), non_blocking=True)
+        self.y.copy_(y.reshape(self.B), non_blocking=True)
+
+    def forward_backward(self) -> None:
+        """Forward + backward into the flat grad buffer (``grad_sync`` per segment if set)."""
+        if self.grad_sync is None:
+            self._exec("fb", 0, self._fb_end)
+        else:
+            first = self._segments[0][0]
+            self._exec("fwd", 0, first)
+            for i, (b, e, lo, hi) in enumerate(self._segments):
+                self._exec(f"seg{i}", b, e)
+                self.grad_sync(self.grad[lo:hi])
+        self._loss_steps += 1
+        self._steps_since_sync += 1
+
+    def step(self) -> None:
+        if self.grad_sync is None:
+            self._exec("step", 0, self.n_ops)
+            self._loss_steps += 1
+            self._steps_since_sync += 1
+        else:
+            self.forward_backward()
+            self._exec("sgd", self._fb_end, self.n_ops)
+
+    def avg_loss(self) -> float:
+        return float(self.loss_acc.item()) / max(1, self._loss_steps)
+
+    def reset_loss(self) -> None:
+        self.loss_acc.zero_()
+        self._loss_steps = 0
+
+    def reset_momentum(self) -> None:
+        self.mom.zero_()
+
+    def sync_counters(self) -> None:
+        """Bring ``num_batches_tracked`` of every BN up to date (kept off the per-step plan)."""
+        if self._steps_since_sync:
+            with torch.no_grad():
+                for st in self._bn_states:
+                    st.bn.num_batches_tracked += self._steps_since_sync
+            self._steps_since_sync = 0
+
+    def close(self) -> None:
+        for h in self._graphs.values():
+            self.lib.ecg_plan_graph_destroy(h)
+        self._graphs.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

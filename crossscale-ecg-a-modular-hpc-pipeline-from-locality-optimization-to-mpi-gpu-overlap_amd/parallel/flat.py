@@ -21,13 +21,15 @@ class FlatParamSpace:
         self.module = module
         self.entries: List[Tuple[nn.Module, str, bool, int, torch.Size]] = []  # (owner, name, is_param, off, shape)
         off = 0
-        for mod in module.modules():
+        for mod in module.modules():  # parameters first (module order) ...
             for name, p in mod._parameters.items():
                 if p is None:
                     continue
                 self.entries.append((mod, name, True, off, p.shape))
                 off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
-            if include_buffers:
+        self.param_numel = off  # ... so the optimizer runs over flat[:param_numel] only
+        if include_buffers:
+            for mod in module.modules():
                 for name, b in mod._buffers.items():
                     if b is None or not b.is_floating_point():
                         continue
@@ -49,8 +51,8 @@ class FlatParamSpace:
         self.n_params = sum(e[4].numel() for e in self.entries if e[2])
 
     def grad_buffer(self) -> torch.Tensor:
-        """A flat gradient buffer with the same layout; each ``p.grad`` becomes a view into it."""
-        g = torch.zeros_like(self.flat)
+        """A flat gradient buffer over the parameter segment; each ``p.grad`` becomes a view into it."""
+        g = torch.zeros(self.param_numel, dtype=self.flat.dtype, device=self.flat.device)
         for mod, name, is_param, o, shp in self.entries:
             if is_param:
                 p = mod._parameters[name]
@@ -72,3 +74,7 @@ class FlatParamSpace:
             pre = names.get(id(mod), "")
             out[f"{pre}.{name}" if pre else name] = (o, tuple(shp))
         return out
+
+    def offset_of(self, tensor: torch.Tensor) -> int:
+        """Element offset of a parameter / buffer view inside the flat buffer."""
+        return (tensor.data_ptr() - self.flat.data_ptr()) // self.flat.element_size()

@@ -14,13 +14,13 @@
 //             of both staged tiles, so fragments come from gfx950's transposing LDS read ds_read_b64_tr_b16;
 //             the (b,t) range is split over workgroups into fp32 partials (summed deterministically after).
 //
-// Block tile 64x64, BK = 64, 4 waves (2x2, 32x32 each = 2x2 MFMA tiles), double-buffered LDS with the next
-// tile's global loads issued before the current tile's MFMAs (register staging, write after the barrier).
+// Forward block tile 64x64 / 128x64 / 128x128 (by size), BK = 64, 4 waves (2x2), double-buffered LDS with the
+// next tile's global loads issued before the current tile's MFMAs (register staging).
 #include "../include/ecg_common.h"
 
 namespace {
 
-constexpr int BM = 64, BN = 64, BK = 64;
+constexpr int BK = 64;
 constexpr int THREADS = 256;
 constexpr int LDS_ROW = BK + 8;  // bf16 elements per LDS row (+16 B pad: conflict-free ds_read_b128)
 
@@ -31,6 +31,9 @@ struct FwdArgs {
   const __bf16* w;    // [Cout][Kw][Cin]
   const float* bias;  // [Cout] or nullptr
   __bf16* y;          // [B][Lout][Cout]
+  float* stats;       // [2][gridDim.x][Cout] per-M-tile partial sum / sum of squares of the stored outputs, or null
+  const __bf16* add;  // [B*Lout][Cout] added before the store (residual-gradient path), or null
+  const __bf16* add_mask;  // if non-null the added term is add * (add_mask > 0)  (ReLU backward of the residual)
   int B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil, relu;
 };
 
@@ -63,76 +66,197 @@ __device__ __forceinline__ void store_one(__bf16* lds, int e, uint4 v) {
   *reinterpret_cast<uint4*>(lds + (e >> 3) * LDS_ROW + (e & 7) * 8) = v;
 }
 
-__global__ __launch_bounds__(THREADS) void conv1d_nlc_fwd_kernel(FwdArgs a) {
-  __shared__ __attribute__((aligned(16))) __bf16 lds[2][2][BM * LDS_ROW];  // [buf][A/B][row][k]
+// Block tile BM x BN (64/128), 4 waves as 2x2, each wave (BM/2) x (BN/2) = FM x FN MFMA 16x16 tiles.
+// Grid is 1-D over MT*NT tiles with a bijective XCD remap: consecutive tile ids (same M panel, all N tiles)
+// run on one XCD, so the A panel (the activations) is read from HBM once per XCD-L2.
+// Epilogue: accumulators -> LDS (fp32) -> row-major pass with 16-B loads/stores: + bias, + residual
+// (optionally ReLU-masked), ReLU, bf16 round, and per-channel BN partials of the rounded values.
+template <int BM, int BN>
+struct FwdCfg {
+  static constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  static constexpr int NA = BM * 8 / THREADS, NB = BN * 8 / THREADS;
+  static constexpr int A_EL = BM * LDS_ROW, B_EL = BN * LDS_ROW;
+  static constexpr int STAGE_BYTES = 2 * (A_EL + B_EL) * 2;
+  static constexpr int EP_LD = WN + 4;
+  static constexpr int EP_BYTES = 4 * WM * EP_LD * 4 + 2 * 2 * BN * 4;
+  static constexpr int SMEM = STAGE_BYTES > EP_BYTES ? STAGE_BYTES : EP_BYTES;
+};
+
+template <int BM, int BN>
+__global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_kernel(FwdArgs a, int MT, int NT) {
+  using Cfg = FwdCfg<BM, BN>;
+  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NA = Cfg::NA, NB = Cfg::NB;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __bf16* const lds = reinterpret_cast<__bf16*>(smem);  // [buf][A (BM rows) | B (BN rows)][LDS_ROW]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1, wc = wv & 1;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  // bijective XCD remap of the 1-D grid (blockIdx % 8 = blocks sharing an XCD)
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int mt = wgid / NT, nt = wgid % NT;
+  const int m0 = mt * BM, n0 = nt * BN;
   const int K = a.Kw * a.Cin;
   const int nk = K / BK;
-  const int e0 = tid, e1 = tid + THREADS;
-  f32x4 acc[2][2];
+  f32x4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  store_one(lds[0][0], e0, load_a_fwd(a, m0, 0, e0));
-  store_one(lds[0][0], e1, load_a_fwd(a, m0, 0, e1));
-  store_one(lds[0][1], e0, load_b_fwd(a, n0, 0, e0));
-  store_one(lds[0][1], e1, load_b_fwd(a, n0, 0, e1));
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint4 ra[NA], rb[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) ra[i] = load_a_fwd(a, m0, 0, tid + i * THREADS);
+#pragma unroll
+  for (int i = 0; i < NB; ++i) rb[i] = load_b_fwd(a, n0, 0, tid + i * THREADS);
+#pragma unroll
+  for (int i = 0; i < NA; ++i) store_one(lds, tid + i * THREADS, ra[i]);
+#pragma unroll
+  for (int i = 0; i < NB; ++i) store_one(lds + Cfg::A_EL, tid + i * THREADS, rb[i]);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    // issue the next tile's global loads before this tile's MFMAs (the last iteration re-reads its own tile,
-    // keeping the loads unconditional so they stay in registers)
+    // next tile's global loads go out before this tile's MFMAs (last iteration re-reads its own tile so the
+    // loads stay unconditional and register-resident)
     const int kn = (kt + 1 < nk ? kt + 1 : kt) * BK;
-    const uint4 ra0 = load_a_fwd(a, m0, kn, e0), ra1 = load_a_fwd(a, m0, kn, e1);
-    const uint4 rb0 = load_b_fwd(a, n0, kn, e0), rb1 = load_b_fwd(a, n0, kn, e1);
-    const __bf16* As = lds[cur][0];
-    const __bf16* Bs = lds[cur][1];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) ra[i] = load_a_fwd(a, m0, kn, tid + i * THREADS);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) rb[i] = load_b_fwd(a, n0, kn, tid + i * THREADS);
+    const __bf16* As = lds + cur * (Cfg::A_EL + Cfg::B_EL);
+    const __bf16* Bs = As + Cfg::A_EL;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8 af[2], bfr[2];
+      bf16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(As + (wr * 32 + i * 16 + (lane & 15)) * LDS_ROW + ks * 32 +
+      for (int i = 0; i < FM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(As + (wr * WM + i * 16 + (lane & 15)) * LDS_ROW + ks * 32 +
                                                  8 * (lane >> 4));
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (wc * 32 + j * 16 + (lane & 15)) * LDS_ROW + ks * 32 +
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (wc * WN + j * 16 + (lane & 15)) * LDS_ROW + ks * 32 +
                                                   8 * (lane >> 4));
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    __bf16* An = lds[cur ^ 1][0];
-    __bf16* Bn = lds[cur ^ 1][1];
-    store_one(An, e0, ra0);
-    store_one(An, e1, ra1);
-    store_one(Bn, e0, rb0);
-    store_one(Bn, e1, rb1);
+    __bf16* An = lds + (cur ^ 1) * (Cfg::A_EL + Cfg::B_EL);
+#pragma unroll
+    for (int i = 0; i < NA; ++i) store_one(An, tid + i * THREADS, ra[i]);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) store_one(An + Cfg::A_EL, tid + i * THREADS, rb[i]);
     __syncthreads();
   }
-  // epilogue: C layout row = 4*(lane>>4) + i, col = lane & 15
+  // ---- epilogue 1: fragments -> LDS (fp32, per-wave region); staging buffers are dead after the last barrier
+  constexpr int EP_LD = Cfg::EP_LD;
+  float* ep = reinterpret_cast<float*>(smem) + wv * WM * EP_LD;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ep[(i * 16 + 4 * (lane >> 4) + q) * EP_LD + j * 16 + (lane & 15)] = acc[i][j][q];
+  __syncthreads();
+  // ---- epilogue 2: row-major, 8 channels per lane
+  constexpr int CG = WN / 8, RSTEP = 64 / CG, ITEMS = WM / RSTEP;
+  const int cg = lane % CG, rs = lane / CG;
   const int M = a.B * a.Lout;
+  const int n = n0 + wc * WN + cg * 8;
+  float bv[8], s[8], ss[8];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int e = 0; e < 8; ++e) {
+    bv[e] = a.bias ? a.bias[n + e] : 0.f;
+    s[e] = ss[e] = 0.f;
+  }
+#pragma unroll 2
+  for (int it = 0; it < ITEMS; ++it) {
+    const int r = rs + it * RSTEP;
+    const int m = m0 + wr * WM + r;
+    if (m < M) {
+      const long o = (long)m * a.Cout + n;
+      const float4 v0 = *reinterpret_cast<const float4*>(ep + r * EP_LD + cg * 8);
+      const float4 v1 = *reinterpret_cast<const float4*>(ep + r * EP_LD + cg * 8 + 4);
+      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wc * 32 + j * 16 + (lane & 15);
-      const float bv = a.bias ? a.bias[n] : 0.f;
+      for (int e = 0; e < 8; ++e) v[e] += bv[e];
+      if (a.add) {
+        const bf16x8 ad = *reinterpret_cast<const bf16x8*>(a.add + o);
+        if (a.add_mask) {
+          const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.add_mask + o);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = m0 + wr * 32 + i * 16 + 4 * (lane >> 4) + q;
-        if (m < M) {
-          float v = acc[i][j][q] + bv;
-          if (a.relu) v = fmaxf(v, 0.f);
-          a.y[(long)m * a.Cout + n] = (__bf16)v;
+          for (int e = 0; e < 8; ++e) v[e] += (float)mk[e] > 0.f ? (float)ad[e] : 0.f;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += (float)ad[e];
         }
       }
+      bf16x8 outv;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (a.relu) v[e] = fmaxf(v[e], 0.f);
+        outv[e] = (__bf16)v[e];
+        const float rv = (float)outv[e];
+        s[e] += rv;
+        ss[e] += rv * rv;
+      }
+      *reinterpret_cast<bf16x8*>(a.y + o) = outv;
     }
+  }
+  if (a.stats) {  // block-uniform
+#pragma unroll
+    for (int off = CG; off < 64; off <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s[e] += __shfl_xor(s[e], off);
+        ss[e] += __shfl_xor(ss[e], off);
+      }
+    float* sred = reinterpret_cast<float*>(smem) + 4 * WM * EP_LD;  // [wr][stat][BN]
+    if (lane < CG) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sred[(wr * 2 + 0) * BN + wc * WN + cg * 8 + e] = s[e];
+        sred[(wr * 2 + 1) * BN + wc * WN + cg * 8 + e] = ss[e];
+      }
+    }
+    __syncthreads();
+    if (tid < 2 * BN) {
+      const int st = tid / BN, c = tid % BN;
+      a.stats[((long)st * MT + mt) * a.Cout + n0 + c] = sred[st * BN + c] + sred[(2 + st) * BN + c];
+    }
+  }
+}
+
+// Tile choice: 128x128 when that still gives >= 2 workgroups per CU (256 CUs), else 128x64, else 64x64.
+inline void pick_fwd_tile(long M, int Cout, int* bm, int* bn) {
+  const long mt128 = (M + 127) / 128;
+  if (Cout % 128 == 0 && mt128 * (Cout / 128) >= 512) {
+    *bm = 128;
+    *bn = 128;
+  } else if (mt128 * (Cout / 64) >= 512) {
+    *bm = 128;
+    *bn = 64;
+  } else {
+    *bm = 64;
+    *bn = 64;
+  }
+}
+
+template <int BM, int BN>
+int launch_fwd(const FwdArgs& a, hipStream_t stream) {
+  using Cfg = FwdCfg<BM, BN>;
+  static bool attr = false;
+  if (!attr) {
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_kernel<BM, BN>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::SMEM));
+    attr = true;
+  }
+  const long M = (long)a.B * a.Lout;
+  const int MT = (int)((M + BM - 1) / BM), NT = a.Cout / BN;
+  hipLaunchKernelGGL((conv1d_nlc_fwd_kernel<BM, BN>), dim3((unsigned)(MT * NT)), dim3(THREADS), Cfg::SMEM, stream,
+                     a, MT, NT);
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
 }
 
 // ------------------------------------------------------------------------------------------- weight grad
@@ -236,19 +360,36 @@ __global__ __launch_bounds__(THREADS) void conv1d_nlc_wgrad_kernel(WgradArgs a) 
 
 // y = conv(x) (+bias)(+ReLU); x [B][Lin][Cin] bf16, w [Cout][Kw][Cin] bf16, y [B][Lout][Cout] bf16.
 // in_dil > 1 reads x as zero-inserted with that dilation (used for the data-gradient of strided convs).
+// Extended form used by the ResNet step plan: ``stats`` receives [2][ceil(B*Lout/64)][Cout] BN partials;
+// ``add`` (optionally masked by ``add_mask`` > 0) is added to the output before rounding.
+ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bias, void* y, float* stats,
+                                  const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
+                                  int Kw, int stride, int pad, int in_dil, int relu, hipStream_t stream) {
+  if (!x || !w || !y || B <= 0 || Lin <= 0 || Lout <= 0 || Kw <= 0 || stride <= 0 || in_dil <= 0 || pad < 0)
+    return ecg::kBadArg;
+  if (Cin % BK != 0 || Cout % 64 != 0 || (add_mask && !add)) return ecg::kBadArg;
+  FwdArgs a{static_cast<const __bf16*>(x), static_cast<const __bf16*>(w), bias, static_cast<__bf16*>(y), stats,
+            static_cast<const __bf16*>(add), static_cast<const __bf16*>(add_mask),
+            B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil, relu};
+  int bm, bn;
+  pick_fwd_tile((long)B * Lout, Cout, &bm, &bn);
+  if (bm == 128 && bn == 128) return launch_fwd<128, 128>(a, stream);
+  if (bm == 128) return launch_fwd<128, 64>(a, stream);
+  return launch_fwd<64, 64>(a, stream);
+}
+
+// Number of M tiles (rows of the BN-statistics partials) the forward kernel uses for this shape.
+ECG_API int ecg_conv1d_nlc_fwd_stat_tiles(long M, int Cout) {
+  int bm, bn;
+  pick_fwd_tile(M, Cout, &bm, &bn);
+  return (int)((M + bm - 1) / bm);
+}
+
 ECG_API int ecg_conv1d_nlc_fwd(const void* x, const void* w, const float* bias, void* y, int B, int Lin, int Cin,
                                int Lout, int Cout, int Kw, int stride, int pad, int in_dil, int relu,
                                hipStream_t stream) {
-  if (!x || !w || !y || B <= 0 || Lin <= 0 || Lout <= 0 || Kw <= 0 || stride <= 0 || in_dil <= 0 || pad < 0)
-    return ecg::kBadArg;
-  if (Cin % BK != 0 || Cout % BN != 0) return ecg::kBadArg;
-  FwdArgs a{static_cast<const __bf16*>(x), static_cast<const __bf16*>(w), bias, static_cast<__bf16*>(y),
-            B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil, relu};
-  const long M = (long)B * Lout;
-  dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)(Cout / BN));
-  hipLaunchKernelGGL(conv1d_nlc_fwd_kernel, grid, dim3(THREADS), 0, stream, a);
-  ECG_HIP_CHECK(hipGetLastError());
-  return ecg::kOk;
+  return ecg_conv1d_nlc_fwd_ex(x, w, bias, y, nullptr, nullptr, nullptr, B, Lin, Cin, Lout, Cout, Kw, stride, pad,
+                               in_dil, relu, stream);
 }
 
 // Partial weight gradients: part[splits][Cout][Kw*Cin] fp32 (sum over dim 0 = dw in [Cout][Kw][Cin]).

@@ -1,0 +1,986 @@
+// ResNet1D training-step engine for gfx950: channels-last (NLC) bf16 activations, fp32 master weights in one
+// flat buffer, BatchNorm in training mode, and a native "step plan" executor that replays the whole
+// forward + backward + SGD step as a list of kernel launches - eagerly or as ONE hipGraph.
+//
+// BASELINE.json config 5 ("Deeper ResNet1D-34 ECG, large-batch bf16 ... scaling stress").
+// Not in the reference (its only model is TinyECG, Module_1/bench_locality.py:8-21); the conv kernels are the
+// MFMA implicit GEMMs of conv1d_mc.hip, everything around them lives here:
+//
+//   stem      conv(1->64, k7, s2, p3) on VALU (C_in = 1 has no GEMM shape) with fused BN statistics,
+//             BN + ReLU + MaxPool(3,2,1) in one pass; backward re-derives the pool argmax (no index tensor).
+//   BN        statistics come out of the producing conv's epilogue (per-64-row-tile partials), a ticketed
+//             finalize kernel reduces them (fp64) and emits scale/shift + running stats in ONE launch;
+//             apply kernels fuse ReLU and the residual (identity or the downsample branch's own BN).
+//   BN bwd    one reduce pass (sum dz, sum dz*xhat [, sum dz*xhat_ds]) + one apply pass; the identity
+//             residual gradient is folded into the data-grad conv's epilogue (add * (out > 0)).
+//   head      global average pool + Linear + softmax cross-entropy + its gradient, one block per sample, and
+//             a deterministic split reduction for dW / db / loss.
+//   weights   one launch converts every conv weight of the flat fp32 master buffer into the bf16 forward
+//             layout [Cout][K][Cin] and the flipped data-grad layout [Cin][K][Cout].
+//   SGD       the flat-buffer SGD kernel (fused_sgd.hip) over all parameters at once.
+//
+// All reductions have a fixed order: the step is bitwise deterministic for a given batch.
+#include "../include/ecg_common.h"
+
+#include <math.h>
+#include <string.h>
+#include <vector>
+
+extern "C" int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bias, void* y, float* stats,
+                                     const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout,
+                                     int Cout, int Kw, int stride, int pad, int in_dil, int relu, hipStream_t stream);
+extern "C" int ecg_conv1d_nlc_wgrad(const void* dy, const void* x, float* part, int splits, int B, int Lin, int Cin,
+                                    int Lout, int Cout, int Kw, int stride, int pad, hipStream_t stream);
+extern "C" int ecg_sgd_flat(float* params, const float* grads, float* mom, long n, float lr, float momentum,
+                            float dampening, float wd, int nesterov, int first, float inv_scale, int* found_inf,
+                            hipStream_t stream);
+
+namespace {
+
+constexpr int TPB = 256;
+
+__device__ __forceinline__ void ld8(const __bf16* p, float* f) {
+  const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = (float)v[i];
+}
+__device__ __forceinline__ void st8(__bf16* p, const float* f) {
+  bf16x8 v;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (__bf16)f[i];
+  *reinterpret_cast<bf16x8*>(p) = v;
+}
+__device__ __forceinline__ void ldf8(const float* p, float* f) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+// ------------------------------------------------------------------------------------------------ stem
+// y[b,t,c] = sum_k w[c,k] x[b, t*s + k - p]; block = 64 rows x 64 channels; stats partial per block.
+__global__ __launch_bounds__(TPB) void stem_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                       __bf16* __restrict__ y, float* __restrict__ stats, int B,
+                                                       int L, int Lo, int K, int stride, int pad) {
+  __shared__ float red[4][2][64];
+  const int tid = threadIdx.x, c = tid & 63, rg = tid >> 6;
+  float wk[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) wk[k] = k < K ? w[c * K + k] : 0.f;
+  const long M = (long)B * Lo;
+  float s = 0.f, ss = 0.f;
+  for (int i = 0; i < 16; ++i) {
+    const long m = (long)blockIdx.x * 64 + rg * 16 + i;
+    if (m >= M) break;
+    const int b = (int)(m / Lo), t = (int)(m % Lo);
+    const float* xb = x + (long)b * L;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int u = t * stride + k - pad;
+      if (k < K && u >= 0 && u < L) acc += wk[k] * xb[u];
+    }
+    const __bf16 r = (__bf16)acc;
+    y[m * 64 + c] = r;
+    const float rv = (float)r;
+    s += rv;
+    ss += rv * rv;
+  }
+  red[rg][0][c] = s;
+  red[rg][1][c] = ss;
+  __syncthreads();
+  if (tid < 128) {
+    const int st = tid >> 6;
+    stats[((long)st * gridDim.x + blockIdx.x) * 64 + c] = red[0][st][c] + red[1][st][c] + red[2][st][c] + red[3][st][c];
+  }
+}
+
+// out[b,o,c] = max_{j in {2o-1,2o,2o+1}} relu(z[b,j,c]*scale[c] + shift[c])   (MaxPool1d(3, 2, 1))
+__global__ __launch_bounds__(TPB) void stem_pool_kernel(const __bf16* __restrict__ z, const float* __restrict__ scale,
+                                                        const float* __restrict__ shift, __bf16* __restrict__ out,
+                                                        int B, int Lz, int Lp, int C) {
+  const int cg = C / 8;
+  const long nv = (long)B * Lp * cg;
+  for (long v = (long)blockIdx.x * TPB + threadIdx.x; v < nv; v += (long)gridDim.x * TPB) {
+    const int c0 = (int)(v % cg) * 8;
+    const long bo = v / cg;
+    const int o = (int)(bo % Lp), b = (int)(bo / Lp);
+    float sc[8], sh[8], mx[8];
+    ldf8(scale + c0, sc);
+    ldf8(shift + c0, sh);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mx[i] = -INFINITY;
+#pragma unroll
+    for (int d = -1; d <= 1; ++d) {
+      const int j = 2 * o + d;
+      if (j < 0 || j >= Lz) continue;
+      float zf[8];
+      ld8(z + ((long)b * Lz + j) * C + c0, zf);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mx[i] = fmaxf(mx[i], fmaxf(zf[i] * sc[i] + sh[i], 0.f));
+    }
+    st8(out + bo * C + c0, mx);
+  }
+}
+
+// Backward of ReLU(BN(z)) -> MaxPool: dz[b,j,c] = (a_j > 0) * sum_{windows o whose first argmax is j} gp[b,o,c]
+// (written bf16) and BN partials sum(dz), sum(dz * xhat) per block of rows.
+__global__ __launch_bounds__(TPB) void stem_bwd_reduce_kernel(
+    const __bf16* __restrict__ gp, const __bf16* __restrict__ z, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ mean, const float* __restrict__ rstd,
+    __bf16* __restrict__ dz, float* __restrict__ part, int B, int Lz, int Lp, int C, int chunk) {
+  __shared__ float red[TPB * 16];
+  const int cg = C / 8, tid = threadIdx.x;
+  const int rpp = TPB / cg, roff = tid / cg, c0 = (tid % cg) * 8;
+  const bool active = roff < rpp;  // C/8 need not divide the block: spare threads idle
+  const long R = (long)B * Lz;
+  float sc[8], sh[8], mu[8], rs[8], a1[8], a2[8];
+  ldf8(scale + c0, sc);
+  ldf8(shift + c0, sh);
+  ldf8(mean + c0, mu);
+  ldf8(rstd + c0, rs);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a1[i] = a2[i] = 0.f;
+  const long r1 = active ? min(R, (long)(blockIdx.x + 1) * chunk) : 0;
+  for (long r = (long)blockIdx.x * chunk + roff; r < r1; r += rpp) {
+    const int b = (int)(r / Lz), j = (int)(r % Lz);
+    const __bf16* zb = z + (long)b * Lz * C + c0;
+    float zj[8], g[8];
+    ld8(zb + (long)j * C, zj);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = 0.f;
+    const int olo = j >> 1, ohi = min(Lp - 1, (j + 1) >> 1);  // windows containing j
+    for (int o = olo; o <= ohi; ++o) {
+      float best[8];
+      int arg[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { best[i] = -INFINITY; arg[i] = -1; }
+#pragma unroll
+      for (int d = -1; d <= 1; ++d) {
+        const int p = 2 * o + d;
+        if (p < 0 || p >= Lz) continue;
+        float zp[8];
+        ld8(zb + (long)p * C, zp);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float av = fmaxf(zp[i] * sc[i] + sh[i], 0.f);
+          if (av > best[i]) { best[i] = av; arg[i] = p; }
+        }
+      }
+      float go[8];
+      ld8(gp + ((long)b * Lp + o) * C + c0, go);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (arg[i] == j) g[i] += go[i];
+    }
+    float d[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float av = zj[i] * sc[i] + sh[i];
+      d[i] = av > 0.f ? g[i] : 0.f;
+    }
+    st8(dz + r * C + c0, d);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float dv = (float)(__bf16)d[i];
+      a1[i] += dv;
+      a2[i] += dv * (zj[i] - mu[i]) * rs[i];
+    }
+  }
+  // reduce over the rpp row groups: red[roff][stat][c]
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[(roff * 2 + 0) * C + c0 + i] = a1[i];
+      red[(roff * 2 + 1) * C + c0 + i] = a2[i];
+    }
+  }
+  __syncthreads();
+  const int T = gridDim.x;
+  for (int idx = tid; idx < 2 * C; idx += TPB) {
+    const int st = idx / C, c = idx % C;
+    float v = 0.f;
+    for (int q = 0; q < rpp; ++q) v += red[(q * 2 + st) * C + c];
+    part[((long)st * T + blockIdx.x) * C + c] = v;
+  }
+}
+
+// dW[c,k] partials: sum over rows of dzz[b,j,c] * x[b, j*s + k - p], dzz = scale*(dz - c1 - xhat*c2)
+__global__ __launch_bounds__(TPB) void stem_wgrad_kernel(
+    const __bf16* __restrict__ dz, const __bf16* __restrict__ z, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ scale, const float* __restrict__ c1,
+    const float* __restrict__ c2, const float* __restrict__ x, float* __restrict__ part, int B, int L, int Lz, int K,
+    int stride, int pad, int chunk) {
+  __shared__ float red[4][64 * 8];
+  const int tid = threadIdx.x, c = tid & 63, rg = tid >> 6;
+  const float mu = mean[c], rs = rstd[c], sc = scale[c], k1 = c1[c], k2 = c2[c];
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  const long R = (long)B * Lz;
+  const long r1 = min(R, (long)(blockIdx.x + 1) * chunk);
+  long r = (long)blockIdx.x * chunk + rg;
+  for (; r + 12 < r1; r += 16) {  // 4 rows in flight per thread
+    float gz[4], xz[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long ru = r + 4 * u;
+      const int b = (int)(ru / Lz), j = (int)(ru % Lz);
+      const float xh = ((float)z[ru * 64 + c] - mu) * rs;
+      gz[u] = sc * ((float)dz[ru * 64 + c] - k1 - xh * k2);
+      const float* xb = x + (long)b * L;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int uu = j * stride + k - pad;
+        xz[u][k] = (k < K && uu >= 0 && uu < L) ? xb[uu] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += gz[u] * xz[u][k];
+  }
+  for (; r < r1; r += 4) {
+    const int b = (int)(r / Lz), j = (int)(r % Lz);
+    const float xh = ((float)z[r * 64 + c] - mu) * rs;
+    const float g = sc * ((float)dz[r * 64 + c] - k1 - xh * k2);
+    const float* xb = x + (long)b * L;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int u = j * stride + k - pad;
+      if (k < K && u >= 0 && u < L) acc[k] += g * xb[u];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[rg][c * 8 + k] = acc[k];
+  __syncthreads();
+  for (int idx = tid; idx < 64 * K; idx += TPB) {
+    const int cc = idx / K, k = idx % K;
+    part[(long)blockIdx.x * 64 * K + idx] =
+        red[0][cc * 8 + k] + red[1][cc * 8 + k] + red[2][cc * 8 + k] + red[3][cc * 8 + k];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ BatchNorm
+struct FinArgs {
+  const float* sA;  // [T][C] partials of stat A (fwd: sum x; bwd: sum dz)
+  const float* sB;  // [T][C] partials of stat B (fwd: sum x^2; bwd: sum dz*xhat)
+  int T, C, mode;   // mode 0 = forward statistics, 1 = backward coefficients
+  double* scratch;  // [gridDim.y][2][C]
+  unsigned* ticket; // [gridDim.x], zero between launches (the last block resets it)
+  float n, eps, momentum;
+  const float* gamma;
+  const float* beta;
+  float* mean;
+  float* rstd;
+  float* scale;  // gamma * rstd
+  float* shift;  // beta - mean * scale
+  float* run_mean;
+  float* run_var;
+  float* dgamma;
+  float* dbeta;
+  float* c1;  // sum dz / n
+  float* c2;  // sum dz*xhat / n
+};
+
+__global__ __launch_bounds__(TPB) void bn_finalize_kernel(FinArgs a) {
+  __shared__ double red[4][2][64];
+  __shared__ unsigned last;
+  const int tid = threadIdx.x, cl = tid & 63, g4 = tid >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int G = gridDim.y;
+  const int t0 = (int)((long)a.T * blockIdx.y / G), t1 = (int)((long)a.T * (blockIdx.y + 1) / G);
+  double s1 = 0.0, s2 = 0.0;
+  for (int t = t0 + g4; t < t1; t += 4) {
+    s1 += (double)a.sA[(long)t * a.C + c];
+    s2 += (double)a.sB[(long)t * a.C + c];
+  }
+  red[g4][0][cl] = s1;
+  red[g4][1][cl] = s2;
+  __syncthreads();
+  if (tid < 64) {
+    const double v1 = red[0][0][cl] + red[1][0][cl] + red[2][0][cl] + red[3][0][cl];
+    const double v2 = red[0][1][cl] + red[1][1][cl] + red[2][1][cl] + red[3][1][cl];
+    a.scratch[((long)blockIdx.y * 2 + 0) * a.C + c] = v1;
+    a.scratch[((long)blockIdx.y * 2 + 1) * a.C + c] = v2;
+  }
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) last = atomicAdd(&a.ticket[blockIdx.x], 1u) == (unsigned)(G - 1);
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  {  // last block: all 256 threads sum the G level-2 partials (device-coherent loads, 4 in flight per thread)
+    double v1 = 0.0, v2 = 0.0;
+    int g = g4;
+    for (; g + 12 < G; g += 16) {
+      double t1[4], t2[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        t1[u] = __hip_atomic_load(&a.scratch[((long)(g + 4 * u) * 2 + 0) * a.C + c], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+        t2[u] = __hip_atomic_load(&a.scratch[((long)(g + 4 * u) * 2 + 1) * a.C + c], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v1 += t1[u];
+        v2 += t2[u];
+      }
+    }
+    for (; g < G; g += 4) {
+      v1 += __hip_atomic_load(&a.scratch[((long)g * 2 + 0) * a.C + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v2 += __hip_atomic_load(&a.scratch[((long)g * 2 + 1) * a.C + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    red[g4][0][cl] = v1;
+    red[g4][1][cl] = v2;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const double v1 = red[0][0][cl] + red[1][0][cl] + red[2][0][cl] + red[3][0][cl];
+    const double v2 = red[0][1][cl] + red[1][1][cl] + red[2][1][cl] + red[3][1][cl];
+    const double n = (double)a.n;
+    if (a.mode == 0) {
+      const double mu = v1 / n;
+      const double var = fmax(v2 / n - mu * mu, 0.0);
+      const float rs = (float)(1.0 / sqrt(var + (double)a.eps));
+      const float sc = a.gamma[c] * rs;
+      a.mean[c] = (float)mu;
+      a.rstd[c] = rs;
+      a.scale[c] = sc;
+      a.shift[c] = a.beta[c] - (float)mu * sc;
+      if (a.run_mean) {
+        const float m = a.momentum;
+        a.run_mean[c] = (1.f - m) * a.run_mean[c] + m * (float)mu;
+        a.run_var[c] = (1.f - m) * a.run_var[c] + m * (float)(var * n / fmax(n - 1.0, 1.0));
+      }
+    } else {
+      if (a.dbeta) a.dbeta[c] = (float)v1;
+      if (a.dgamma) a.dgamma[c] = (float)v2;
+      a.c1[c] = (float)(v1 / n);
+      a.c2[c] = (float)(v2 / n);
+    }
+  }
+  if (tid == 0) a.ticket[blockIdx.x] = 0u;
+}
+
+// MODE 0: out = relu(z*scale + shift); 1: out = relu(z*scale + shift + res); 2: + (zd*scale_d + shift_d)
+template <int MODE>
+__global__ __launch_bounds__(TPB) void bn_act_kernel(const __bf16* __restrict__ z, const float* __restrict__ scale,
+                                                     const float* __restrict__ shift, const __bf16* __restrict__ res,
+                                                     const float* __restrict__ scale_d,
+                                                     const float* __restrict__ shift_d, __bf16* __restrict__ out,
+                                                     long R, int C) {
+  const int cg = C / 8;
+  const long nv = R * cg;
+  for (long v = (long)blockIdx.x * TPB + threadIdx.x; v < nv; v += (long)gridDim.x * TPB) {
+    const int c0 = (int)(v % cg) * 8;
+    const long o = v * 8;
+    float zf[8], sc[8], sh[8], y[8];
+    ld8(z + o, zf);
+    ldf8(scale + c0, sc);
+    ldf8(shift + c0, sh);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) y[i] = zf[i] * sc[i] + sh[i];
+    if (MODE >= 1) {
+      float rf[8];
+      ld8(res + o, rf);
+      if (MODE == 2) {
+        float sd[8], hd[8];
+        ldf8(scale_d + c0, sd);
+        ldf8(shift_d + c0, hd);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) rf[i] = rf[i] * sd[i] + hd[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) y[i] += rf[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) y[i] = fmaxf(y[i], 0.f);
+    st8(out + o, y);
+  }
+}
+
+// dz = gy * (mask_src > 0); partial sums of dz, dz*xhat (and dz*xhat_d when NS == 3) per block of rows.
+template <int NS>
+__global__ __launch_bounds__(TPB) void bn_bwd_reduce_kernel(
+    const __bf16* __restrict__ gy, const __bf16* __restrict__ msk, const __bf16* __restrict__ z,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const __bf16* __restrict__ zd,
+    const float* __restrict__ mean_d, const float* __restrict__ rstd_d, float* __restrict__ part, long R, int C,
+    int chunk) {
+  __shared__ float red[TPB * 8 * 3];
+  const int cg = C / 8, tid = threadIdx.x;
+  const int rpp = TPB / cg, roff = tid / cg, c0 = (tid % cg) * 8;
+  const bool active = roff < rpp;
+  float mu[8], rs[8], mud[8], rsd[8], a1[8], a2[8], a3[8];
+  ldf8(mean + c0, mu);
+  ldf8(rstd + c0, rs);
+  if (NS == 3) {
+    ldf8(mean_d + c0, mud);
+    ldf8(rstd_d + c0, rsd);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a1[i] = a2[i] = a3[i] = 0.f;
+  const long r1 = active ? min(R, (long)(blockIdx.x + 1) * chunk) : 0;
+  for (long r = (long)blockIdx.x * chunk + roff; r < r1; r += rpp) {
+    const long o = r * C + c0;
+    float g[8], m[8], zf[8];
+    ld8(gy + o, g);
+    ld8(msk + o, m);
+    ld8(z + o, zf);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float d = m[i] > 0.f ? g[i] : 0.f;
+      a1[i] += d;
+      a2[i] += d * (zf[i] - mu[i]) * rs[i];
+    }
+    if (NS == 3) {
+      float zdf[8];
+      ld8(zd + o, zdf);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = m[i] > 0.f ? g[i] : 0.f;
+        a3[i] += d * (zdf[i] - mud[i]) * rsd[i];
+      }
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[(roff * NS + 0) * C + c0 + i] = a1[i];
+      red[(roff * NS + 1) * C + c0 + i] = a2[i];
+      if (NS == 3) red[(roff * NS + 2) * C + c0 + i] = a3[i];
+    }
+  }
+  __syncthreads();
+  const int T = gridDim.x;
+  for (int idx = tid; idx < NS * C; idx += TPB) {
+    const int st = idx / C, c = idx % C;
+    float v = 0.f;
+    for (int q = 0; q < rpp; ++q) v += red[(q * NS + st) * C + c];
+    part[((long)st * T + blockIdx.x) * C + c] = v;
+  }
+}
+
+// dzz = scale*(dz - c1 - xhat*c2) with dz = gy*(mask > 0); DS: also dzd = scale_d*(dz - c1 - xhat_d*c2_d)
+template <bool DS>
+__global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(
+    const __bf16* __restrict__ gy, const __bf16* __restrict__ msk, const __bf16* __restrict__ z,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ scale,
+    const float* __restrict__ c1, const float* __restrict__ c2, __bf16* __restrict__ out,
+    const __bf16* __restrict__ zd, const float* __restrict__ mean_d, const float* __restrict__ rstd_d,
+    const float* __restrict__ scale_d, const float* __restrict__ c2_d, __bf16* __restrict__ out_d, long R, int C) {
+  const int cg = C / 8;
+  const long nv = R * cg;
+  for (long v = (long)blockIdx.x * TPB + threadIdx.x; v < nv; v += (long)gridDim.x * TPB) {
+    const int c0 = (int)(v % cg) * 8;
+    const long o = v * 8;
+    float g[8], m[8], zf[8], mu[8], rs[8], sc[8], k1[8], k2[8], y[8];
+    ld8(gy + o, g);
+    ld8(msk + o, m);
+    ld8(z + o, zf);
+    ldf8(mean + c0, mu);
+    ldf8(rstd + c0, rs);
+    ldf8(scale + c0, sc);
+    ldf8(c1 + c0, k1);
+    ldf8(c2 + c0, k2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      g[i] = m[i] > 0.f ? g[i] : 0.f;
+      y[i] = sc[i] * (g[i] - k1[i] - (zf[i] - mu[i]) * rs[i] * k2[i]);
+    }
+    st8(out + o, y);
+    if (DS) {
+      ld8(zd + o, zf);
+      ldf8(mean_d + c0, mu);
+      ldf8(rstd_d + c0, rs);
+      ldf8(scale_d + c0, sc);
+      ldf8(c2_d + c0, k2);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) y[i] = sc[i] * (g[i] - k1[i] - (zf[i] - mu[i]) * rs[i] * k2[i]);
+      st8(out_d + o, y);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ head
+// One block per sample: feat = mean_t h[b,t,:]; logits = W feat + bias; CE loss; g = (softmax - onehot)/B;
+// gh[b,t,c] = (W^T g)[c] / Lf.  Stores g, feat and loss/B for the split reduction.
+constexpr int MAXC = 16;
+__global__ __launch_bounds__(TPB) void head_fwd_bwd_kernel(const __bf16* __restrict__ h, const float* __restrict__ W,
+                                                           const float* __restrict__ bias,
+                                                           const int* __restrict__ labels, __bf16* __restrict__ gh,
+                                                           float* __restrict__ gbuf, float* __restrict__ fbuf,
+                                                           float* __restrict__ lbuf, int B, int Lf, int C, int ncls) {
+  __shared__ float feat[1024];
+  __shared__ float wred[TPB / 64][MAXC];
+  __shared__ float gs[MAXC];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const __bf16* hb = h + (long)b * Lf * C;
+  const float invL = 1.f / (float)Lf;
+  for (int c = tid; c < C; c += TPB) {
+    float s = 0.f;
+    for (int t = 0; t < Lf; ++t) s += (float)hb[(long)t * C + c];
+    s *= invL;
+    feat[c] = s;
+    fbuf[(long)b * C + c] = s;
+  }
+  __syncthreads();
+  for (int j = 0; j < ncls; ++j) {
+    float p = 0.f;
+    for (int c = tid; c < C; c += TPB) p += W[(long)j * C + c] * feat[c];
+    p = ecg::wave_sum(p);
+    if (lane == 0) wred[wv][j] = p;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float lg[MAXC], mx = -INFINITY;
+    for (int j = 0; j < ncls; ++j) {
+      float v = bias[j];
+      for (int q = 0; q < TPB / 64; ++q) v += wred[q][j];
+      lg[j] = v;
+      mx = fmaxf(mx, v);
+    }
+    float se = 0.f;
+    for (int j = 0; j < ncls; ++j) se += expf(lg[j] - mx);
+    const int y = labels[b];
+    const float lse = mx + logf(se);
+    lbuf[b] = (lse - lg[y]) / (float)B;
+    for (int j = 0; j < ncls; ++j) {
+      const float g = (expf(lg[j] - lse) - (j == y ? 1.f : 0.f)) / (float)B;
+      gs[j] = g;
+      gbuf[(long)b * ncls + j] = g;
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += TPB) {
+    float d = 0.f;
+    for (int j = 0; j < ncls; ++j) d += gs[j] * W[(long)j * C + c];
+    const __bf16 v = (__bf16)(d * invL);
+    for (int t = 0; t < Lf; ++t) gh[((long)b * Lf + t) * C + c] = v;
+  }
+}
+
+// partial[gb][j*C + c] = sum_{b in slice} g[b,j] feat[b,c]; [ncls*C + j] = sum g[b,j]; [ncls*C + ncls] = sum loss
+__global__ __launch_bounds__(TPB) void head_reduce_kernel(const float* __restrict__ gbuf,
+                                                          const float* __restrict__ fbuf,
+                                                          const float* __restrict__ lbuf, float* __restrict__ part,
+                                                          int B, int C, int ncls) {
+  __shared__ float red[4][64][MAXC + 1];
+  const int tid = threadIdx.x, cl = tid & 63, g4 = tid >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int Gb = gridDim.y;
+  const int b0 = (int)((long)B * blockIdx.y / Gb), b1 = (int)((long)B * (blockIdx.y + 1) / Gb);
+  float acc[MAXC + 1];
+#pragma unroll
+  for (int j = 0; j <= MAXC; ++j) acc[j] = 0.f;
+  const bool extra = blockIdx.x == 0 && cl < 1;
+  for (int b = b0 + g4; b < b1; b += 4) {
+    const float f = c < C ? fbuf[(long)b * C + c] : 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXC; ++j)
+      if (j < ncls) acc[j] += gbuf[(long)b * ncls + j] * f;
+    if (extra) acc[MAXC] += lbuf[b];
+  }
+#pragma unroll
+  for (int j = 0; j <= MAXC; ++j) red[g4][cl][j] = acc[j];
+  __syncthreads();
+  const long N = (long)ncls * C + ncls + 1;
+  float* out = part + (long)blockIdx.y * N;
+  if (tid < 64 && c < C) {
+    for (int j = 0; j < ncls; ++j)
+      out[(long)j * C + c] = red[0][cl][j] + red[1][cl][j] + red[2][cl][j] + red[3][cl][j];
+  }
+  if (blockIdx.x == 0 && tid < ncls + 1) {  // db[j] = sum_b g[b,j] (own pass: tiny), loss
+    float v = 0.f;
+    if (tid < ncls) {
+      for (int b = b0; b < b1; ++b) v += gbuf[(long)b * ncls + tid];
+    } else {
+      v = red[0][0][MAXC] + red[1][0][MAXC] + red[2][0][MAXC] + red[3][0][MAXC];
+    }
+    out[(long)ncls * C + tid] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ reductions
+// out[i] = sum_s part[s*N + i] for i < split; out2[i - split] += sum for i >= split (accumulating tail).
+// Block = 64 columns x 16 split groups (1024 threads), 4 loads in flight per thread, fixed-order LDS combine.
+constexpr int RS_GROUPS = 16;
+__global__ __launch_bounds__(64 * RS_GROUPS) void reduce_sum_kernel(const float* __restrict__ part, int S, long N,
+                                                                    float* __restrict__ out, long split,
+                                                                    float* __restrict__ out2) {
+  __shared__ float red[RS_GROUPS][64];
+  const int col = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const long i = (long)blockIdx.x * 64 + col;
+  float v = 0.f;
+  if (i < N) {
+    int s = sg;
+    for (; s + 3 * RS_GROUPS < S; s += 4 * RS_GROUPS) {
+      float t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[u] = part[(long)(s + u * RS_GROUPS) * N + i];
+      v += (t[0] + t[1]) + (t[2] + t[3]);
+    }
+    for (; s < S; s += RS_GROUPS) v += part[(long)s * N + i];
+  }
+  red[sg][col] = v;
+  __syncthreads();
+  if (sg == 0 && i < N) {
+    float r = 0.f;
+#pragma unroll
+    for (int q = 0; q < RS_GROUPS; ++q) r += red[q][col];
+    if (i < split) out[i] = r;
+    else out2[i - split] += r;
+  }
+}
+
+// grad[co][ci][k] = sum_s part[s][co][k*Cin + ci]  (nn.Conv1d weight layout).  Block = 64 float4 columns of
+// the source layout x 4 split groups (coalesced 16-B loads, 4 independent chains), reduced through LDS, then
+// scattered into the parameter layout.  N = Cout*K*Cin is a multiple of 4096 (C_in, C_out % 64 == 0).
+__global__ __launch_bounds__(TPB) void reduce_wgrad_kernel(const float* __restrict__ part, int S, int Cout, int K,
+                                                           int Cin, float* __restrict__ grad) {
+  __shared__ float4 red[4][64];
+  const long N = (long)Cout * K * Cin;
+  const int tid = threadIdx.x, col = tid & 63, sg = tid >> 6;
+  const long i4 = (long)blockIdx.x * 64 + col;  // float4 index
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  const long N4 = N / 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i4 < N4) {
+    int s = sg;
+    for (; s + 12 < S; s += 16) {
+      float4 t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[u] = p4[(long)(s + 4 * u) * N4 + i4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc.x += t[u].x; acc.y += t[u].y; acc.z += t[u].z; acc.w += t[u].w;
+      }
+    }
+    for (; s < S; s += 4) {
+      const float4 t = p4[(long)s * N4 + i4];
+      acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+    }
+  }
+  red[sg][col] = acc;
+  __syncthreads();
+  if (sg == 0 && i4 < N4) {
+    float4 v = red[0][col];
+    for (int q = 1; q < 4; ++q) {
+      v.x += red[q][col].x; v.y += red[q][col].y; v.z += red[q][col].z; v.w += red[q][col].w;
+    }
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const long src = i4 * 4 + e;  // = co*K*Cin + k*Cin + ci
+      const int ci = (int)(src % Cin);
+      const long r = src / Cin;
+      const int k = (int)(r % K), co = (int)(r / K);
+      grad[((long)co * Cin + ci) * K + k] = vv[e];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ weights
+struct WEntry {
+  long src;  // offset (elements) of the fp32 [Cout][Cin][K] weight in the flat buffer
+  long wf;   // offset of the bf16 [Cout][K][Cin] copy
+  long wb;   // offset of the bf16 [Cin][K][Cout] flipped copy (data-grad)
+  int Cout, Cin, K, block0;
+};
+
+__global__ __launch_bounds__(TPB) void weight_prep_kernel(const WEntry* __restrict__ tab, int n,
+                                                          const float* __restrict__ flat, __bf16* __restrict__ arena) {
+  __shared__ int sel;
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int i = 1; i < n; ++i)
+      if ((int)blockIdx.x >= tab[i].block0) s = i;
+    sel = s;
+  }
+  __syncthreads();
+  const WEntry e = tab[sel];
+  const long N = (long)e.Cout * e.Cin * e.K;
+  const long i = ((long)blockIdx.x - e.block0) * TPB + threadIdx.x;
+  if (i >= N) return;
+  const int k = (int)(i % e.K);
+  const long r = i / e.K;
+  const int ci = (int)(r % e.Cin), co = (int)(r / e.Cin);
+  const __bf16 v = (__bf16)flat[e.src + i];
+  arena[e.wf + ((long)co * e.K + k) * e.Cin + ci] = v;
+  arena[e.wb + ((long)ci * e.K + (e.K - 1 - k)) * e.Cout + co] = v;
+}
+
+inline unsigned grid_for(long n, long per_block = TPB, long cap = 8192) {
+  long g = (n + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+// ------------------------------------------------------------------------------------------------ plan
+enum OpKind : int {
+  OP_CONV_FWD = 1,
+  OP_CONV_WGRAD = 2,
+  OP_REDUCE_WGRAD = 3,
+  OP_BN_FIN = 4,
+  OP_BN_ACT = 5,
+  OP_BN_BWD_REDUCE = 6,
+  OP_BN_BWD_APPLY = 7,
+  OP_STEM_FWD = 8,
+  OP_STEM_POOL = 9,
+  OP_STEM_BWD_REDUCE = 10,
+  OP_STEM_WGRAD = 11,
+  OP_REDUCE_SUM = 12,
+  OP_WEIGHT_PREP = 13,
+  OP_HEAD = 14,
+  OP_HEAD_REDUCE = 15,
+  OP_SGD = 16,
+};
+constexpr int OP_WORDS = 32;
+
+template <typename T>
+inline T* P(int64_t v) { return reinterpret_cast<T*>(static_cast<intptr_t>(v)); }
+inline float F(int64_t v) {
+  double d;
+  memcpy(&d, &v, sizeof d);
+  return (float)d;
+}
+
+int run_op(const int64_t* o, hipStream_t st) {
+  const int kind = (int)o[0];
+  switch (kind) {
+    case OP_CONV_FWD:
+      return ecg_conv1d_nlc_fwd_ex(P<void>(o[1]), P<void>(o[2]), P<float>(o[3]), P<void>(o[4]), P<float>(o[5]),
+                                   P<void>(o[6]), P<void>(o[7]), (int)o[8], (int)o[9], (int)o[10], (int)o[11],
+                                   (int)o[12], (int)o[13], (int)o[14], (int)o[15], (int)o[16], (int)o[17], st);
+    case OP_CONV_WGRAD:
+      return ecg_conv1d_nlc_wgrad(P<void>(o[1]), P<void>(o[2]), P<float>(o[3]), (int)o[4], (int)o[5], (int)o[6],
+                                  (int)o[7], (int)o[8], (int)o[9], (int)o[10], (int)o[11], (int)o[12], st);
+    case OP_REDUCE_WGRAD: {
+      const long N = o[3] * o[4] * o[5];
+      if (N % 256) return ecg::kBadArg;
+      hipLaunchKernelGGL(reduce_wgrad_kernel, dim3((unsigned)(N / 256)), dim3(TPB), 0, st, P<const float>(o[1]), (int)o[2],
+                         (int)o[3], (int)o[4], (int)o[5], P<float>(o[6]));
+      break;
+    }
+    case OP_BN_FIN: {
+      FinArgs a{};
+      a.sA = P<const float>(o[1]);
+      a.sB = P<const float>(o[2]);
+      a.T = (int)o[3];
+      a.C = (int)o[4];
+      a.mode = (int)o[5];
+      a.scratch = P<double>(o[6]);
+      a.ticket = P<unsigned>(o[7]);
+      a.n = F(o[8]);
+      a.eps = F(o[9]);
+      a.momentum = F(o[10]);
+      a.gamma = P<const float>(o[11]);
+      a.beta = P<const float>(o[12]);
+      a.mean = P<float>(o[13]);
+      a.rstd = P<float>(o[14]);
+      a.scale = P<float>(o[15]);
+      a.shift = P<float>(o[16]);
+      a.run_mean = P<float>(o[17]);
+      a.run_var = P<float>(o[18]);
+      a.dgamma = P<float>(o[19]);
+      a.dbeta = P<float>(o[20]);
+      a.c1 = P<float>(o[21]);
+      a.c2 = P<float>(o[22]);
+      const int G = (int)o[23];
+      if (a.C % 64 || G < 1 || G > 1024) return ecg::kBadArg;
+      hipLaunchKernelGGL(bn_finalize_kernel, dim3(a.C / 64, G), dim3(TPB), 0, st, a);
+      break;
+    }
+    case OP_BN_ACT: {
+      const int mode = (int)o[1];
+      const long R = o[9];
+      const int C = (int)o[10];
+      if (C % 8) return ecg::kBadArg;
+      const dim3 g(grid_for(R * C / 8));
+      if (mode == 0)
+        hipLaunchKernelGGL(bn_act_kernel<0>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]), P<const float>(o[3]),
+                           P<const float>(o[4]), nullptr, nullptr, nullptr, P<__bf16>(o[8]), R, C);
+      else if (mode == 1)
+        hipLaunchKernelGGL(bn_act_kernel<1>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]), P<const float>(o[3]),
+                           P<const float>(o[4]), P<const __bf16>(o[5]), nullptr, nullptr, P<__bf16>(o[8]), R, C);
+      else
+        hipLaunchKernelGGL(bn_act_kernel<2>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]), P<const float>(o[3]),
+                           P<const float>(o[4]), P<const __bf16>(o[5]), P<const float>(o[6]), P<const float>(o[7]),
+                           P<__bf16>(o[8]), R, C);
+      break;
+    }
+    case OP_BN_BWD_REDUCE: {
+      const int ns = (int)o[1];
+      const long R = o[11];
+      const int C = (int)o[12], chunk = (int)o[13];
+      if (C % 8 || C > 8 * TPB || chunk <= 0) return ecg::kBadArg;
+      const dim3 g((unsigned)((R + chunk - 1) / chunk));
+      if (ns == 2)
+        hipLaunchKernelGGL(bn_bwd_reduce_kernel<2>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]), P<const __bf16>(o[3]),
+                           P<const __bf16>(o[4]), P<const float>(o[5]), P<const float>(o[6]), nullptr, nullptr,
+                           nullptr, P<float>(o[10]), R, C, chunk);
+      else
+        hipLaunchKernelGGL(bn_bwd_reduce_kernel<3>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]), P<const __bf16>(o[3]),
+                           P<const __bf16>(o[4]), P<const float>(o[5]), P<const float>(o[6]), P<const __bf16>(o[7]),
+                           P<const float>(o[8]), P<const float>(o[9]), P<float>(o[10]), R, C, chunk);
+      break;
+    }
+    case OP_BN_BWD_APPLY: {
+      const bool ds = o[1] != 0;
+      const long R = o[17];
+      const int C = (int)o[18];
+      const dim3 g(grid_for(R * C / 8));
+      if (!ds)
+        hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]),
+                           P<const __bf16>(o[3]), P<const __bf16>(o[4]), P<const float>(o[5]), P<const float>(o[6]),
+                           P<const float>(o[7]), P<const float>(o[8]), P<const float>(o[9]), P<__bf16>(o[10]),
+                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, R, C);
+      else
+        hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]),
+                           P<const __bf16>(o[3]), P<const __bf16>(o[4]), P<const float>(o[5]), P<const float>(o[6]),
+                           P<const float>(o[7]), P<const float>(o[8]), P<const float>(o[9]), P<__bf16>(o[10]),
+                           P<const __bf16>(o[11]), P<const float>(o[12]), P<const float>(o[13]),
+                           P<const float>(o[14]), P<const float>(o[15]), P<__bf16>(o[16]), R, C);
+      break;
+    }
+    case OP_STEM_FWD: {
+      const int B = (int)o[5], L = (int)o[6], Lo = (int)o[7], K = (int)o[8];
+      if (K > 8) return ecg::kBadArg;
+      const long M = (long)B * Lo;
+      hipLaunchKernelGGL(stem_fwd_kernel, dim3((unsigned)((M + 63) / 64)), dim3(TPB), 0, st, P<const float>(o[1]),
+                         P<const float>(o[2]), P<__bf16>(o[3]), P<float>(o[4]), B, L, Lo, K, (int)o[9], (int)o[10]);
+      break;
+    }
+    case OP_STEM_POOL: {
+      const int B = (int)o[5], Lz = (int)o[6], Lp = (int)o[7], C = (int)o[8];
+      hipLaunchKernelGGL(stem_pool_kernel, dim3(grid_for((long)B * Lp * C / 8)), dim3(TPB), 0, st,
+                         P<const __bf16>(o[1]), P<const float>(o[2]), P<const float>(o[3]), P<__bf16>(o[4]), B, Lz, Lp,
+                         C);
+      break;
+    }
+    case OP_STEM_BWD_REDUCE: {
+      const int B = (int)o[9], Lz = (int)o[10], Lp = (int)o[11], C = (int)o[12], chunk = (int)o[13];
+      if (C % 8 || 2 * C * (TPB / (C / 8)) > TPB * 16) return ecg::kBadArg;
+      const long R = (long)B * Lz;
+      hipLaunchKernelGGL(stem_bwd_reduce_kernel, dim3((unsigned)((R + chunk - 1) / chunk)), dim3(TPB), 0, st,
+                         P<const __bf16>(o[1]), P<const __bf16>(o[2]), P<const float>(o[3]), P<const float>(o[4]),
+                         P<const float>(o[5]), P<const float>(o[6]), P<__bf16>(o[7]), P<float>(o[8]), B, Lz, Lp, C,
+                         chunk);
+      break;
+    }
+    case OP_STEM_WGRAD: {
+      const int B = (int)o[10], L = (int)o[11], Lz = (int)o[12], K = (int)o[13], chunk = (int)o[16];
+      if (K > 8) return ecg::kBadArg;
+      const long R = (long)B * Lz;
+      hipLaunchKernelGGL(stem_wgrad_kernel, dim3((unsigned)((R + chunk - 1) / chunk)), dim3(TPB), 0, st,
+                         P<const __bf16>(o[1]), P<const __bf16>(o[2]), P<const float>(o[3]), P<const float>(o[4]),
+                         P<const float>(o[5]), P<const float>(o[6]), P<const float>(o[7]), P<const float>(o[8]),
+                         P<float>(o[9]), B, L, Lz, K, (int)o[14], (int)o[15], chunk);
+      break;
+    }
+    case OP_REDUCE_SUM: {
+      const long N = o[3];
+      hipLaunchKernelGGL(reduce_sum_kernel, dim3((unsigned)((N + 63) / 64)), dim3(64 * RS_GROUPS), 0, st,
+                         P<const float>(o[1]), (int)o[2], N,
+                         P<float>(o[4]), (long)o[5], P<float>(o[6]));
+      break;
+    }
+    case OP_WEIGHT_PREP:
+      hipLaunchKernelGGL(weight_prep_kernel, dim3((unsigned)o[3]), dim3(TPB), 0, st, P<const WEntry>(o[1]),
+                         (int)o[2], P<const float>(o[4]), P<__bf16>(o[5]));
+      break;
+    case OP_HEAD: {
+      const int B = (int)o[9], Lf = (int)o[10], C = (int)o[11], ncls = (int)o[12];
+      if (C > 1024 || ncls > MAXC || ncls < 1) return ecg::kBadArg;
+      hipLaunchKernelGGL(head_fwd_bwd_kernel, dim3(B), dim3(TPB), 0, st, P<const __bf16>(o[1]), P<const float>(o[2]),
+                         P<const float>(o[3]), P<const int>(o[4]), P<__bf16>(o[5]), P<float>(o[6]), P<float>(o[7]),
+                         P<float>(o[8]), B, Lf, C, ncls);
+      break;
+    }
+    case OP_HEAD_REDUCE: {
+      const int B = (int)o[5], C = (int)o[6], ncls = (int)o[7], Gb = (int)o[8];
+      hipLaunchKernelGGL(head_reduce_kernel, dim3((unsigned)((C + 63) / 64), (unsigned)Gb), dim3(TPB), 0, st,
+                         P<const float>(o[1]), P<const float>(o[2]), P<const float>(o[3]), P<float>(o[4]), B, C, ncls);
+      break;
+    }
+    case OP_SGD:
+      return ecg_sgd_flat(P<float>(o[1]), P<const float>(o[2]), P<float>(o[3]), (long)o[4], F(o[5]), F(o[6]), 0.f,
+                          F(o[7]), (int)o[8], 0, 1.f, nullptr, st);
+    default:
+      return ecg::kBadArg;
+  }
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
+}
+
+struct PlanGraph {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+};
+
+}  // namespace
+
+// Size of one encoded op (int64 words).
+ECG_API int ecg_plan_op_words() { return OP_WORDS; }
+
+// Number of blocks the weight-prep op needs for a table; fills WEntry.block0 in a host-side copy.
+ECG_API int ecg_plan_wentry_bytes() { return (int)sizeof(WEntry); }
+
+// Run ``nops`` encoded ops back to back on ``stream``.  Returns the first failing op's status (ops before it
+// have been enqueued).  ``first_bad`` (optional) receives its index.
+ECG_API int ecg_plan_run(const int64_t* ops, int nops, int* first_bad, hipStream_t stream) {
+  if (!ops || nops < 0) return ecg::kBadArg;
+  for (int i = 0; i < nops; ++i) {
+    const int st = run_op(ops + (long)i * OP_WORDS, stream);
+    if (st) {
+      if (first_bad) *first_bad = i;
+      return st;
+    }
+  }
+  return ecg::kOk;
+}
+
+// Capture the plan into one hipGraph (all pointers baked in; callers keep every buffer alive).
+ECG_API int ecg_plan_graph_create(void** handle, const int64_t* ops, int nops, int* first_bad) {
+  if (!handle || !ops || nops <= 0) return ecg::kBadArg;
+  hipStream_t cap;
+  ECG_HIP_CHECK(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
+  PlanGraph* pg = new PlanGraph();
+  hipError_t e = hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal);
+  if (e != hipSuccess) {
+    delete pg;
+    (void)hipStreamDestroy(cap);
+    return ecg::kHipError;
+  }
+  const int st = ecg_plan_run(ops, nops, first_bad, cap);
+  e = hipStreamEndCapture(cap, &pg->graph);
+  (void)hipStreamDestroy(cap);
+  if (st != 0 || e != hipSuccess) {
+    if (pg->graph) (void)hipGraphDestroy(pg->graph);
+    delete pg;
+    return st ? st : ecg::kHipError;
+  }
+  e = hipGraphInstantiate(&pg->exec, pg->graph, nullptr, nullptr, 0);
+  if (e != hipSuccess) {
+    (void)hipGraphDestroy(pg->graph);
+    delete pg;
+    return ecg::kHipError;
+  }
+  *handle = pg;
+  return ecg::kOk;
+}
+
+ECG_API int ecg_plan_graph_launch(void* handle, hipStream_t stream) {
+  if (!handle) return ecg::kBadArg;
+  ECG_HIP_CHECK(hipGraphLaunch(static_cast<PlanGraph*>(handle)->exec, stream));
+  return ecg::kOk;
+}
+
+ECG_API int ecg_plan_graph_destroy(void* handle) {
+  if (!handle) return ecg::kOk;
+  PlanGraph* pg = static_cast<PlanGraph*>(handle);
+  if (pg->exec) (void)hipGraphExecDestroy(pg->exec);
+  if (pg->graph) (void)hipGraphDestroy(pg->graph);
+  delete pg;
+  return ecg::kOk;
+}

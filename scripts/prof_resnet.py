@@ -5,9 +5,10 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import crossscale_ecg  # noqa: E402,F401
-from crossscale_ecg.bench.resnet import train_throughput  # noqa: E402
+from crossscale_ecg.bench.resnet import engine_throughput, train_throughput  # noqa: E402
 
 if __name__ == "__main__":
-    be = sys.argv[1] if len(sys.argv) > 1 else "hip"
+    be = sys.argv[1] if len(sys.argv) > 1 else "engine"
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 256
-    print(be, B, train_throughput(be, B=B, steps=10))
+    v = engine_throughput(B=B, steps=10) if be == "engine" else train_throughput(be, B=B, steps=10)
+    print(be, B, v)

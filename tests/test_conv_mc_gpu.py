@@ -18,6 +18,9 @@ CASES = [  # B, L, Cin, Cout, K, stride, pad
     (2, 32, 256, 512, 3, 2, 1),  # (L+2p-K) % stride != 0: last input row only reached by one tap
     (3, 32, 256, 512, 1, 2, 0),
     (2, 9, 64, 64, 3, 2, 1),
+    (1024, 70, 64, 64, 3, 1, 1),  # 128x64 tiles
+    (512, 64, 128, 256, 3, 1, 1),  # 128x128 tiles
+    (600, 64, 128, 256, 3, 2, 1),  # 128x128, strided, ragged last M tile
 ]
 
 
