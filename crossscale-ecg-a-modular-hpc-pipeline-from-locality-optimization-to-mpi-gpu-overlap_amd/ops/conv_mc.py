@@ -31,6 +31,7 @@ def _bind(lib):
     vp, i32 = _lib.vp, _lib.i32
     _lib._sig(lib, "ecg_conv1d_nlc_fwd", [vp, vp, vp, vp] + [i32] * 10 + [vp])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad", [vp, vp, vp] + [i32] * 9 + [vp])
+    _lib._sig(lib, "ecg_conv1d_nlc_wgrad_tiles", [i32, i32, i32])
     lib._conv_mc_bound = True
 
 
@@ -66,9 +67,10 @@ def wgrad_raw(dy: torch.Tensor, x: torch.Tensor, K: int, stride: int, pad: int,
     _, Lin, Cin = x.shape
     R = B * Lout
     chunks = (R + 63) // 64
-    tiles = (Cout // 64) * (K * Cin // 64)
-    if splits is None:  # aim for ~2 workgroups per CU, at least 4 r-chunks per workgroup
-        splits = max(1, min(chunks // 4 if chunks >= 4 else 1, max(1, 512 // max(1, tiles))))
+    lib = _lib_k()
+    tiles = lib.ecg_conv1d_nlc_wgrad_tiles(Cout, K, Cin)
+    if splits is None:  # ~4 workgroups per CU, >= 8 row chunks per workgroup, <= 256 partial slices
+        splits = max(1, min(256, max(1, chunks // 8), max(1, 1024 // max(1, tiles))))
     part = torch.empty((splits, Cout, K * Cin), dtype=torch.float32, device=dy.device)
     st = _lib_k().ecg_conv1d_nlc_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr(), splits, B, Lin, Cin, Lout, Cout, K,
                                        stride, pad, _lib.stream_ptr(dy.device))

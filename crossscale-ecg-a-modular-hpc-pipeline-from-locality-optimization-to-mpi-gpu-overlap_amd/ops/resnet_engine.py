@@ -46,7 +46,9 @@ def _bind(lib):
     _lib._sig(lib, "ecg_plan_graph_destroy", [vp])
     _lib._sig(lib, "ecg_plan_op_words", [])
     _lib._sig(lib, "ecg_plan_wentry_bytes", [])
+    _lib._sig(lib, "ecg_plan_stem_rows", [])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles", [ctypes.c_long, i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_wgrad_tiles", [i32, i32, i32])
     lib._plan_bound = True
     if lib.ecg_plan_op_words() != OP_WORDS or lib.ecg_plan_wentry_bytes() != 40:
         raise _lib.NativeError("resnet plan ABI mismatch (rebuild csrc)")
@@ -171,10 +173,10 @@ class ResNetStepEngine:
 
         # ---- wgrad split plan + workspace
         def wsplits(R, Cout, K, Cin):
-            # ~512 workgroups, >= 8 row chunks each, <= 64 partial slices (the reduce reads S x |dW|)
+            # ~1024 workgroups, >= 8 row chunks each, <= 256 partial slices (the reduce reads S x |dW|)
             chunks = (R + 63) // 64
-            tiles = (Cout // 64) * (K * Cin // 64)
-            return max(1, min(64, max(1, chunks // 8), max(1, 512 // tiles)))
+            tiles = self.lib.ecg_conv1d_nlc_wgrad_tiles(Cout, K, Cin)
+            return max(1, min(256, max(1, chunks // 8), max(1, 1024 // tiles)))
 
         ws_need = 0
         for (Li, Ci, Lo, Co, s), blk in zip(shapes, blocks):
@@ -182,7 +184,7 @@ class ResNetStepEngine:
             ws_need = max(ws_need, wsplits(R, Co, 3, Ci) * Co * 3 * Ci, wsplits(R, Co, 3, Co) * Co * 3 * Co)
             if blk.downsample is not None:
                 ws_need = max(ws_need, wsplits(R, Co, 1, Ci) * Co * Ci)
-        stem_chunk = max(256, -(-(B * Lz) // 1024 + 3) // 4 * 4)  # <= ~1024 partial slices
+        stem_chunk = max(256, -(-(B * Lz) // 1024))  # <= ~1024 partial slices
         stem_blocks = (B * Lz + stem_chunk - 1) // stem_chunk
         Gb = max(1, min(64, B // 64))
         ws_need = max(ws_need, stem_blocks * 64 * Ks, Gb * (ncls * self.Cf + ncls + 1))
@@ -243,7 +245,8 @@ class ResNetStepEngine:
 
         # =============================== forward
         op("WEIGHT_PREP", P(tab), len(convs), wprep_blocks, P(self.flat), P(self.warena))
-        T0 = (B * Lz + 63) // 64
+        sr = self.lib.ecg_plan_stem_rows()
+        T0 = (B * Lz + sr - 1) // sr
         op("STEM_FWD", P(self.x), P(c0.weight), P(self.z0), P(stats), B, L, Lz, Ks, Ss, Ps)
         fin_fwd(bn0, T0, B * Lz)
         op("STEM_POOL", P(self.z0), P(bn0.scale), P(bn0.shift), P(self.h0), B, Lz, Lp, 64)

@@ -18,6 +18,9 @@
 // next tile's global loads issued before the current tile's MFMAs (register staging).
 #include "../include/ecg_common.h"
 
+#include <climits>
+#include <cstdlib>
+
 namespace {
 
 constexpr int BK = 64;
@@ -82,8 +85,9 @@ struct FwdCfg {
   static constexpr int SMEM = STAGE_BYTES > EP_BYTES ? STAGE_BYTES : EP_BYTES;
 };
 
-template <int BM, int BN>
-__global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_kernel(FwdArgs a, int MT, int NT) {
+template <int BM, int BN, int PF>
+__global__ __launch_bounds__(THREADS, (PF == 2 && BM * BN > 8192 ? 1 : 2)) void conv1d_nlc_fwd_kernel(FwdArgs a, int MT,
+                                                                                                  int NT) {
   using Cfg = FwdCfg<BM, BN>;
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NA = Cfg::NA, NB = Cfg::NB;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -103,26 +107,47 @@ __global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_kernel(FwdArgs a, i
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint4 ra[NA], rb[NB];
+  // Two register sets: set 0 holds even K tiles, set 1 odd ones.  Tile t+3's loads are issued while tile t is
+  // multiplied, so each load has two full MFMA phases to land (the loop is unrolled by two to keep the set
+  // index compile-time).  Tiles past the end are clamped to the last one (unconditional, register-resident).
+  uint4 ra0[NA], rb0[NB], ra1[PF == 2 ? NA : 1], rb1[PF == 2 ? NB : 1];
+  // per-thread A rows are fixed across K tiles: precompute each row's sample base and first input position
+  const int M = a.B * a.Lout;
+  long abase[NA];
+  int apos[NA];
 #pragma unroll
-  for (int i = 0; i < NA; ++i) ra[i] = load_a_fwd(a, m0, 0, tid + i * THREADS);
+  for (int i = 0; i < NA; ++i) {
+    const int e = tid + i * THREADS, m = m0 + (e >> 3);
+    const int b = m / a.Lout, t = m % a.Lout;
+    abase[i] = (long)b * a.Lin * a.Cin + (e & 7) * 8;
+    apos[i] = m < M ? t * a.stride - a.pad : INT_MIN / 2;  // invalid rows never pass the range check
+  }
+  const __bf16* wb = a.w + (long)(n0 + (tid >> 3)) * (a.Kw * a.Cin) + (tid & 7) * 8;
+  const int Lext = a.in_dil > 1 ? (a.Lin - 1) * a.in_dil + 1 : a.Lin;  // extent of the (dilated) input
+  auto ld_set = [&](uint4* ra, uint4* rb, int t) {
+    const int kk = (t < nk ? t : nk - 1) * BK;
+    const int k = kk / a.Cin, c0 = kk - k * a.Cin;
 #pragma unroll
-  for (int i = 0; i < NB; ++i) rb[i] = load_b_fwd(a, n0, 0, tid + i * THREADS);
+    for (int i = 0; i < NA; ++i) {
+      int u = apos[i] + k;
+      bool ok = u >= 0 && u < Lext;
+      if (a.in_dil > 1) {
+        ok = ok && (u % a.in_dil == 0);
+        u /= a.in_dil;
+      }
+      ra[i] = ok ? *reinterpret_cast<const uint4*>(a.x + abase[i] + (long)u * a.Cin + c0) : make_uint4(0u, 0u, 0u, 0u);
+    }
 #pragma unroll
-  for (int i = 0; i < NA; ++i) store_one(lds, tid + i * THREADS, ra[i]);
+    for (int i = 0; i < NB; ++i)
+      rb[i] = *reinterpret_cast<const uint4*>(wb + (long)i * (THREADS / 8) * (a.Kw * a.Cin) + kk);
+  };
+  auto st_set = [&](__bf16* base, const uint4* ra, const uint4* rb) {
 #pragma unroll
-  for (int i = 0; i < NB; ++i) store_one(lds + Cfg::A_EL, tid + i * THREADS, rb[i]);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    // next tile's global loads go out before this tile's MFMAs (last iteration re-reads its own tile so the
-    // loads stay unconditional and register-resident)
-    const int kn = (kt + 1 < nk ? kt + 1 : kt) * BK;
+    for (int i = 0; i < NA; ++i) store_one(base, tid + i * THREADS, ra[i]);
 #pragma unroll
-    for (int i = 0; i < NA; ++i) ra[i] = load_a_fwd(a, m0, kn, tid + i * THREADS);
-#pragma unroll
-    for (int i = 0; i < NB; ++i) rb[i] = load_b_fwd(a, n0, kn, tid + i * THREADS);
-    const __bf16* As = lds + cur * (Cfg::A_EL + Cfg::B_EL);
+    for (int i = 0; i < NB; ++i) store_one(base + Cfg::A_EL, tid + i * THREADS, rb[i]);
+  };
+  auto mma = [&](const __bf16* As) {
     const __bf16* Bs = As + Cfg::A_EL;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
@@ -141,12 +166,36 @@ __global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_kernel(FwdArgs a, i
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    __bf16* An = lds + (cur ^ 1) * (Cfg::A_EL + Cfg::B_EL);
-#pragma unroll
-    for (int i = 0; i < NA; ++i) store_one(An, tid + i * THREADS, ra[i]);
-#pragma unroll
-    for (int i = 0; i < NB; ++i) store_one(An + Cfg::A_EL, tid + i * THREADS, rb[i]);
+  };
+  __bf16* const L0 = lds;
+  __bf16* const L1 = lds + (Cfg::A_EL + Cfg::B_EL);
+  if constexpr (PF == 2) {
+    ld_set(ra0, rb0, 0);
+    st_set(L0, ra0, rb0);
+    ld_set(ra1, rb1, 1);
+    ld_set(ra0, rb0, 2);
     __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+      mma(L0);                // tile kt (even)
+      st_set(L1, ra1, rb1);   // tile kt+1
+      ld_set(ra1, rb1, kt + 3);
+      __syncthreads();
+      if (kt + 1 >= nk) break;  // block-uniform
+      mma(L1);                // tile kt+1
+      st_set(L0, ra0, rb0);   // tile kt+2
+      ld_set(ra0, rb0, kt + 4);
+      __syncthreads();
+    }
+  } else {  // one register set: tile t+1's loads in flight during tile t's MFMAs
+    ld_set(ra0, rb0, 0);
+    st_set(L0, ra0, rb0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      ld_set(ra0, rb0, kt + 1);
+      mma((kt & 1) ? L1 : L0);
+      st_set((kt & 1) ? L0 : L1, ra0, rb0);
+      __syncthreads();
+    }
   }
   // ---- epilogue 1: fragments -> LDS (fp32, per-wave region); staging buffers are dead after the last barrier
   constexpr int EP_LD = Cfg::EP_LD;
@@ -161,7 +210,6 @@ __global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_kernel(FwdArgs a, i
   // ---- epilogue 2: row-major, 8 channels per lane
   constexpr int CG = WN / 8, RSTEP = 64 / CG, ITEMS = WM / RSTEP;
   const int cg = lane % CG, rs = lane / CG;
-  const int M = a.B * a.Lout;
   const int n = n0 + wc * WN + cg * 8;
   float bv[8], s[8], ss[8];
 #pragma unroll
@@ -242,118 +290,232 @@ inline void pick_fwd_tile(long M, int Cout, int* bm, int* bn) {
   }
 }
 
-template <int BM, int BN>
-int launch_fwd(const FwdArgs& a, hipStream_t stream) {
+// ECG_CONV_PF=1|2 selects the register prefetch depth (default 1; read once).
+inline int prefetch_depth() {
+  static int pf = -1;
+  if (pf < 0) {
+    const char* e = getenv("ECG_CONV_PF");
+    pf = (e && atoi(e) == 2) ? 2 : 1;
+  }
+  return pf;
+}
+
+template <int BM, int BN, int PF>
+int launch_fwd_pf(const FwdArgs& a, hipStream_t stream) {
   using Cfg = FwdCfg<BM, BN>;
   static bool attr = false;
   if (!attr) {
-    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_kernel<BM, BN>,
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_kernel<BM, BN, PF>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::SMEM));
     attr = true;
   }
   const long M = (long)a.B * a.Lout;
   const int MT = (int)((M + BM - 1) / BM), NT = a.Cout / BN;
-  hipLaunchKernelGGL((conv1d_nlc_fwd_kernel<BM, BN>), dim3((unsigned)(MT * NT)), dim3(THREADS), Cfg::SMEM, stream,
-                     a, MT, NT);
+  hipLaunchKernelGGL((conv1d_nlc_fwd_kernel<BM, BN, PF>), dim3((unsigned)(MT * NT)), dim3(THREADS), Cfg::SMEM,
+                     stream, a, MT, NT);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
 
+template <int BM, int BN>
+int launch_fwd(const FwdArgs& a, hipStream_t stream) {
+  return prefetch_depth() == 2 ? launch_fwd_pf<BM, BN, 2>(a, stream) : launch_fwd_pf<BM, BN, 1>(a, stream);
+}
+
 // ------------------------------------------------------------------------------------------- weight grad
+// Division by a runtime-invariant divisor without the ~40-instruction integer divide (Granlund-Montgomery):
+// q = (umulhi(n, m) + n) >> s, exact for 0 <= n < 2^31.
+struct FastDiv {
+  uint32_t m;
+  int s;
+  int d;
+};
+inline FastDiv make_fastdiv(int d) {
+  int s = 0;
+  while ((1u << s) < (uint32_t)d) ++s;
+  const uint64_t m = ((uint64_t)1 << 32) * (((uint64_t)1 << s) - (uint64_t)d) / (uint64_t)d + 1;
+  return FastDiv{(uint32_t)m, s, d};
+}
+__device__ __forceinline__ int fdiv(int n, const FastDiv& f) {
+  return (int)(((uint64_t)__umulhi((uint32_t)n, f.m) + (uint32_t)n) >> f.s);
+}
+
 struct WgradArgs {
   const __bf16* dy;  // [B][Lout][Cout]
   const __bf16* x;   // [B][Lin][Cin]
   float* part;       // [splits][Cout][Kw*Cin] fp32 partials
   int B, Lin, Cin, Lout, Cout, Kw, stride, pad, chunks_per_split;
+  FastDiv lout;  // r -> (b, t) = divmod(r, Lout)
 };
 
-constexpr int WG_ROW = 64 + 4;  // bf16 per LDS row for the [r][c] images (136 B: 8-B aligned tr reads)
 
 __device__ __forceinline__ s16x4 tr16(const __bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
 }
 
-__global__ __launch_bounds__(THREADS) void conv1d_nlc_wgrad_kernel(WgradArgs a) {
-  __shared__ __attribute__((aligned(16))) __bf16 lds[2][64 * WG_ROW];  // [dy tile | x tile], rows = r
+// Tiles BM (C_out) x BN (taps*C_in), reduction over 64-row chunks of (b,t); both LDS images are [r][col] and
+// the MFMA fragments come out of them with transposing reads.  Register-prefetched double buffer (next chunk's
+// global loads in flight during this chunk's MFMAs); 1-D grid, split-major so the workgroups on one XCD
+// share the same activation rows; partial tiles leave through an LDS-staged float4 epilogue.
+template <int BM, int BN>
+struct WgCfg {
+  static constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  static constexpr int ROW_A = BM + 4, ROW_B = BN + 4;  // bf16 per LDS row (8-B aligned tr reads)
+  static constexpr int NA = BM / 32, NB = BN / 32;      // 16-B loads per thread per chunk
+  static constexpr int A_EL = 64 * ROW_A, B_EL = 64 * ROW_B;
+  static constexpr int STAGE_BYTES = 2 * (A_EL + B_EL) * 2;
+  static constexpr int EP_LD = WN + 4;
+  static constexpr int EP_BYTES = 4 * WM * EP_LD * 4;
+  static constexpr int SMEM = STAGE_BYTES > EP_BYTES ? STAGE_BYTES : EP_BYTES;
+};
+
+__device__ __forceinline__ void st_split(__bf16* p, uint4 v) {  // 8-B aligned 16-B store
+  *reinterpret_cast<uint2*>(p) = make_uint2(v.x, v.y);
+  *reinterpret_cast<uint2*>(p + 4) = make_uint2(v.z, v.w);
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_wgrad_kernel(WgradArgs a, int TM, int TN, int splits) {
+  using Cfg = WgCfg<BM, BN>;
+  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NA = Cfg::NA, NB = Cfg::NB;
+  constexpr int ROW_A = Cfg::ROW_A, ROW_B = Cfg::ROW_B;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __bf16* const lds = reinterpret_cast<__bf16*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1, wc = wv & 1;
-  const int co0 = blockIdx.x * 64;
-  const int n0 = blockIdx.y * 64;  // n = k*Cin + ci, tile inside one tap (Cin % 64 == 0)
-  const int k = n0 / a.Cin, c0 = n0 % a.Cin;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int tiles = TM * TN;
+  const int split = wgid / tiles, tile = wgid % tiles;
+  const int co0 = (tile / TN) * BM, n0 = (tile % TN) * BN;
+  const int k = n0 / a.Cin, c0 = n0 % a.Cin;  // the BN columns lie inside one tap
   const int R = a.B * a.Lout;
   const int nchunks = (R + 63) / 64;
-  const int ch0 = blockIdx.z * a.chunks_per_split;
+  const int ch0 = split * a.chunks_per_split;
   const int ch1 = min(nchunks, ch0 + a.chunks_per_split);
-  f32x4 acc[2][2];
+  f32x4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4, h = lane >> 4;
-  for (int ch = ch0; ch < ch1; ++ch) {
-    const int r0 = ch * 64;
-    __syncthreads();  // previous chunk's reads done
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int e = tid + it * THREADS;  // 0..511: row = e >> 3, part = e & 7 (8 bf16 each)
-      const int row = e >> 3, part = e & 7;
-      const int r = r0 + row;
-      uint4 vdy = make_uint4(0u, 0u, 0u, 0u), vx = make_uint4(0u, 0u, 0u, 0u);
-      if (r < R) {
-        vdy = *reinterpret_cast<const uint4*>(a.dy + (long)r * a.Cout + co0 + part * 8);
-        const int b = r / a.Lout, t = r % a.Lout;
-        const int u = t * a.stride + k - a.pad;
-        if (u >= 0 && u < a.Lin) vx = *reinterpret_cast<const uint4*>(a.x + ((long)b * a.Lin + u) * a.Cin + c0 + part * 8);
-      }
-      *reinterpret_cast<uint2*>(lds[0] + row * WG_ROW + part * 8) = make_uint2(vdy.x, vdy.y);
-      *reinterpret_cast<uint2*>(lds[0] + row * WG_ROW + part * 8 + 4) = make_uint2(vdy.z, vdy.w);
-      *reinterpret_cast<uint2*>(lds[1] + row * WG_ROW + part * 8) = make_uint2(vx.x, vx.y);
-      *reinterpret_cast<uint2*>(lds[1] + row * WG_ROW + part * 8 + 4) = make_uint2(vx.z, vx.w);
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto load_a = [&](int ch, int e) -> uint4 {  // dy[r][co0 + 8*part]
+    const int row = e / (BM / 8), part = e % (BM / 8);
+    const int r = ch * 64 + row;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (r < R) v = *reinterpret_cast<const uint4*>(a.dy + (long)r * a.Cout + co0 + part * 8);
+    return v;
+  };
+  auto load_b = [&](int ch, int e) -> uint4 {  // x[b, t*s + k - p][c0 + 8*part]
+    const int row = e / (BN / 8), part = e % (BN / 8);
+    const int r = ch * 64 + row;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (r < R) {
+      const int b = fdiv(r, a.lout), t = r - b * a.Lout;
+      const int u = t * a.stride + k - a.pad;
+      if (u >= 0 && u < a.Lin) v = *reinterpret_cast<const uint4*>(a.x + ((long)b * a.Lin + u) * a.Cin + c0 + part * 8);
     }
+    return v;
+  };
+  auto store_ab = [&](__bf16* base, const uint4* ra, const uint4* rb) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int e = tid + i * THREADS;
+      st_split(base + (e / (BM / 8)) * ROW_A + (e % (BM / 8)) * 8, ra[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int e = tid + i * THREADS;
+      st_split(base + Cfg::A_EL + (e / (BN / 8)) * ROW_B + (e % (BN / 8)) * 8, rb[i]);
+    }
+  };
+
+  if (ch0 < ch1) {  // block-uniform
+    uint4 ra[NA], rb[NB];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) ra[i] = load_a(ch0, tid + i * THREADS);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) rb[i] = load_b(ch0, tid + i * THREADS);
+    store_ab(lds, ra, rb);
     __syncthreads();
+    const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4, h = lane >> 4;
+    for (int ch = ch0; ch < ch1; ++ch) {
+      const int cur = (ch - ch0) & 1;
+      const int cn = ch + 1 < ch1 ? ch + 1 : ch;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {  // two 32-deep k-steps over r
-      bf16x8 af[2], bfr[2];
-      // lane quarter h covers r = ks*32 + 8h .. +7 ; transposing reads give column (lane&15) of 4 rows
-      const int rr = ks * 32 + 8 * h + q;
+      for (int i = 0; i < NA; ++i) ra[i] = load_a(cn, tid + i * THREADS);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int col = wr * 32 + i * 16 + p4;
+      for (int i = 0; i < NB; ++i) rb[i] = load_b(cn, tid + i * THREADS);
+      const __bf16* As = lds + cur * (Cfg::A_EL + Cfg::B_EL);
+      const __bf16* Bs = As + Cfg::A_EL;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {  // two 32-deep k-steps over r
         typedef short s16x8v __attribute__((ext_vector_type(8)));
-        const s16x4 lo = tr16(lds[0] + rr * WG_ROW + col);
-        const s16x4 hi = tr16(lds[0] + (rr + 4) * WG_ROW + col);
-        s16x8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8, v);
+        bf16x8 af[FM], bfr[FN];
+        const int rr = ks * 32 + 8 * h + q;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int col = wr * WM + i * 16 + p4;
+          const s16x4 lo = tr16(As + rr * ROW_A + col);
+          const s16x4 hi = tr16(As + (rr + 4) * ROW_A + col);
+          s16x8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          af[i] = __builtin_bit_cast(bf16x8, v);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int col = wc * WN + j * 16 + p4;
+          const s16x4 lo = tr16(Bs + rr * ROW_B + col);
+          const s16x4 hi = tr16(Bs + (rr + 4) * ROW_B + col);
+          s16x8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          bfr[j] = __builtin_bit_cast(bf16x8, v);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = wc * 32 + j * 16 + p4;
-        typedef short s16x8v __attribute__((ext_vector_type(8)));
-        const s16x4 lo = tr16(lds[1] + rr * WG_ROW + col);
-        const s16x4 hi = tr16(lds[1] + (rr + 4) * WG_ROW + col);
-        s16x8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        bfr[j] = __builtin_bit_cast(bf16x8, v);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      store_ab(lds + (cur ^ 1) * (Cfg::A_EL + Cfg::B_EL), ra, rb);
+      __syncthreads();
     }
   }
-  // partial[split][co][n]
-  const int N = a.Kw * a.Cin;
-  float* out = a.part + (long)blockIdx.z * a.Cout * N;
+  // epilogue: partial[split][co][n] through an LDS fp32 image, float4 row stores
+  constexpr int EP_LD = Cfg::EP_LD;
+  float* ep = reinterpret_cast<float*>(smem) + wv * WM * EP_LD;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wc * 32 + j * 16 + (lane & 15);
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const int co = co0 + wr * 32 + i * 16 + 4 * (lane >> 4) + qq;
-        out[(long)co * N + n] = acc[i][j][qq];
-      }
-    }
+      for (int qq = 0; qq < 4; ++qq)
+        ep[(i * 16 + 4 * (lane >> 4) + qq) * EP_LD + j * 16 + (lane & 15)] = acc[i][j][qq];
+  __syncthreads();
+  constexpr int C4 = WN / 4, RSTEP = 64 / C4;
+  const int c4 = lane % C4, rs = lane / C4;
+  const long N = (long)a.Kw * a.Cin;
+  float* out = a.part + (long)split * a.Cout * N;
+#pragma unroll 4
+  for (int r = rs; r < WM; r += RSTEP) {
+    const float4 v = *reinterpret_cast<const float4*>(ep + r * EP_LD + c4 * 4);
+    *reinterpret_cast<float4*>(out + (long)(co0 + wr * WM + r) * N + n0 + wc * WN + c4 * 4) = v;
+  }
+}
+
+template <int BM, int BN>
+int launch_wgrad(const WgradArgs& a, int splits, hipStream_t stream) {
+  using Cfg = WgCfg<BM, BN>;
+  static bool attr = false;
+  if (!attr) {
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_wgrad_kernel<BM, BN>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::SMEM));
+    attr = true;
+  }
+  const int TM = a.Cout / BM, TN = a.Kw * a.Cin / BN;
+  hipLaunchKernelGGL((conv1d_nlc_wgrad_kernel<BM, BN>), dim3((unsigned)(TM * TN * splits)), dim3(THREADS),
+                     Cfg::SMEM, stream, a, TM, TN, splits);
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
 }
 
 }  // namespace
@@ -402,9 +564,16 @@ ECG_API int ecg_conv1d_nlc_wgrad(const void* dy, const void* x, float* part, int
   const int nchunks = (int)((R + 63) / 64);
   const int cps = (nchunks + splits - 1) / splits;
   WgradArgs a{static_cast<const __bf16*>(dy), static_cast<const __bf16*>(x), part, B, Lin, Cin, Lout, Cout, Kw,
-              stride, pad, cps};
-  dim3 grid((unsigned)(Cout / 64), (unsigned)(Kw * Cin / 64), (unsigned)splits);
-  hipLaunchKernelGGL(conv1d_nlc_wgrad_kernel, grid, dim3(THREADS), 0, stream, a);
-  ECG_HIP_CHECK(hipGetLastError());
-  return ecg::kOk;
+              stride, pad, cps, make_fastdiv(Lout)};
+  const bool bm128 = Cout % 128 == 0, bn128 = Cin % 128 == 0;
+  if (bm128 && bn128) return launch_wgrad<128, 128>(a, splits, stream);
+  if (bm128) return launch_wgrad<128, 64>(a, splits, stream);
+  if (bn128) return launch_wgrad<64, 128>(a, splits, stream);
+  return launch_wgrad<64, 64>(a, splits, stream);
+}
+
+// Workgroup tiles (C_out tiles x tap*C_in tiles) the weight-gradient kernel uses for this shape (split sizing).
+ECG_API int ecg_conv1d_nlc_wgrad_tiles(int Cout, int Kw, int Cin) {
+  const int bm = Cout % 128 == 0 ? 128 : 64, bn = Cin % 128 == 0 ? 128 : 64;
+  return (Cout / bm) * (Kw * Cin / bn);
 }

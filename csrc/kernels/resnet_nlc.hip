@@ -23,6 +23,7 @@
 #include "../include/ecg_common.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #include <vector>
 
@@ -56,39 +57,64 @@ __device__ __forceinline__ void ldf8(const float* p, float* f) {
 }
 
 // ------------------------------------------------------------------------------------------------ stem
-// y[b,t,c] = sum_k w[c,k] x[b, t*s + k - p]; block = 64 rows x 64 channels; stats partial per block.
+// y[b,t,c] = sum_k w[c,k] x[b, t*s + k - p].  Block = STEM_ROWS rows; thread = 8 channels (16-B stores) of one
+// row per pass (8 channel groups x 32 row lanes); BN partials per block.
+constexpr int STEM_ROWS = 256;
 __global__ __launch_bounds__(TPB) void stem_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                        __bf16* __restrict__ y, float* __restrict__ stats, int B,
                                                        int L, int Lo, int K, int stride, int pad) {
   __shared__ float red[4][2][64];
-  const int tid = threadIdx.x, c = tid & 63, rg = tid >> 6;
-  float wk[8];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int cg = tid & 7, rl = tid >> 3, c0 = cg * 8;
+  float wk[8][8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) wk[k] = k < K ? w[c * K + k] : 0.f;
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) wk[e][k] = k < K ? w[(c0 + e) * K + k] : 0.f;
   const long M = (long)B * Lo;
-  float s = 0.f, ss = 0.f;
-  for (int i = 0; i < 16; ++i) {
-    const long m = (long)blockIdx.x * 64 + rg * 16 + i;
+  float s[8], ss[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = ss[e] = 0.f;
+  for (int i = 0; i < STEM_ROWS / 32; ++i) {
+    const long m = (long)blockIdx.x * STEM_ROWS + rl + 32 * i;
     if (m >= M) break;
     const int b = (int)(m / Lo), t = (int)(m % Lo);
     const float* xb = x + (long)b * L;
-    float acc = 0.f;
+    float xv[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int u = t * stride + k - pad;
-      if (k < K && u >= 0 && u < L) acc += wk[k] * xb[u];
+      xv[k] = (k < K && u >= 0 && u < L) ? xb[u] : 0.f;
     }
-    const __bf16 r = (__bf16)acc;
-    y[m * 64 + c] = r;
-    const float rv = (float)r;
-    s += rv;
-    ss += rv * rv;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc += wk[e][k] * xv[k];
+      v[e] = (float)(__bf16)acc;
+      s[e] += v[e];
+      ss[e] += v[e] * v[e];
+    }
+    st8(y + m * 64 + c0, v);
   }
-  red[rg][0][c] = s;
-  red[rg][1][c] = ss;
+#pragma unroll
+  for (int off = 8; off < 64; off <<= 1)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s[e] += __shfl_xor(s[e], off);
+      ss[e] += __shfl_xor(ss[e], off);
+    }
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[wv][0][c0 + e] = s[e];
+      red[wv][1][c0 + e] = ss[e];
+    }
+  }
   __syncthreads();
   if (tid < 128) {
-    const int st = tid >> 6;
+    const int st = tid >> 6, c = tid & 63;
     stats[((long)st * gridDim.x + blockIdx.x) * 64 + c] = red[0][st][c] + red[1][st][c] + red[2][st][c] + red[3][st][c];
   }
 }
@@ -203,54 +229,58 @@ __global__ __launch_bounds__(TPB) void stem_bwd_reduce_kernel(
   }
 }
 
-// dW[c,k] partials: sum over rows of dzz[b,j,c] * x[b, j*s + k - p], dzz = scale*(dz - c1 - xhat*c2)
+// dW[c,k] partials: sum over rows of dzz[b,j,c] * x[b, j*s + k - p], dzz = scale*(dz - c1 - xhat*c2).
+// Thread = 8 channels (16-B loads) x all taps of one row per pass; 8 channel groups x 32 row lanes per block.
 __global__ __launch_bounds__(TPB) void stem_wgrad_kernel(
     const __bf16* __restrict__ dz, const __bf16* __restrict__ z, const float* __restrict__ mean,
     const float* __restrict__ rstd, const float* __restrict__ scale, const float* __restrict__ c1,
     const float* __restrict__ c2, const float* __restrict__ x, float* __restrict__ part, int B, int L, int Lz, int K,
     int stride, int pad, int chunk) {
   __shared__ float red[4][64 * 8];
-  const int tid = threadIdx.x, c = tid & 63, rg = tid >> 6;
-  const float mu = mean[c], rs = rstd[c], sc = scale[c], k1 = c1[c], k2 = c2[c];
-  float acc[8];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int cg = tid & 7, rl = tid >> 3, c0 = cg * 8;
+  float mu[8], rs[8], sc[8], k1[8], k2[8], acc[8][8];
+  ldf8(mean + c0, mu);
+  ldf8(rstd + c0, rs);
+  ldf8(scale + c0, sc);
+  ldf8(c1 + c0, k1);
+  ldf8(c2 + c0, k2);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[e][k] = 0.f;
   const long R = (long)B * Lz;
   const long r1 = min(R, (long)(blockIdx.x + 1) * chunk);
-  long r = (long)blockIdx.x * chunk + rg;
-  for (; r + 12 < r1; r += 16) {  // 4 rows in flight per thread
-    float gz[4], xz[4][8];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const long ru = r + 4 * u;
-      const int b = (int)(ru / Lz), j = (int)(ru % Lz);
-      const float xh = ((float)z[ru * 64 + c] - mu) * rs;
-      gz[u] = sc * ((float)dz[ru * 64 + c] - k1 - xh * k2);
-      const float* xb = x + (long)b * L;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int uu = j * stride + k - pad;
-        xz[u][k] = (k < K && uu >= 0 && uu < L) ? xb[uu] : 0.f;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += gz[u] * xz[u][k];
-  }
-  for (; r < r1; r += 4) {
+  for (long r = (long)blockIdx.x * chunk + rl; r < r1; r += 32) {
     const int b = (int)(r / Lz), j = (int)(r % Lz);
-    const float xh = ((float)z[r * 64 + c] - mu) * rs;
-    const float g = sc * ((float)dz[r * 64 + c] - k1 - xh * k2);
+    float dv[8], zv[8], xv[8];
+    ld8(dz + r * 64 + c0, dv);
+    ld8(z + r * 64 + c0, zv);
     const float* xb = x + (long)b * L;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int u = j * stride + k - pad;
-      if (k < K && u >= 0 && u < L) acc[k] += g * xb[u];
+      xv[k] = (k < K && u >= 0 && u < L) ? xb[u] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float g = sc[e] * (dv[e] - k1[e] - (zv[e] - mu[e]) * rs[e] * k2[e]);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[e][k] += g * xv[k];
     }
   }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) red[rg][c * 8 + k] = acc[k];
+  for (int off = 8; off < 64; off <<= 1)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[e][k] += __shfl_xor(acc[e][k], off);
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[wv][(c0 + e) * 8 + k] = acc[e][k];
+  }
   __syncthreads();
   for (int idx = tid; idx < 64 * K; idx += TPB) {
     const int cc = idx / K, k = idx % K;
@@ -280,6 +310,30 @@ struct FinArgs {
   float* c1;  // sum dz / n
   float* c2;  // sum dz*xhat / n
 };
+
+__device__ __forceinline__ void bn_fin_outputs(const FinArgs& a, int c, double v1, double v2) {
+  const double n = (double)a.n;
+  if (a.mode == 0) {
+    const double mu = v1 / n;
+    const double var = fmax(v2 / n - mu * mu, 0.0);
+    const float rs = (float)(1.0 / sqrt(var + (double)a.eps));
+    const float sc = a.gamma[c] * rs;
+    a.mean[c] = (float)mu;
+    a.rstd[c] = rs;
+    a.scale[c] = sc;
+    a.shift[c] = a.beta[c] - (float)mu * sc;
+    if (a.run_mean) {
+      const float m = a.momentum;
+      a.run_mean[c] = (1.f - m) * a.run_mean[c] + m * (float)mu;
+      a.run_var[c] = (1.f - m) * a.run_var[c] + m * (float)(var * n / fmax(n - 1.0, 1.0));
+    }
+  } else {
+    if (a.dbeta) a.dbeta[c] = (float)v1;
+    if (a.dgamma) a.dgamma[c] = (float)v2;
+    a.c1[c] = (float)(v1 / n);
+    a.c2[c] = (float)(v2 / n);
+  }
+}
 
 __global__ __launch_bounds__(TPB) void bn_finalize_kernel(FinArgs a) {
   __shared__ double red[4][2][64];
@@ -360,6 +414,45 @@ __global__ __launch_bounds__(TPB) void bn_finalize_kernel(FinArgs a) {
     }
   }
   if (tid == 0) a.ticket[blockIdx.x] = 0u;
+}
+
+// Two-launch form (default): phase 1 writes the G level-2 partials with plain stores, the kernel boundary makes
+// them visible, phase 2 (one block per 64 channels) reduces them - no fences on the critical path.
+__global__ __launch_bounds__(TPB) void bn_partial_kernel(FinArgs a) {
+  __shared__ double red[4][2][64];
+  const int tid = threadIdx.x, cl = tid & 63, g4 = tid >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int G = gridDim.y;
+  const int t0 = (int)((long)a.T * blockIdx.y / G), t1 = (int)((long)a.T * (blockIdx.y + 1) / G);
+  double s1 = 0.0, s2 = 0.0;
+  for (int t = t0 + g4; t < t1; t += 4) {
+    s1 += (double)a.sA[(long)t * a.C + c];
+    s2 += (double)a.sB[(long)t * a.C + c];
+  }
+  red[g4][0][cl] = s1;
+  red[g4][1][cl] = s2;
+  __syncthreads();
+  if (tid < 64) {
+    a.scratch[((long)blockIdx.y * 2 + 0) * a.C + c] = red[0][0][cl] + red[1][0][cl] + red[2][0][cl] + red[3][0][cl];
+    a.scratch[((long)blockIdx.y * 2 + 1) * a.C + c] = red[0][1][cl] + red[1][1][cl] + red[2][1][cl] + red[3][1][cl];
+  }
+}
+
+__global__ __launch_bounds__(TPB) void bn_final_kernel(FinArgs a, int G) {
+  __shared__ double red[4][2][64];
+  const int tid = threadIdx.x, cl = tid & 63, g4 = tid >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double v1 = 0.0, v2 = 0.0;
+  for (int g = g4; g < G; g += 4) {
+    v1 += a.scratch[((long)g * 2 + 0) * a.C + c];
+    v2 += a.scratch[((long)g * 2 + 1) * a.C + c];
+  }
+  red[g4][0][cl] = v1;
+  red[g4][1][cl] = v2;
+  __syncthreads();
+  if (tid < 64)
+    bn_fin_outputs(a, c, red[0][0][cl] + red[1][0][cl] + red[2][0][cl] + red[3][0][cl],
+                   red[0][1][cl] + red[1][1][cl] + red[2][1][cl] + red[3][1][cl]);
 }
 
 // MODE 0: out = relu(z*scale + shift); 1: out = relu(z*scale + shift + res); 2: + (zd*scale_d + shift_d)
@@ -745,6 +838,17 @@ inline float F(int64_t v) {
   return (float)d;
 }
 
+// ECG_BN_FIN=ticket selects the single-launch ticketed finalize (fence + last-block reduction); default: two
+// launches.  Read once.
+inline int fin_mode() {
+  static int m = -1;
+  if (m < 0) {
+    const char* e = getenv("ECG_BN_FIN");
+    m = (e && strcmp(e, "ticket") == 0) ? 1 : 0;
+  }
+  return m;
+}
+
 int run_op(const int64_t* o, hipStream_t st) {
   const int kind = (int)o[0];
   switch (kind) {
@@ -788,7 +892,12 @@ int run_op(const int64_t* o, hipStream_t st) {
       a.c2 = P<float>(o[22]);
       const int G = (int)o[23];
       if (a.C % 64 || G < 1 || G > 1024) return ecg::kBadArg;
-      hipLaunchKernelGGL(bn_finalize_kernel, dim3(a.C / 64, G), dim3(TPB), 0, st, a);
+      if (fin_mode() == 1) {
+        hipLaunchKernelGGL(bn_finalize_kernel, dim3(a.C / 64, G), dim3(TPB), 0, st, a);
+      } else {
+        hipLaunchKernelGGL(bn_partial_kernel, dim3(a.C / 64, G), dim3(TPB), 0, st, a);
+        hipLaunchKernelGGL(bn_final_kernel, dim3(a.C / 64), dim3(TPB), 0, st, a, G);
+      }
       break;
     }
     case OP_BN_ACT: {
@@ -847,7 +956,8 @@ int run_op(const int64_t* o, hipStream_t st) {
       const int B = (int)o[5], L = (int)o[6], Lo = (int)o[7], K = (int)o[8];
       if (K > 8) return ecg::kBadArg;
       const long M = (long)B * Lo;
-      hipLaunchKernelGGL(stem_fwd_kernel, dim3((unsigned)((M + 63) / 64)), dim3(TPB), 0, st, P<const float>(o[1]),
+      hipLaunchKernelGGL(stem_fwd_kernel, dim3((unsigned)((M + STEM_ROWS - 1) / STEM_ROWS)), dim3(TPB), 0, st,
+                         P<const float>(o[1]),
                          P<const float>(o[2]), P<__bf16>(o[3]), P<float>(o[4]), B, L, Lo, K, (int)o[9], (int)o[10]);
       break;
     }
@@ -922,6 +1032,9 @@ struct PlanGraph {
 
 // Size of one encoded op (int64 words).
 ECG_API int ecg_plan_op_words() { return OP_WORDS; }
+
+// Rows per block of the stem forward kernel (= rows per BN-statistics partial of the stem BN).
+ECG_API int ecg_plan_stem_rows() { return STEM_ROWS; }
 
 // Number of blocks the weight-prep op needs for a table; fills WEntry.block0 in a host-side copy.
 ECG_API int ecg_plan_wentry_bytes() { return (int)sizeof(WEntry); }
