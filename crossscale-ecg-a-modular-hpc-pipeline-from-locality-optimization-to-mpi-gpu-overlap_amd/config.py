@@ -20,7 +20,7 @@ class FedAvgConfig:
     # ---- MI355X additions ----
     kernel_backend: str = "auto"  # auto | fused | hip | torch  (hip = MFMA conv kernels for ResNet1D)
     amp_dtype: str = "bf16"  # bf16 | fp16 | none  (dtype of the G1 configuration)
-    overlap: str = "none"  # none | delayed
+    overlap: str = "none"  # none | tail (exact, ResNet engine) | delayed (stale-by-one)
     sync: str = "fedavg"  # fedavg | none | ddp
     bcast_every_round: bool = True  # the reference broadcasts every round; RCCL AVG makes it redundant
     synthetic_windows: int = 0  # >0: skip shards, generate N(0,1) windows on device

@@ -29,7 +29,7 @@ from ..models.resnet1d import ResNet1D
 OP_WORDS = 32
 OP = dict(CONV_FWD=1, CONV_WGRAD=2, REDUCE_WGRAD=3, BN_FIN=4, BN_ACT=5, BN_BWD_REDUCE=6, BN_BWD_APPLY=7,
           STEM_FWD=8, STEM_POOL=9, STEM_BWD_REDUCE=10, STEM_WGRAD=11, REDUCE_SUM=12, WEIGHT_PREP=13, HEAD=14,
-          HEAD_REDUCE=15, SGD=16)
+          HEAD_REDUCE=15, SGD=16, GATHER=17, COUNTER_INC=18)
 
 
 def _f(x: float) -> int:
@@ -72,13 +72,17 @@ class ResNetStepEngine:
     """Fixed-shape training step for a :class:`ResNet1D` (any depth, BasicBlocks, channels multiple of 64).
 
     ``set_batch(x, y)`` copies a batch into the static input buffers; ``step()`` runs forward, backward and
-    SGD; ``forward_backward()`` skips the SGD (tests, DDP).  ``grad_sync(flat_range_tensor)`` - if given -
-    is called for each backward segment's gradient range in order (DDP all-reduce hook).
+    SGD; ``forward_backward()`` skips the SGD (tests, DDP) and ``apply_update()`` runs it.
+    ``grad_sync(flat_range_tensor)`` - if given - is called for each backward segment's gradient range in
+    order (DDP all-reduce hook).  ``source=(X [N, L] fp32, Y [N] int32, table [S, B] int32)`` puts the batch
+    gather inside the step plan: step ``c`` of a round reads ``table[c % S]`` (device counter, reset by
+    ``reset_counter()``), so one captured step graph serves every batch.
     """
 
     def __init__(self, model: ResNet1D, batch_size: int, seq_len: int = 500, lr: float = 1e-2,
                  momentum: float = 0.9, weight_decay: float = 0.0, nesterov: bool = False, use_graph: bool = True,
-                 grad_sync: Optional[Callable[[torch.Tensor], None]] = None):
+                 grad_sync: Optional[Callable[[torch.Tensor], None]] = None,
+                 source: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None):
         dev = next(model.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("ResNetStepEngine needs a GPU (HIP kernels)")
@@ -94,10 +98,19 @@ class ResNetStepEngine:
         self.grad = self.space.grad_buffer()
         self.mom = torch.zeros_like(self.grad)
         self.loss_acc = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.counter = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.source = source
+        if source is not None:
+            X, Y, table = source
+            if (X.dtype != torch.float32 or X.dim() != 2 or X.shape[1] != seq_len or X.stride(1) != 1
+                    or Y.dtype != torch.int32 or table.dtype != torch.int32 or table.dim() != 2
+                    or table.shape[1] != batch_size or not table.is_contiguous()):
+                raise ValueError("source must be (X fp32 [N, L], Y int32 [N], table int32 [S, B])")
         self._steps_since_sync = 0
         self._loss_steps = 0
         self._keep: List[torch.Tensor] = []
         self._graphs: Dict[str, int] = {}
+        self._range_ops: Dict[Tuple[int, int], torch.Tensor] = {}
         self._build()
 
     # ------------------------------------------------------------------------------------------ allocation
@@ -244,6 +257,10 @@ class ResNetStepEngine:
             op("REDUCE_WGRAD", P(ws), S, Cout, K, Cin, self._gptr(weight))
 
         # =============================== forward
+        if self.source is not None:
+            X, Y, table = self.source
+            op("GATHER", P(X), X.stride(0), P(Y), P(table), P(self.counter), table.shape[0], B, L, P(self.x), P(self.y))
+            op("COUNTER_INC", P(self.counter))
         op("WEIGHT_PREP", P(tab), len(convs), wprep_blocks, P(self.flat), P(self.warena))
         sr = self.lib.ecg_plan_stem_rows()
         T0 = (B * Lz + sr - 1) // sr
@@ -394,6 +411,10 @@ class ResNetStepEngine:
         self._loss_steps += 1
         self._steps_since_sync += 1
 
+    def apply_update(self) -> None:
+        """The SGD op alone (after ``forward_backward`` and any gradient all-reduce)."""
+        self._exec("sgd", self._fb_end, self.n_ops)
+
     def step(self) -> None:
         if self.grad_sync is None:
             self._exec("step", 0, self.n_ops)
@@ -401,7 +422,22 @@ class ResNetStepEngine:
             self._steps_since_sync += 1
         else:
             self.forward_backward()
-            self._exec("sgd", self._fb_end, self.n_ops)
+            self.apply_update()
+
+    def reset_counter(self) -> None:
+        self.counter.zero_()
+
+    def sgd_range(self, lo: int, hi: int) -> None:
+        """SGD on the flat parameter range [lo, hi) only (the per-segment update of ``--overlap tail``)."""
+        key = (lo, hi)
+        ops = self._range_ops.get(key)
+        if ops is None:
+            w = [OP["SGD"], self.flat.data_ptr() + 4 * lo, self.grad.data_ptr() + 4 * lo, self.mom.data_ptr() + 4 * lo,
+                 hi - lo, _f(self.lr), _f(self.momentum), _f(self.wd), int(self.nesterov)]
+            ops = self._range_ops[key] = torch.tensor([w + [0] * (OP_WORDS - len(w))], dtype=torch.int64)
+        bad = ctypes.c_int(-1)
+        st = self.lib.ecg_plan_run(ops.data_ptr(), 1, ctypes.byref(bad), _lib.stream_ptr(self.dev))
+        _lib.check(st, "ecg_plan_run(sgd_range)")
 
     def avg_loss(self) -> float:
         return float(self.loss_acc.item()) / max(1, self._loss_steps)

@@ -11,6 +11,9 @@ MI355X execution (vs the reference's host-staged per-tensor MPI calls and per-st
   * G1 local round = ONE native hipGraph replay of ``local_steps`` fused HIP steps (``ops.fused_tiny``);
   * FedAvg = ONE RCCL ``all_reduce(AVG)`` of the flat fp32 weight buffer; broadcast = ONE RCCL broadcast;
   * ``--overlap delayed``: the all-reduce runs on RCCL's stream under the next round (stale-by-one FedAvg);
+  * ``--overlap tail`` (ResNet engine): the round's last step applies SGD per backward segment and all-reduces
+    each segment's weights while earlier segments still run backward (exact FedAvg, comm overlapped);
+  * ResNet1D G1 runs on the native step engine (``train.resnet_trainer``; one hipGraph replay per step);
   * ``--sync none``: pseudo-federated independent clients; ``--sync ddp``: synchronous gradient DP;
   * ``--drop-prob``: client dropout with sample-weighted averaging; ``--ckpt-every``/``--resume``.
 """
@@ -85,6 +88,10 @@ def make_trainer(cfg: FedAvgConfig, config_name: str, model, x, y, ctx: DistCont
         prec = "bf16" if (config_name == "G1" and cfg.amp_dtype == "bf16") else "fp32"
         return FusedTinyTrainer(model, x, y, cfg.batch_size, cfg.local_steps, lr=cfg.lr, momentum=cfg.momentum,
                                 seed=seed, precision=prec)
+    if backend == "hip":  # ResNet1D on the native step engine
+        from .resnet_trainer import ResNetEngineTrainer
+        return ResNetEngineTrainer(model, x, y, cfg.batch_size, cfg.local_steps, lr=cfg.lr, momentum=cfg.momentum,
+                                   seed=seed, ctx=ctx, sync=cfg.sync)
     amp = None if config_name == "G0" else _amp(cfg)
     net = model
     if cfg.sync == "ddp" and ctx.distributed:
@@ -157,8 +164,6 @@ def run_fedavg(cfg: FedAvgConfig, ctx: DistContext) -> List[Dict]:
         torch.manual_seed(cfg.seed)  # identical init on every client (the round-0 broadcast makes it exact)
         model = build_model(cfg.model, cfg.num_classes).to(dev)
         backend = pick_backend(cfg, cname, ctx)
-        if hasattr(model, "backend"):  # ResNet1D: MFMA channels-last convs on the GPU unless --kernel-backend torch
-            model.backend = "hip" if backend == "hip" else "torch"
         flat = model.flatten_parameters() if hasattr(model, "flatten_parameters") else None
         trainer = make_trainer(cfg, cname, model, x, y, ctx, backend)
         start_round = 0
@@ -182,15 +187,17 @@ def run_fedavg(cfg: FedAvgConfig, ctx: DistContext) -> List[Dict]:
                 _sync(dev)
             t_c1 = time.perf_counter()
             # ---- local steps -----------------------------------------------------------------
+            tail = (cfg.overlap == "tail" and cfg.sync == "fedavg" and ctx.distributed
+                    and hasattr(trainer, "tail_fedavg") and cfg.drop_prob == 0)
+            local_steps = cfg.local_steps - 1 if tail else cfg.local_steps
             with profiling.range("local_round"):
                 if cfg.sync == "ddp" and backend == "fused" and ctx.distributed:
-                    _ddp_fused_round(trainer, ctx, cfg.local_steps)
+                    _ddp_fused_round(trainer, ctx, local_steps)
                 else:
-                    trainer.run_round(cfg.local_steps)
+                    trainer.run_round(local_steps)
                 _sync(dev)
             t_l1 = time.perf_counter()
-            avg_loss = trainer.avg_loss()
-            n_samples = cfg.batch_size * cfg.local_steps
+            n_samples = cfg.batch_size * local_steps
             # ---- FedAvg ----------------------------------------------------------------------
             _sync(dev)
             t_c2 = time.perf_counter()
@@ -202,10 +209,13 @@ def run_fedavg(cfg: FedAvgConfig, ctx: DistContext) -> List[Dict]:
                         weighted_fedavg_(model_flat(model), w, ctx)
                     elif delayed is not None:
                         delayed.boundary()
+                    elif tail:  # last local step + per-segment all-reduce overlapped with its backward
+                        trainer.tail_fedavg()
                     else:
                         fedavg_allreduce(comm, model)
                 _sync(dev)
             t_c3 = time.perf_counter()
+            avg_loss = trainer.avg_loss()
             local_ms = (t_l1 - t_c1) * 1e3
             comm_ms = ((t_c1 - t_c0) + (t_c3 - t_c2)) * 1e3
             row = RoundStats(config=cname, world_size=ctx.world_size, rank=ctx.rank, round_idx=r,

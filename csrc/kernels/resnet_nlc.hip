@@ -772,6 +772,24 @@ __global__ __launch_bounds__(TPB) void reduce_wgrad_kernel(const float* __restri
   }
 }
 
+// ------------------------------------------------------------------------------------------------ data
+// Batch staging inside the step graph: the step index comes from a device counter, so one captured step is
+// replayed for every batch of a round; the index table [S][B] is refilled in place between rounds.
+__global__ __launch_bounds__(TPB) void gather_step_kernel(const float* __restrict__ X, long ldx,
+                                                          const int* __restrict__ Y, const int* __restrict__ table,
+                                                          const int* __restrict__ counter, int S, int B, int L,
+                                                          float* __restrict__ out_x, int* __restrict__ out_y) {
+  const int b = blockIdx.x;
+  const int step = *counter % S;
+  const long row = table[(long)step * B + b];
+  const float* src = X + row * ldx;
+  float* dst = out_x + (long)b * L;
+  for (int i = threadIdx.x; i < L; i += TPB) dst[i] = src[i];
+  if (threadIdx.x == 0) out_y[b] = Y[row];
+}
+
+__global__ void counter_inc_kernel(int* counter) { *counter += 1; }
+
 // ------------------------------------------------------------------------------------------------ weights
 struct WEntry {
   long src;  // offset (elements) of the fp32 [Cout][Cin][K] weight in the flat buffer
@@ -827,6 +845,8 @@ enum OpKind : int {
   OP_HEAD = 14,
   OP_HEAD_REDUCE = 15,
   OP_SGD = 16,
+  OP_GATHER = 17,
+  OP_COUNTER_INC = 18,
 };
 constexpr int OP_WORDS = 32;
 
@@ -1016,6 +1036,17 @@ int run_op(const int64_t* o, hipStream_t st) {
     case OP_SGD:
       return ecg_sgd_flat(P<float>(o[1]), P<const float>(o[2]), P<float>(o[3]), (long)o[4], F(o[5]), F(o[6]), 0.f,
                           F(o[7]), (int)o[8], 0, 1.f, nullptr, st);
+    case OP_GATHER: {
+      const int S = (int)o[6], B = (int)o[7], L = (int)o[8];
+      if (S <= 0 || B <= 0 || L <= 0) return ecg::kBadArg;
+      hipLaunchKernelGGL(gather_step_kernel, dim3(B), dim3(TPB), 0, st, P<const float>(o[1]), (long)o[2],
+                         P<const int>(o[3]), P<const int>(o[4]), P<const int>(o[5]), S, B, L, P<float>(o[9]),
+                         P<int>(o[10]));
+      break;
+    }
+    case OP_COUNTER_INC:
+      hipLaunchKernelGGL(counter_inc_kernel, dim3(1), dim3(1), 0, st, P<int>(o[1]));
+      break;
     default:
       return ecg::kBadArg;
   }
