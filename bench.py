@@ -40,7 +40,9 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--batch-size", type=int, default=256)
+    ap.add_argument("--model", choices=["tiny_ecg", "resnet1d34", "resnet1d18"], default="tiny_ecg",
+                    help="tiny_ecg = BASELINE headline; resnet1d34 = BASELINE config 5 (scaling stress)")
+    ap.add_argument("--batch-size", type=int, default=None, help="per client (default 256; 1024 for ResNet1D)")
     ap.add_argument("--local-steps", type=int, default=50)
     ap.add_argument("--max-windows", type=int, default=20000)
     ap.add_argument("--win-len", type=int, default=500)
@@ -123,6 +125,9 @@ def main(argv=None):
     dev = ctx.device
     if dev.type != "cuda":
         raise SystemExit("bench.py needs a GPU")
+    resnet = a.model.startswith("resnet")
+    if a.batch_size is None:
+        a.batch_size = 1024 if resnet else 256
     B, S = a.batch_size, a.local_steps
     # per-client synthetic shard, resident in HBM
     gen = torch.Generator(device=dev)
@@ -131,10 +136,18 @@ def main(argv=None):
     y = torch.zeros(a.max_windows, dtype=torch.long, device=dev)
 
     torch.manual_seed(1234)  # same initial global model on every client (== round-0 broadcast)
-    model = TinyECG(num_classes=2).to(dev)
+    if resnet:
+        from crossscale_ecg.models import build_model
+        model = build_model(a.model, 2).to(dev)
+    else:
+        model = TinyECG(num_classes=2).to(dev)
     flat = model.flatten_parameters()
 
-    if a.backend == "fused":
+    if resnet and a.backend == "fused":  # native ResNet step engine (one hipGraph per step)
+        from crossscale_ecg.train.resnet_trainer import ResNetEngineTrainer
+        trainer = ResNetEngineTrainer(model, x, y, B, S, lr=1e-2, momentum=0.9, seed=4321 + ctx.rank, ctx=ctx)
+        run = lambda k: timed_fused(trainer, ctx, k, S, flat)  # noqa: E731
+    elif a.backend == "fused":
         from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
         trainer = FusedTinyTrainer(model, x, y, B, S, lr=1e-2, momentum=0.9, seed=4321 + ctx.rank)
         run = lambda k: timed_fused(trainer, ctx, k, S, flat)  # noqa: E731
@@ -174,7 +187,14 @@ def main(argv=None):
     loss = trainer.avg_loss() if hasattr(trainer, "avg_loss") else float("nan")
 
     extras = {}
-    if ctx.rank == 0 and not a.no_extras:
+    if ctx.rank == 0 and not a.no_extras and resnet:
+        try:
+            from crossscale_ecg.bench.resnet import train_throughput
+            extras["torch_eager_samples_per_s_per_gpu"] = round(train_throughput("torch", B=B, L=a.win_len), 1)
+            extras["speedup_vs_torch_eager_per_gpu"] = round(value / a.gpus / extras["torch_eager_samples_per_s_per_gpu"], 2)
+        except Exception as e:  # pragma: no cover
+            extras["torch_eager_error"] = repr(e)[:200]
+    elif ctx.rank == 0 and not a.no_extras:
         try:
             extras["torch_eager_samples_per_s_per_gpu"] = round(torch_eager_rate(x, y, B, 100, dev), 1)
             extras["speedup_vs_torch_eager_per_gpu"] = round(value / a.gpus / extras["torch_eager_samples_per_s_per_gpu"], 2)
@@ -189,8 +209,9 @@ def main(argv=None):
             extras["conv1d_error"] = repr(e)[:200]
 
     if ctx.rank == 0:
+        n_par = sum(p.numel() for p in model.parameters())
         rec = {
-            "metric": METRIC,
+            "metric": METRIC if not resnet else "ECG samples/sec (node), ResNet1D-34 scaling-stress config (BASELINE config 5)",
             "value": round(value, 1),
             "unit": "samples/s",
             "n_gpus": a.gpus,
@@ -203,7 +224,7 @@ def main(argv=None):
             "dtype": "bf16",
             "data": "synthetic",
             "config": {
-                "model": f"TinyECG ({num_params(2)} params)",
+                "model": f"TinyECG ({num_params(2)} params)" if not resnet else f"{a.model} ({n_par} params)",
                 "global_batch": B * a.gpus,
                 "seq_len": a.win_len,
                 "parallelism": f"dp{a.gpus}",

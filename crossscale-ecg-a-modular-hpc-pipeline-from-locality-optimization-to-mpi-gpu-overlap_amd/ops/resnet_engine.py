@@ -241,15 +241,19 @@ class ResNetStepEngine:
                P(tickets), _f(n), _f(eps), _f(bnm), P(bn.weight), P(bn.bias), P(st.mean), P(st.rstd), P(st.scale),
                P(st.shift), P(bn.running_mean), P(bn.running_var), 0, 0, 0, 0, G)
 
-        def fin_bwd(st: _BN, T, n, statB):
+        def fin_bwd(st: _BN, T, n, statB, base=None):
             G = max(1, min(128, T // 64))
             bn = st.bn
-            op("BN_FIN", bpart.data_ptr(), bpart.data_ptr() + 4 * statB * T * st.C, T, st.C, 1, P(fin_scratch),
+            base = bpart.data_ptr() if base is None else base
+            op("BN_FIN", base, base + 4 * statB * T * st.C, T, st.C, 1, P(fin_scratch),
                P(tickets), _f(n), _f(eps), _f(bnm), P(bn.weight), P(bn.bias), 0, 0, 0, 0, 0, 0,
                self._gptr(bn.weight), self._gptr(bn.bias), P(st.c1), P(st.c2), G)
 
-        def conv(x, Lin, Cin, w_ptr, y, Lout, Cout, K, s, p, dil=1, st=None, add=None, add_mask=None):
-            op("CONV_FWD", P(x), w_ptr, 0, P(y), P(st), P(add), P(add_mask), B, Lin, Cin, Lout, Cout, K, s, p, dil, 0)
+        def conv(x, Lin, Cin, w_ptr, y, Lout, Cout, K, s, p, dil=1, st=None, add=None, add_mask=None, bnb=None):
+            # bnb = (mask, z, mean, rstd, zd, mean_d, rstd_d): BN-backward statistics fused into the epilogue
+            extra = [P(t) if isinstance(t, torch.Tensor) else int(t or 0) for t in (bnb or ())]
+            op("CONV_FWD", P(x), w_ptr, 0, P(y), P(st), P(add), P(add_mask), B, Lin, Cin, Lout, Cout, K, s, p, dil, 0,
+               *extra)
 
         def wgrad(dy, x, Lin, Cin, Lout, Cout, K, s, p, weight):
             S = wsplits(B * Lout, Cout, K, Cin)
@@ -303,38 +307,55 @@ class ResNetStepEngine:
         stage_of = []
         for si, st in enumerate((m.layer1, m.layer2, m.layer3, m.layer4)):
             stage_of += [si] * len(st)
+        # BN-backward fusion: every data-grad conv's epilogue stores the ReLU-masked gradient and emits the
+        # statistics (sum dz, sum dz*xhat [, sum dz*xhat_ds]) of the BatchNorm that consumes it; only the last
+        # block (whose gradient comes from the head) runs a separate reduce pass.
+        stats_b = self._t(3 * max_T * 512, dtype=torch.float32)  # cross-block BN2 statistics (conv1 dgrad -> next)
         nxt = gB
         seg_hi = self.space.param_numel
+        bn2_src = None  # (partials base, T) of the current block's BN2 statistics
         for bi in range(len(blocks) - 1, -1, -1):
             (Li, Ci, Lo, Co, s), blk, a, (b1, b2, bd) = shapes[bi], blocks[bi], acts[bi], bns[bi]
             R = B * Lo
-            ch = chunk_for(Co)
-            Tb = (R + ch - 1) // ch
-            gy, din = gcur, nxt
-            ns = 3 if bd is not None else 2
-            op("BN_BWD_REDUCE", ns, P(gy), P(a["out"]), P(a["z2"]), P(b2.mean), P(b2.rstd),
-               P(a.get("zd")), P(bd.mean) if bd else 0, P(bd.rstd) if bd else 0, P(bpart), R, Co, ch)
-            fin_bwd(b2, Tb, R, 1)
+            dzm, din = gcur, nxt  # dzm: ReLU-masked grad wrt this block's output
+            if bn2_src is None:  # last block: gradient from the head
+                ch = chunk_for(Co)
+                Tb = (R + ch - 1) // ch
+                op("BN_BWD_REDUCE", 3 if bd is not None else 2, P(gcur), P(a["out"]), P(a["z2"]), P(b2.mean),
+                   P(b2.rstd), P(a.get("zd")), P(bd.mean) if bd else 0, P(bd.rstd) if bd else 0, P(bpart), R, Co, ch,
+                   P(dzm))
+                bn2_src = (bpart.data_ptr(), Tb)
+            base, T2 = bn2_src
+            fin_bwd(b2, T2, R, 1, base)
             if bd is not None:
-                fin_bwd(bd, Tb, R, 2)
-            op("BN_BWD_APPLY", 1 if bd is not None else 0, P(gy), P(a["out"]), P(a["z2"]), P(b2.mean), P(b2.rstd),
+                fin_bwd(bd, T2, R, 2, base)
+            op("BN_BWD_APPLY", 1 if bd is not None else 0, P(dzm), 0, P(a["z2"]), P(b2.mean), P(b2.rstd),
                P(b2.scale), P(b2.c1), P(b2.c2), P(dz2), P(a.get("zd")), P(bd.mean) if bd else 0,
                P(bd.rstd) if bd else 0, P(bd.scale) if bd else 0, P(bd.c2) if bd else 0, P(dzd), R, Co)
             wgrad(dz2, a["a1"], Lo, Co, Lo, Co, 3, 1, 1, blk.conv2.weight)
-            conv(dz2, Lo, Co, self._wb[id(blk.conv2)], ga1, Lo, Co, 3, 1, 1)  # dgrad conv2 (stride 1, pad 1)
-            op("BN_BWD_REDUCE", 2, P(ga1), P(a["a1"]), P(a["z1"]), P(b1.mean), P(b1.rstd), 0, 0, 0, P(bpart), R, Co,
-               ch)
-            fin_bwd(b1, Tb, R, 1)
-            op("BN_BWD_APPLY", 0, P(ga1), P(a["a1"]), P(a["z1"]), P(b1.mean), P(b1.rstd), P(b1.scale), P(b1.c1),
+            # dgrad conv2 (stride 1, pad 1) -> ReLU-masked grad wrt a1 + BN1 backward statistics
+            T1 = self.lib.ecg_conv1d_nlc_fwd_stat_tiles(R, Co)
+            conv(dz2, Lo, Co, self._wb[id(blk.conv2)], ga1, Lo, Co, 3, 1, 1, st=stats,
+                 bnb=(a["a1"], a["z1"], b1.mean, b1.rstd, 0, 0, 0))
+            fin_bwd(b1, T1, R, 1, stats.data_ptr())
+            op("BN_BWD_APPLY", 0, P(ga1), 0, P(a["z1"]), P(b1.mean), P(b1.rstd), P(b1.scale), P(b1.c1),
                P(b1.c2), P(dz1), 0, 0, 0, 0, 0, 0, R, Co)
             wgrad(dz1, a["in"], Li, Ci, Lo, Co, 3, s, 1, blk.conv1.weight)
+            add = dzm
             if bd is not None:
                 wgrad(dzd, a["in"], Li, Ci, Lo, Co, 1, s, 0, blk.downsample[0].weight)
                 conv(dzd, Lo, Co, self._wb[id(blk.downsample[0])], tmp, Li, Ci, 1, 1, 0, dil=s)
-                conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=tmp)
-            else:
-                conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=gy, add_mask=a["out"])
-            gcur, nxt = din, gy
+                add = tmp
+            if bi > 0:  # din is the previous block's output gradient: mask it and emit that block's BN2 stats
+                pa, (_, pb2, pbd) = acts[bi - 1], bns[bi - 1]
+                Tn = self.lib.ecg_conv1d_nlc_fwd_stat_tiles(B * Li, Ci)
+                conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=add, st=stats_b,
+                     bnb=(pa["out"], pa["z2"], pb2.mean, pb2.rstd, pa.get("zd") if pbd else 0,
+                          pbd.mean if pbd else 0, pbd.rstd if pbd else 0))
+                bn2_src = (stats_b.data_ptr(), Tn)
+            else:  # into the stem: plain gradient wrt the pooled activations
+                conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=add)
+            gcur, nxt = din, dzm
             if bi == 0 or stage_of[bi - 1] != stage_of[bi]:  # stage boundary: close a grad segment
                 if stage_of[bi] == 0:
                     break  # layer1 joins the stem segment

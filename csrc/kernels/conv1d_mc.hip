@@ -38,6 +38,17 @@ struct FwdArgs {
   const __bf16* add;  // [B*Lout][Cout] added before the store (residual-gradient path), or null
   const __bf16* add_mask;  // if non-null the added term is add * (add_mask > 0)  (ReLU backward of the residual)
   int B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil, relu;
+  // BatchNorm-backward statistics mode (stat_mode == 1; data-grad convs): the stored value is masked by
+  // smask > 0 (ReLU backward) and the partials are sum(v), sum(v * xhat) [, sum(v * xhat_d)] with
+  // xhat = (sz - smean) * srstd (and the downsample branch's szd / smean_d / srstd_d when szd != null).
+  int stat_mode;
+  const __bf16* smask;
+  const __bf16* sz;
+  const float* smean;
+  const float* srstd;
+  const __bf16* szd;
+  const float* smean_d;
+  const float* srstd_d;
 };
 
 // A tile: 64 rows (b,t) x 64 kk (one tap k, channels c0..c0+63); element e (0..511) = row e>>3, 8 bf16 part e&7
@@ -81,7 +92,7 @@ struct FwdCfg {
   static constexpr int A_EL = BM * LDS_ROW, B_EL = BN * LDS_ROW;
   static constexpr int STAGE_BYTES = 2 * (A_EL + B_EL) * 2;
   static constexpr int EP_LD = WN + 4;
-  static constexpr int EP_BYTES = 4 * WM * EP_LD * 4 + 2 * 2 * BN * 4;
+  static constexpr int EP_BYTES = 4 * WM * EP_LD * 4 + 2 * 3 * BN * 4;
   static constexpr int SMEM = STAGE_BYTES > EP_BYTES ? STAGE_BYTES : EP_BYTES;
 };
 
@@ -211,11 +222,16 @@ __global__ __launch_bounds__(THREADS, (PF == 2 && BM * BN > 8192 ? 1 : 2)) void 
   constexpr int CG = WN / 8, RSTEP = 64 / CG, ITEMS = WM / RSTEP;
   const int cg = lane % CG, rs = lane / CG;
   const int n = n0 + wc * WN + cg * 8;
-  float bv[8], s[8], ss[8];
+  const bool bwd = a.stat_mode == 1, ds = bwd && a.szd != nullptr;
+  float bv[8], s1[8], s2[8], s3[8], mu[8], rsd[8], mud[8], rsdd[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     bv[e] = a.bias ? a.bias[n + e] : 0.f;
-    s[e] = ss[e] = 0.f;
+    s1[e] = s2[e] = s3[e] = 0.f;
+    mu[e] = bwd ? a.smean[n + e] : 0.f;
+    rsd[e] = bwd ? a.srstd[n + e] : 0.f;
+    mud[e] = ds ? a.smean_d[n + e] : 0.f;
+    rsdd[e] = ds ? a.srstd_d[n + e] : 0.f;
   }
 #pragma unroll 2
   for (int it = 0; it < ITEMS; ++it) {
@@ -239,38 +255,63 @@ __global__ __launch_bounds__(THREADS, (PF == 2 && BM * BN > 8192 ? 1 : 2)) void 
           for (int e = 0; e < 8; ++e) v[e] += (float)ad[e];
         }
       }
+      if (bwd && a.smask) {
+        const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.smask + o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (float)mk[e] > 0.f ? v[e] : 0.f;
+      }
       bf16x8 outv;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         if (a.relu) v[e] = fmaxf(v[e], 0.f);
         outv[e] = (__bf16)v[e];
-        const float rv = (float)outv[e];
-        s[e] += rv;
-        ss[e] += rv * rv;
+        v[e] = (float)outv[e];
       }
       *reinterpret_cast<bf16x8*>(a.y + o) = outv;
+      if (bwd) {
+        const bf16x8 zz = *reinterpret_cast<const bf16x8*>(a.sz + o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s1[e] += v[e];
+          s2[e] += v[e] * ((float)zz[e] - mu[e]) * rsd[e];
+        }
+        if (ds) {
+          const bf16x8 zd = *reinterpret_cast<const bf16x8*>(a.szd + o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s3[e] += v[e] * ((float)zd[e] - mud[e]) * rsdd[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s1[e] += v[e];
+          s2[e] += v[e] * v[e];
+        }
+      }
     }
   }
   if (a.stats) {  // block-uniform
+    const int NS = ds ? 3 : 2;
 #pragma unroll
     for (int off = CG; off < 64; off <<= 1)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        s[e] += __shfl_xor(s[e], off);
-        ss[e] += __shfl_xor(ss[e], off);
+        s1[e] += __shfl_xor(s1[e], off);
+        s2[e] += __shfl_xor(s2[e], off);
+        if (ds) s3[e] += __shfl_xor(s3[e], off);
       }
     float* sred = reinterpret_cast<float*>(smem) + 4 * WM * EP_LD;  // [wr][stat][BN]
     if (lane < CG) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        sred[(wr * 2 + 0) * BN + wc * WN + cg * 8 + e] = s[e];
-        sred[(wr * 2 + 1) * BN + wc * WN + cg * 8 + e] = ss[e];
+        sred[(wr * 3 + 0) * BN + wc * WN + cg * 8 + e] = s1[e];
+        sred[(wr * 3 + 1) * BN + wc * WN + cg * 8 + e] = s2[e];
+        sred[(wr * 3 + 2) * BN + wc * WN + cg * 8 + e] = s3[e];
       }
     }
     __syncthreads();
-    if (tid < 2 * BN) {
-      const int st = tid / BN, c = tid % BN;
-      a.stats[((long)st * MT + mt) * a.Cout + n0 + c] = sred[st * BN + c] + sred[(2 + st) * BN + c];
+    for (int i = tid; i < NS * BN; i += THREADS) {
+      const int st = i / BN, c = i % BN;
+      a.stats[((long)st * MT + mt) * a.Cout + n0 + c] = sred[st * BN + c] + sred[(3 + st) * BN + c];
     }
   }
 }
@@ -524,15 +565,28 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t stream) {
 // in_dil > 1 reads x as zero-inserted with that dilation (used for the data-gradient of strided convs).
 // Extended form used by the ResNet step plan: ``stats`` receives [2][ceil(B*Lout/64)][Cout] BN partials;
 // ``add`` (optionally masked by ``add_mask`` > 0) is added to the output before rounding.
+// ``bnb`` (optional, stat_mode 1): {smask, sz, smean, srstd, szd, smean_d, srstd_d} of the BatchNorm whose
+// backward statistics the data-grad epilogue produces ([2 or 3][M tiles][Cout] into ``stats``).
 ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bias, void* y, float* stats,
                                   const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
-                                  int Kw, int stride, int pad, int in_dil, int relu, hipStream_t stream) {
+                                  int Kw, int stride, int pad, int in_dil, int relu, const void* const* bnb,
+                                  hipStream_t stream) {
   if (!x || !w || !y || B <= 0 || Lin <= 0 || Lout <= 0 || Kw <= 0 || stride <= 0 || in_dil <= 0 || pad < 0)
     return ecg::kBadArg;
   if (Cin % BK != 0 || Cout % 64 != 0 || (add_mask && !add)) return ecg::kBadArg;
+  if (bnb && (!stats || !bnb[1] || !bnb[2] || !bnb[3] || (bnb[4] && (!bnb[5] || !bnb[6])))) return ecg::kBadArg;
   FwdArgs a{static_cast<const __bf16*>(x), static_cast<const __bf16*>(w), bias, static_cast<__bf16*>(y), stats,
             static_cast<const __bf16*>(add), static_cast<const __bf16*>(add_mask),
-            B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil, relu};
+            B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil, relu, bnb ? 1 : 0};
+  if (bnb) {
+    a.smask = static_cast<const __bf16*>(bnb[0]);
+    a.sz = static_cast<const __bf16*>(bnb[1]);
+    a.smean = static_cast<const float*>(bnb[2]);
+    a.srstd = static_cast<const float*>(bnb[3]);
+    a.szd = static_cast<const __bf16*>(bnb[4]);
+    a.smean_d = static_cast<const float*>(bnb[5]);
+    a.srstd_d = static_cast<const float*>(bnb[6]);
+  }
   int bm, bn;
   pick_fwd_tile((long)B * Lout, Cout, &bm, &bn);
   if (bm == 128 && bn == 128) return launch_fwd<128, 128>(a, stream);
@@ -551,7 +605,7 @@ ECG_API int ecg_conv1d_nlc_fwd(const void* x, const void* w, const float* bias, 
                                int Lout, int Cout, int Kw, int stride, int pad, int in_dil, int relu,
                                hipStream_t stream) {
   return ecg_conv1d_nlc_fwd_ex(x, w, bias, y, nullptr, nullptr, nullptr, B, Lin, Cin, Lout, Cout, Kw, stride, pad,
-                               in_dil, relu, stream);
+                               in_dil, relu, nullptr, stream);
 }
 
 // Partial weight gradients: part[splits][Cout][Kw*Cin] fp32 (sum over dim 0 = dw in [Cout][Kw][Cin]).

@@ -29,7 +29,8 @@
 
 extern "C" int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bias, void* y, float* stats,
                                      const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout,
-                                     int Cout, int Kw, int stride, int pad, int in_dil, int relu, hipStream_t stream);
+                                     int Cout, int Kw, int stride, int pad, int in_dil, int relu,
+                                     const void* const* bnb, hipStream_t stream);
 extern "C" int ecg_conv1d_nlc_wgrad(const void* dy, const void* x, float* part, int splits, int B, int Lin, int Cin,
                                     int Lout, int Cout, int Kw, int stride, int pad, hipStream_t stream);
 extern "C" int ecg_sgd_flat(float* params, const float* grads, float* mom, long n, float lr, float momentum,
@@ -498,7 +499,7 @@ __global__ __launch_bounds__(TPB) void bn_bwd_reduce_kernel(
     const __bf16* __restrict__ gy, const __bf16* __restrict__ msk, const __bf16* __restrict__ z,
     const float* __restrict__ mean, const float* __restrict__ rstd, const __bf16* __restrict__ zd,
     const float* __restrict__ mean_d, const float* __restrict__ rstd_d, float* __restrict__ part, long R, int C,
-    int chunk) {
+    int chunk, __bf16* __restrict__ dzm) {
   __shared__ float red[TPB * 8 * 3];
   const int cg = C / 8, tid = threadIdx.x;
   const int rpp = TPB / cg, roff = tid / cg, c0 = (tid % cg) * 8;
@@ -520,8 +521,15 @@ __global__ __launch_bounds__(TPB) void bn_bwd_reduce_kernel(
     ld8(msk + o, m);
     ld8(z + o, zf);
 #pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = m[i] > 0.f ? g[i] : 0.f;
+    if (dzm) {  // optional masked copy (the block's ReLU-backward output, consumed by the apply/dgrad ops)
+      st8(dzm + o, g);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = (float)(__bf16)g[i];
+    }
+#pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float d = m[i] > 0.f ? g[i] : 0.f;
+      const float d = g[i];
       a1[i] += d;
       a2[i] += d * (zf[i] - mu[i]) * rs[i];
     }
@@ -529,10 +537,7 @@ __global__ __launch_bounds__(TPB) void bn_bwd_reduce_kernel(
       float zdf[8];
       ld8(zd + o, zdf);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float d = m[i] > 0.f ? g[i] : 0.f;
-        a3[i] += d * (zdf[i] - mud[i]) * rsd[i];
-      }
+      for (int i = 0; i < 8; ++i) a3[i] += g[i] * (zdf[i] - mud[i]) * rsd[i];
     }
   }
   if (active) {
@@ -568,7 +573,12 @@ __global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(
     const long o = v * 8;
     float g[8], m[8], zf[8], mu[8], rs[8], sc[8], k1[8], k2[8], y[8];
     ld8(gy + o, g);
-    ld8(msk + o, m);
+    if (msk) {
+      ld8(msk + o, m);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) m[i] = 1.f;
+    }
     ld8(z + o, zf);
     ldf8(mean + c0, mu);
     ldf8(rstd + c0, rs);
@@ -872,10 +882,14 @@ inline int fin_mode() {
 int run_op(const int64_t* o, hipStream_t st) {
   const int kind = (int)o[0];
   switch (kind) {
-    case OP_CONV_FWD:
+    case OP_CONV_FWD: {  // words 18..24: BN-backward statistics operands (stat_mode 1 when o[19] != 0)
+      const void* bnb[7] = {P<void>(o[18]), P<void>(o[19]), P<void>(o[20]), P<void>(o[21]),
+                            P<void>(o[22]), P<void>(o[23]), P<void>(o[24])};
       return ecg_conv1d_nlc_fwd_ex(P<void>(o[1]), P<void>(o[2]), P<float>(o[3]), P<void>(o[4]), P<float>(o[5]),
                                    P<void>(o[6]), P<void>(o[7]), (int)o[8], (int)o[9], (int)o[10], (int)o[11],
-                                   (int)o[12], (int)o[13], (int)o[14], (int)o[15], (int)o[16], (int)o[17], st);
+                                   (int)o[12], (int)o[13], (int)o[14], (int)o[15], (int)o[16], (int)o[17],
+                                   o[19] ? bnb : nullptr, st);
+    }
     case OP_CONV_WGRAD:
       return ecg_conv1d_nlc_wgrad(P<void>(o[1]), P<void>(o[2]), P<float>(o[3]), (int)o[4], (int)o[5], (int)o[6],
                                   (int)o[7], (int)o[8], (int)o[9], (int)o[10], (int)o[11], (int)o[12], st);
@@ -947,11 +961,12 @@ int run_op(const int64_t* o, hipStream_t st) {
       if (ns == 2)
         hipLaunchKernelGGL(bn_bwd_reduce_kernel<2>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]), P<const __bf16>(o[3]),
                            P<const __bf16>(o[4]), P<const float>(o[5]), P<const float>(o[6]), nullptr, nullptr,
-                           nullptr, P<float>(o[10]), R, C, chunk);
+                           nullptr, P<float>(o[10]), R, C, chunk, P<__bf16>(o[14]));
       else
         hipLaunchKernelGGL(bn_bwd_reduce_kernel<3>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]), P<const __bf16>(o[3]),
                            P<const __bf16>(o[4]), P<const float>(o[5]), P<const float>(o[6]), P<const __bf16>(o[7]),
-                           P<const float>(o[8]), P<const float>(o[9]), P<float>(o[10]), R, C, chunk);
+                           P<const float>(o[8]), P<const float>(o[9]), P<float>(o[10]), R, C, chunk,
+                           P<__bf16>(o[14]));
       break;
     }
     case OP_BN_BWD_APPLY: {
