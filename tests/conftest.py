@@ -8,7 +8,17 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def pytest_addoption(parser):
+    parser.addoption("--hip-serialize", action="store_true",
+                     help="debug mode: AMD_SERIALIZE_KERNEL=3 + HIP_LAUNCH_BLOCKING=1 (every launch synchronous, so "
+                          "a faulting kernel is reported at its own launch)")
+
+
 def pytest_configure(config):
+    if config.getoption("--hip-serialize", default=False):
+        os.environ["AMD_SERIALIZE_KERNEL"] = "3"
+        os.environ["HIP_LAUNCH_BLOCKING"] = "1"
+        os.environ["AMD_SERIALIZE_COPY"] = "3"
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the HIP kernels")
     config.addinivalue_line("markers", "slow: multi-process or long-running test")
     # Build (incrementally, seconds when cached) the native libraries so CPU tests can load the
