@@ -49,6 +49,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_plan_stem_rows", [])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles", [ctypes.c_long, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_tiles", [i32, i32, i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles_ex", [i32, i32, i32, i32])
     lib._plan_bound = True
     if lib.ecg_plan_op_words() != OP_WORDS or lib.ecg_plan_wentry_bytes() != 40:
         raise _lib.NativeError("resnet plan ABI mismatch (rebuild csrc)")
@@ -348,7 +349,7 @@ class ResNetStepEngine:
                 add = tmp
             if bi > 0:  # din is the previous block's output gradient: mask it and emit that block's BN2 stats
                 pa, (_, pb2, pbd) = acts[bi - 1], bns[bi - 1]
-                Tn = self.lib.ecg_conv1d_nlc_fwd_stat_tiles(B * Li, Ci)
+                Tn = self.lib.ecg_conv1d_nlc_fwd_stat_tiles_ex(B, Li, Ci, s)  # phase-decomposed when s > 1
                 conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=add, st=stats_b,
                      bnb=(pa["out"], pa["z2"], pb2.mean, pb2.rstd, pa.get("zd") if pbd else 0,
                           pbd.mean if pbd else 0, pbd.rstd if pbd else 0))

@@ -19,7 +19,6 @@
 #include "../include/ecg_common.h"
 
 #include <climits>
-#include <cstdlib>
 
 namespace {
 
@@ -42,6 +41,7 @@ struct FwdArgs {
   // smask > 0 (ReLU backward) and the partials are sum(v), sum(v * xhat) [, sum(v * xhat_d)] with
   // xhat = (sz - smean) * srstd (and the downsample branch's szd / smean_d / srstd_d when szd != null).
   int stat_mode;
+  int Lph, tpp;  // strided data-grad (in_dil > 1): output rows per sample per phase, M tiles per phase
   const __bf16* smask;
   const __bf16* sz;
   const float* smean;
@@ -96,9 +96,8 @@ struct FwdCfg {
   static constexpr int SMEM = STAGE_BYTES > EP_BYTES ? STAGE_BYTES : EP_BYTES;
 };
 
-template <int BM, int BN, int PF>
-__global__ __launch_bounds__(THREADS, (PF == 2 && BM * BN > 8192 ? 1 : 2)) void conv1d_nlc_fwd_kernel(FwdArgs a, int MT,
-                                                                                                  int NT) {
+template <int BM, int BN, int EPI>
+__global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_kernel(FwdArgs a, int MT, int NT) {
   using Cfg = FwdCfg<BM, BN>;
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NA = Cfg::NA, NB = Cfg::NB;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -110,34 +109,44 @@ __global__ __launch_bounds__(THREADS, (PF == 2 && BM * BN > 8192 ? 1 : 2)) void 
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
   const int mt = wgid / NT, nt = wgid % NT;
-  const int m0 = mt * BM, n0 = nt * BN;
   const int K = a.Kw * a.Cin;
-  const int nk = K / BK;
+  // Strided data-grad (in_dil = s > 1) is phase-decomposed: output rows u = i*s + ph of one phase share the
+  // taps k = k0 + j*s (k0 = (pad - ph) mod s) that hit non-inserted input rows, so the zero half of the
+  // dilated input is never multiplied.  M tiles are per phase; K tiles run over the phase's taps only.
+  const int P = a.in_dil;
+  const int ph = P > 1 ? mt / a.tpp : 0;
+  const int m0 = (P > 1 ? mt - ph * a.tpp : mt) * BM, n0 = nt * BN;
+  const int CB = a.Cin / BK;
+  const int k0 = P > 1 ? ((a.pad - ph) % P + P) % P : 0;
+  const int nk = P > 1 ? (k0 < a.Kw ? (a.Kw - k0 + P - 1) / P : 0) * CB : K / BK;
   f32x4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // Two register sets: set 0 holds even K tiles, set 1 odd ones.  Tile t+3's loads are issued while tile t is
-  // multiplied, so each load has two full MFMA phases to land (the loop is unrolled by two to keep the set
-  // index compile-time).  Tiles past the end are clamped to the last one (unconditional, register-resident).
-  uint4 ra0[NA], rb0[NB], ra1[PF == 2 ? NA : 1], rb1[PF == 2 ? NB : 1];
+  // One register set: tile t+1's global loads are in flight during tile t's MFMAs.  (Measured alternatives,
+  // profiles/r1_resnet/conv_microbench_*: a second register set (tile t+2 in flight) costs occupancy and runs
+  // 35 % slower; B fragments loaded straight from L2 into registers, bypassing LDS, 25-35 % slower.)
+  uint4 ra0[NA], rb0[NB];
   // per-thread A rows are fixed across K tiles: precompute each row's sample base and first input position
-  const int M = a.B * a.Lout;
+  const int Lrow = P > 1 ? a.Lph : a.Lout;  // rows per sample in this kernel's (phase-local) M index
+  const int M = a.B * Lrow;
   long abase[NA];
   int apos[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
     const int e = tid + i * THREADS, m = m0 + (e >> 3);
-    const int b = m / a.Lout, t = m % a.Lout;
+    const int b = m / Lrow, t = m % Lrow;
+    const int u = P > 1 ? t * P + ph : t;  // output position
     abase[i] = (long)b * a.Lin * a.Cin + (e & 7) * 8;
-    apos[i] = m < M ? t * a.stride - a.pad : INT_MIN / 2;  // invalid rows never pass the range check
+    apos[i] = (m < M && u < a.Lout) ? u * a.stride - a.pad : INT_MIN / 2;  // invalid rows never pass the check
   }
   const __bf16* wb = a.w + (long)(n0 + (tid >> 3)) * (a.Kw * a.Cin) + (tid & 7) * 8;
   const int Lext = a.in_dil > 1 ? (a.Lin - 1) * a.in_dil + 1 : a.Lin;  // extent of the (dilated) input
   auto ld_set = [&](uint4* ra, uint4* rb, int t) {
-    const int kk = (t < nk ? t : nk - 1) * BK;
-    const int k = kk / a.Cin, c0 = kk - k * a.Cin;
+    const int tc = t < nk ? t : nk - 1;
+    const int k = k0 + (tc / CB) * P, c0 = (tc % CB) * BK;
+    const int kk = k * a.Cin + c0;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       int u = apos[i] + k;
@@ -180,24 +189,7 @@ __global__ __launch_bounds__(THREADS, (PF == 2 && BM * BN > 8192 ? 1 : 2)) void 
   };
   __bf16* const L0 = lds;
   __bf16* const L1 = lds + (Cfg::A_EL + Cfg::B_EL);
-  if constexpr (PF == 2) {
-    ld_set(ra0, rb0, 0);
-    st_set(L0, ra0, rb0);
-    ld_set(ra1, rb1, 1);
-    ld_set(ra0, rb0, 2);
-    __syncthreads();
-    for (int kt = 0; kt < nk; kt += 2) {
-      mma(L0);                // tile kt (even)
-      st_set(L1, ra1, rb1);   // tile kt+1
-      ld_set(ra1, rb1, kt + 3);
-      __syncthreads();
-      if (kt + 1 >= nk) break;  // block-uniform
-      mma(L1);                // tile kt+1
-      st_set(L0, ra0, rb0);   // tile kt+2
-      ld_set(ra0, rb0, kt + 4);
-      __syncthreads();
-    }
-  } else {  // one register set: tile t+1's loads in flight during tile t's MFMAs
+  if (nk > 0) {  // block-uniform (a phase without taps leaves acc = 0)
     ld_set(ra0, rb0, 0);
     st_set(L0, ra0, rb0);
     __syncthreads();
@@ -222,14 +214,19 @@ __global__ __launch_bounds__(THREADS, (PF == 2 && BM * BN > 8192 ? 1 : 2)) void 
   constexpr int CG = WN / 8, RSTEP = 64 / CG, ITEMS = WM / RSTEP;
   const int cg = lane % CG, rs = lane / CG;
   const int n = n0 + wc * WN + cg * 8;
-  const bool bwd = a.stat_mode == 1, ds = bwd && a.szd != nullptr;
+  constexpr bool bwd = EPI == 1;  // compile-time: the forward epilogue carries none of the backward code
+  const bool ds = bwd && a.szd != nullptr;
   float bv[8], s1[8], s2[8], s3[8], mu[8], rsd[8], mud[8], rsdd[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     bv[e] = a.bias ? a.bias[n + e] : 0.f;
     s1[e] = s2[e] = s3[e] = 0.f;
-    mu[e] = bwd ? a.smean[n + e] : 0.f;
-    rsd[e] = bwd ? a.srstd[n + e] : 0.f;
+    mu[e] = 0.f;
+    rsd[e] = 0.f;
+    if constexpr (bwd) {
+      mu[e] = a.smean[n + e];
+      rsd[e] = a.srstd[n + e];
+    }
     mud[e] = ds ? a.smean_d[n + e] : 0.f;
     rsdd[e] = ds ? a.srstd_d[n + e] : 0.f;
   }
@@ -237,8 +234,10 @@ __global__ __launch_bounds__(THREADS, (PF == 2 && BM * BN > 8192 ? 1 : 2)) void 
   for (int it = 0; it < ITEMS; ++it) {
     const int r = rs + it * RSTEP;
     const int m = m0 + wr * WM + r;
-    if (m < M) {
-      const long o = (long)m * a.Cout + n;
+    const int bb = m / Lrow, tt = m - bb * Lrow;
+    const int uu = P > 1 ? tt * P + ph : tt;
+    if (m < M && uu < a.Lout) {
+      const long o = ((long)bb * a.Lout + uu) * a.Cout + n;
       const float4 v0 = *reinterpret_cast<const float4*>(ep + r * EP_LD + cg * 8);
       const float4 v1 = *reinterpret_cast<const float4*>(ep + r * EP_LD + cg * 8 + 4);
       float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
@@ -255,7 +254,7 @@ __global__ __launch_bounds__(THREADS, (PF == 2 && BM * BN > 8192 ? 1 : 2)) void 
           for (int e = 0; e < 8; ++e) v[e] += (float)ad[e];
         }
       }
-      if (bwd && a.smask) {
+      if (bwd && a.smask != nullptr) {
         const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.smask + o);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = (float)mk[e] > 0.f ? v[e] : 0.f;
@@ -268,7 +267,7 @@ __global__ __launch_bounds__(THREADS, (PF == 2 && BM * BN > 8192 ? 1 : 2)) void 
         v[e] = (float)outv[e];
       }
       *reinterpret_cast<bf16x8*>(a.y + o) = outv;
-      if (bwd) {
+      if constexpr (bwd) {
         const bf16x8 zz = *reinterpret_cast<const bf16x8*>(a.sz + o);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -331,36 +330,34 @@ inline void pick_fwd_tile(long M, int Cout, int* bm, int* bn) {
   }
 }
 
-// ECG_CONV_PF=1|2 selects the register prefetch depth (default 1; read once).
-inline int prefetch_depth() {
-  static int pf = -1;
-  if (pf < 0) {
-    const char* e = getenv("ECG_CONV_PF");
-    pf = (e && atoi(e) == 2) ? 2 : 1;
-  }
-  return pf;
-}
-
-template <int BM, int BN, int PF>
-int launch_fwd_pf(const FwdArgs& a, hipStream_t stream) {
+template <int BM, int BN, int EPI>
+int launch_fwd_epi(const FwdArgs& a, hipStream_t stream) {
   using Cfg = FwdCfg<BM, BN>;
   static bool attr = false;
   if (!attr) {
-    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_kernel<BM, BN, PF>,
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_kernel<BM, BN, EPI>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::SMEM));
     attr = true;
   }
-  const long M = (long)a.B * a.Lout;
-  const int MT = (int)((M + BM - 1) / BM), NT = a.Cout / BN;
-  hipLaunchKernelGGL((conv1d_nlc_fwd_kernel<BM, BN, PF>), dim3((unsigned)(MT * NT)), dim3(THREADS), Cfg::SMEM,
-                     stream, a, MT, NT);
+  FwdArgs b = a;
+  int MT;
+  if (a.in_dil > 1) {
+    b.Lph = (a.Lout + a.in_dil - 1) / a.in_dil;
+    b.tpp = (int)(((long)a.B * b.Lph + BM - 1) / BM);
+    MT = a.in_dil * b.tpp;
+  } else {
+    MT = (int)(((long)a.B * a.Lout + BM - 1) / BM);
+  }
+  const int NT = a.Cout / BN;
+  hipLaunchKernelGGL((conv1d_nlc_fwd_kernel<BM, BN, EPI>), dim3((unsigned)(MT * NT)), dim3(THREADS), Cfg::SMEM,
+                     stream, b, MT, NT);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
 
 template <int BM, int BN>
 int launch_fwd(const FwdArgs& a, hipStream_t stream) {
-  return prefetch_depth() == 2 ? launch_fwd_pf<BM, BN, 2>(a, stream) : launch_fwd_pf<BM, BN, 1>(a, stream);
+  return a.stat_mode == 1 ? launch_fwd_epi<BM, BN, 1>(a, stream) : launch_fwd_epi<BM, BN, 0>(a, stream);
 }
 
 // ------------------------------------------------------------------------------------------- weight grad
@@ -599,6 +596,15 @@ ECG_API int ecg_conv1d_nlc_fwd_stat_tiles(long M, int Cout) {
   int bm, bn;
   pick_fwd_tile(M, Cout, &bm, &bn);
   return (int)((M + bm - 1) / bm);
+}
+
+// Same for a call with batch B, output length Lout and input dilation in_dil (phase-decomposed data-grad).
+ECG_API int ecg_conv1d_nlc_fwd_stat_tiles_ex(int B, int Lout, int Cout, int in_dil) {
+  int bm, bn;
+  pick_fwd_tile((long)B * Lout, Cout, &bm, &bn);
+  if (in_dil <= 1) return (int)(((long)B * Lout + bm - 1) / bm);
+  const int Lph = (Lout + in_dil - 1) / in_dil;
+  return in_dil * (int)(((long)B * Lph + bm - 1) / bm);
 }
 
 ECG_API int ecg_conv1d_nlc_fwd(const void* x, const void* w, const float* bias, void* y, int B, int Lin, int Cin,
