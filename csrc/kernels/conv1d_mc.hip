@@ -19,6 +19,7 @@
 #include "../include/ecg_common.h"
 
 #include <climits>
+#include <cstdlib>
 
 namespace {
 
@@ -90,14 +91,17 @@ struct FwdCfg {
   static constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   static constexpr int NA = BM * 8 / THREADS, NB = BN * 8 / THREADS;
   static constexpr int A_EL = BM * LDS_ROW, B_EL = BN * LDS_ROW;
-  static constexpr int STAGE_BYTES = 2 * (A_EL + B_EL) * 2;
   static constexpr int EP_LD = WN + 4;
-  static constexpr int EP_BYTES = 4 * WM * EP_LD * 4 + 2 * 3 * BN * 4;
-  static constexpr int SMEM = STAGE_BYTES > EP_BYTES ? STAGE_BYTES : EP_BYTES;
+  static constexpr int EP_BYTES = 4 * (WM / 2) * EP_LD * 4 + 2 * 3 * BN * 4;  // epilogue staged in two halves
+  static constexpr int stage_bytes(int nbuf) { return nbuf * (A_EL + B_EL) * 2; }
+  static constexpr int smem(int nbuf) { return stage_bytes(nbuf) > EP_BYTES ? stage_bytes(nbuf) : EP_BYTES; }
 };
 
-template <int BM, int BN, int EPI>
-__global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_kernel(FwdArgs a, int MT, int NT) {
+// NBUF = 2: double-buffered LDS, one barrier per K tile (2 workgroups / CU at 128x128).
+// NBUF = 1: one LDS buffer, two barriers per K tile, half the LDS -> 3 workgroups / CU, i.e. 1.5x the
+//           register-staged tiles in flight per CU for this HBM-latency-bound loop.
+template <int BM, int BN, int EPI, int NBUF>
+__global__ __launch_bounds__(THREADS, NBUF == 1 ? 3 : 2) void conv1d_nlc_fwd_kernel(FwdArgs a, int MT, int NT) {
   using Cfg = FwdCfg<BM, BN>;
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NA = Cfg::NA, NB = Cfg::NB;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -188,30 +192,29 @@ __global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_kernel(FwdArgs a, i
     }
   };
   __bf16* const L0 = lds;
-  __bf16* const L1 = lds + (Cfg::A_EL + Cfg::B_EL);
+  __bf16* const L1 = lds + (NBUF == 2 ? Cfg::A_EL + Cfg::B_EL : 0);
   if (nk > 0) {  // block-uniform (a phase without taps leaves acc = 0)
     ld_set(ra0, rb0, 0);
     st_set(L0, ra0, rb0);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       ld_set(ra0, rb0, kt + 1);
-      mma((kt & 1) ? L1 : L0);
-      st_set((kt & 1) ? L0 : L1, ra0, rb0);
+      if constexpr (NBUF == 2) {
+        mma((kt & 1) ? L1 : L0);
+        st_set((kt & 1) ? L0 : L1, ra0, rb0);
+      } else {
+        mma(L0);
+        __syncthreads();  // every wave is done reading the buffer
+        st_set(L0, ra0, rb0);
+      }
       __syncthreads();
     }
   }
-  // ---- epilogue 1: fragments -> LDS (fp32, per-wave region); staging buffers are dead after the last barrier
-  constexpr int EP_LD = Cfg::EP_LD;
-  float* ep = reinterpret_cast<float*>(smem) + wv * WM * EP_LD;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) ep[(i * 16 + 4 * (lane >> 4) + q) * EP_LD + j * 16 + (lane & 15)] = acc[i][j][q];
-  __syncthreads();
-  // ---- epilogue 2: row-major, 8 channels per lane
-  constexpr int CG = WN / 8, RSTEP = 64 / CG, ITEMS = WM / RSTEP;
+  // ---- epilogue: fragments -> LDS (fp32, per-wave region, two halves of WM/2 rows) -> row-major pass with
+  // 8 channels per lane.  The staging buffers are dead after the last barrier.
+  constexpr int EP_LD = Cfg::EP_LD, HR = WM / 2;
+  float* ep = reinterpret_cast<float*>(smem) + wv * HR * EP_LD;
+  constexpr int CG = WN / 8, RSTEP = 64 / CG, ITEMS = HR / RSTEP;
   const int cg = lane % CG, rs = lane / CG;
   const int n = n0 + wc * WN + cg * 8;
   constexpr bool bwd = EPI == 1;  // compile-time: the forward epilogue carries none of the backward code
@@ -230,60 +233,73 @@ __global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_kernel(FwdArgs a, i
     mud[e] = ds ? a.smean_d[n + e] : 0.f;
     rsdd[e] = ds ? a.srstd_d[n + e] : 0.f;
   }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h) __syncthreads();  // previous half fully read
+#pragma unroll
+    for (int i = 0; i < FM / 2; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          ep[(i * 16 + 4 * (lane >> 4) + q) * EP_LD + j * 16 + (lane & 15)] = acc[h * (FM / 2) + i][j][q];
+    __syncthreads();
 #pragma unroll 2
-  for (int it = 0; it < ITEMS; ++it) {
-    const int r = rs + it * RSTEP;
-    const int m = m0 + wr * WM + r;
-    const int bb = m / Lrow, tt = m - bb * Lrow;
-    const int uu = P > 1 ? tt * P + ph : tt;
-    if (m < M && uu < a.Lout) {
-      const long o = ((long)bb * a.Lout + uu) * a.Cout + n;
-      const float4 v0 = *reinterpret_cast<const float4*>(ep + r * EP_LD + cg * 8);
-      const float4 v1 = *reinterpret_cast<const float4*>(ep + r * EP_LD + cg * 8 + 4);
-      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    for (int it = 0; it < ITEMS; ++it) {
+      const int rl = rs + it * RSTEP;
+      const int r = h * HR + rl;
+      const int m = m0 + wr * WM + r;
+      const int bb = m / Lrow, tt = m - bb * Lrow;
+      const int uu = P > 1 ? tt * P + ph : tt;
+      if (m < M && uu < a.Lout) {
+        const long o = ((long)bb * a.Lout + uu) * a.Cout + n;
+        const float4 v0 = *reinterpret_cast<const float4*>(ep + rl * EP_LD + cg * 8);
+        const float4 v1 = *reinterpret_cast<const float4*>(ep + rl * EP_LD + cg * 8 + 4);
+        float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += bv[e];
-      if (a.add) {
-        const bf16x8 ad = *reinterpret_cast<const bf16x8*>(a.add + o);
-        if (a.add_mask) {
-          const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.add_mask + o);
+        for (int e = 0; e < 8; ++e) v[e] += bv[e];
+        if (a.add) {
+          const bf16x8 ad = *reinterpret_cast<const bf16x8*>(a.add + o);
+          if (a.add_mask) {
+            const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.add_mask + o);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += (float)mk[e] > 0.f ? (float)ad[e] : 0.f;
+            for (int e = 0; e < 8; ++e) v[e] += (float)mk[e] > 0.f ? (float)ad[e] : 0.f;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += (float)ad[e];
+          }
+        }
+        if (bwd && a.smask != nullptr) {
+          const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.smask + o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = (float)mk[e] > 0.f ? v[e] : 0.f;
+        }
+        bf16x8 outv;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (a.relu) v[e] = fmaxf(v[e], 0.f);
+          outv[e] = (__bf16)v[e];
+          v[e] = (float)outv[e];
+        }
+        *reinterpret_cast<bf16x8*>(a.y + o) = outv;
+        if constexpr (bwd) {
+          const bf16x8 zz = *reinterpret_cast<const bf16x8*>(a.sz + o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            s1[e] += v[e];
+            s2[e] += v[e] * ((float)zz[e] - mu[e]) * rsd[e];
+          }
+          if (ds) {
+            const bf16x8 zd = *reinterpret_cast<const bf16x8*>(a.szd + o);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s3[e] += v[e] * ((float)zd[e] - mud[e]) * rsdd[e];
+          }
         } else {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += (float)ad[e];
-        }
-      }
-      if (bwd && a.smask != nullptr) {
-        const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.smask + o);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (float)mk[e] > 0.f ? v[e] : 0.f;
-      }
-      bf16x8 outv;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        if (a.relu) v[e] = fmaxf(v[e], 0.f);
-        outv[e] = (__bf16)v[e];
-        v[e] = (float)outv[e];
-      }
-      *reinterpret_cast<bf16x8*>(a.y + o) = outv;
-      if constexpr (bwd) {
-        const bf16x8 zz = *reinterpret_cast<const bf16x8*>(a.sz + o);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          s1[e] += v[e];
-          s2[e] += v[e] * ((float)zz[e] - mu[e]) * rsd[e];
-        }
-        if (ds) {
-          const bf16x8 zd = *reinterpret_cast<const bf16x8*>(a.szd + o);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) s3[e] += v[e] * ((float)zd[e] - mud[e]) * rsdd[e];
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          s1[e] += v[e];
-          s2[e] += v[e] * v[e];
+          for (int e = 0; e < 8; ++e) {
+            s1[e] += v[e];
+            s2[e] += v[e] * v[e];
+          }
         }
       }
     }
@@ -298,7 +314,7 @@ __global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_kernel(FwdArgs a, i
         s2[e] += __shfl_xor(s2[e], off);
         if (ds) s3[e] += __shfl_xor(s3[e], off);
       }
-    float* sred = reinterpret_cast<float*>(smem) + 4 * WM * EP_LD;  // [wr][stat][BN]
+    float* sred = reinterpret_cast<float*>(smem) + 4 * HR * EP_LD;  // [wr][stat][BN]
     if (lane < CG) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -330,13 +346,24 @@ inline void pick_fwd_tile(long M, int Cout, int* bm, int* bn) {
   }
 }
 
-template <int BM, int BN, int EPI>
-int launch_fwd_epi(const FwdArgs& a, hipStream_t stream) {
+// ECG_CONV_NBUF=1|2 selects the LDS buffering of the forward/data-grad kernel (read once; default 1).
+inline int conv_nbuf() {
+  static int nb = -1;
+  if (nb < 0) {
+    const char* e = getenv("ECG_CONV_NBUF");
+    nb = (e && atoi(e) == 2) ? 2 : 1;
+  }
+  return nb;
+}
+
+template <int BM, int BN, int EPI, int NBUF>
+int launch_fwd_cfg(const FwdArgs& a, hipStream_t stream) {
   using Cfg = FwdCfg<BM, BN>;
+  constexpr int SMEM = Cfg::smem(NBUF);
   static bool attr = false;
   if (!attr) {
-    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_kernel<BM, BN, EPI>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::SMEM));
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_kernel<BM, BN, EPI, NBUF>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
     attr = true;
   }
   FwdArgs b = a;
@@ -349,7 +376,7 @@ int launch_fwd_epi(const FwdArgs& a, hipStream_t stream) {
     MT = (int)(((long)a.B * a.Lout + BM - 1) / BM);
   }
   const int NT = a.Cout / BN;
-  hipLaunchKernelGGL((conv1d_nlc_fwd_kernel<BM, BN, EPI>), dim3((unsigned)(MT * NT)), dim3(THREADS), Cfg::SMEM,
+  hipLaunchKernelGGL((conv1d_nlc_fwd_kernel<BM, BN, EPI, NBUF>), dim3((unsigned)(MT * NT)), dim3(THREADS), SMEM,
                      stream, b, MT, NT);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
@@ -357,7 +384,9 @@ int launch_fwd_epi(const FwdArgs& a, hipStream_t stream) {
 
 template <int BM, int BN>
 int launch_fwd(const FwdArgs& a, hipStream_t stream) {
-  return a.stat_mode == 1 ? launch_fwd_epi<BM, BN, 1>(a, stream) : launch_fwd_epi<BM, BN, 0>(a, stream);
+  if (conv_nbuf() == 2)
+    return a.stat_mode == 1 ? launch_fwd_cfg<BM, BN, 1, 2>(a, stream) : launch_fwd_cfg<BM, BN, 0, 2>(a, stream);
+  return a.stat_mode == 1 ? launch_fwd_cfg<BM, BN, 1, 1>(a, stream) : launch_fwd_cfg<BM, BN, 0, 1>(a, stream);
 }
 
 // ------------------------------------------------------------------------------------------- weight grad
