@@ -421,18 +421,19 @@ __device__ __forceinline__ s16x4 tr16(const __bf16* p) {
 }
 
 // Tiles BM (C_out) x BN (taps*C_in), reduction over 64-row chunks of (b,t); both LDS images are [r][col] and
-// the MFMA fragments come out of them with transposing reads.  Register-prefetched double buffer (next chunk's
-// global loads in flight during this chunk's MFMAs); 1-D grid, split-major so the workgroups on one XCD
-// share the same activation rows; partial tiles leave through an LDS-staged float4 epilogue.
+// the MFMA fragments come out of them with transposing reads.  Register prefetch (the next chunk's global
+// loads are in flight during this chunk's MFMAs) into ONE LDS buffer (two barriers per chunk), which keeps
+// three workgroups resident per CU; 1-D grid, split-major so the workgroups on one XCD share the same
+// activation rows; partial tiles leave through an LDS-staged float4 epilogue.
 template <int BM, int BN>
 struct WgCfg {
   static constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   static constexpr int ROW_A = BM + 4, ROW_B = BN + 4;  // bf16 per LDS row (8-B aligned tr reads)
   static constexpr int NA = BM / 32, NB = BN / 32;      // 16-B loads per thread per chunk
   static constexpr int A_EL = 64 * ROW_A, B_EL = 64 * ROW_B;
-  static constexpr int STAGE_BYTES = 2 * (A_EL + B_EL) * 2;
+  static constexpr int STAGE_BYTES = (A_EL + B_EL) * 2;  // one buffer (two barriers per chunk): 3 WGs / CU
   static constexpr int EP_LD = WN + 4;
-  static constexpr int EP_BYTES = 4 * WM * EP_LD * 4;
+  static constexpr int EP_BYTES = 4 * (WM / 2) * EP_LD * 4;  // epilogue staged in two halves
   static constexpr int SMEM = STAGE_BYTES > EP_BYTES ? STAGE_BYTES : EP_BYTES;
 };
 
@@ -442,7 +443,7 @@ __device__ __forceinline__ void st_split(__bf16* p, uint4 v) {  // 8-B aligned 1
 }
 
 template <int BM, int BN>
-__global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_wgrad_kernel(WgradArgs a, int TM, int TN, int splits) {
+__global__ __launch_bounds__(THREADS, 3) void conv1d_nlc_wgrad_kernel(WgradArgs a, int TM, int TN, int splits) {
   using Cfg = WgCfg<BM, BN>;
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NA = Cfg::NA, NB = Cfg::NB;
   constexpr int ROW_A = Cfg::ROW_A, ROW_B = Cfg::ROW_B;
@@ -508,13 +509,12 @@ __global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_wgrad_kernel(WgradArgs 
     __syncthreads();
     const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4, h = lane >> 4;
     for (int ch = ch0; ch < ch1; ++ch) {
-      const int cur = (ch - ch0) & 1;
       const int cn = ch + 1 < ch1 ? ch + 1 : ch;
 #pragma unroll
       for (int i = 0; i < NA; ++i) ra[i] = load_a(cn, tid + i * THREADS);
 #pragma unroll
       for (int i = 0; i < NB; ++i) rb[i] = load_b(cn, tid + i * THREADS);
-      const __bf16* As = lds + cur * (Cfg::A_EL + Cfg::B_EL);
+      const __bf16* As = lds;
       const __bf16* Bs = As + Cfg::A_EL;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {  // two 32-deep k-steps over r
@@ -543,29 +543,34 @@ __global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_wgrad_kernel(WgradArgs 
           for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
-      store_ab(lds + (cur ^ 1) * (Cfg::A_EL + Cfg::B_EL), ra, rb);
+      __syncthreads();  // every wave is done reading the buffer
+      store_ab(lds, ra, rb);
       __syncthreads();
     }
   }
   // epilogue: partial[split][co][n] through an LDS fp32 image, float4 row stores
-  constexpr int EP_LD = Cfg::EP_LD;
-  float* ep = reinterpret_cast<float*>(smem) + wv * WM * EP_LD;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq)
-        ep[(i * 16 + 4 * (lane >> 4) + qq) * EP_LD + j * 16 + (lane & 15)] = acc[i][j][qq];
-  __syncthreads();
+  constexpr int EP_LD = Cfg::EP_LD, HR = WM / 2;
+  float* ep = reinterpret_cast<float*>(smem) + wv * HR * EP_LD;
   constexpr int C4 = WN / 4, RSTEP = 64 / C4;
   const int c4 = lane % C4, rs = lane / C4;
   const long N = (long)a.Kw * a.Cin;
   float* out = a.part + (long)split * a.Cout * N;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();  // main loop / previous half done with the LDS
+#pragma unroll
+    for (int i = 0; i < FM / 2; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+          ep[(i * 16 + 4 * (lane >> 4) + qq) * EP_LD + j * 16 + (lane & 15)] = acc[h * (FM / 2) + i][j][qq];
+    __syncthreads();
 #pragma unroll 4
-  for (int r = rs; r < WM; r += RSTEP) {
-    const float4 v = *reinterpret_cast<const float4*>(ep + r * EP_LD + c4 * 4);
-    *reinterpret_cast<float4*>(out + (long)(co0 + wr * WM + r) * N + n0 + wc * WN + c4 * 4) = v;
+    for (int r = rs; r < HR; r += RSTEP) {
+      const float4 v = *reinterpret_cast<const float4*>(ep + r * EP_LD + c4 * 4);
+      *reinterpret_cast<float4*>(out + (long)(co0 + wr * WM + h * HR + r) * N + n0 + wc * WN + c4 * 4) = v;
+    }
   }
 }
 
