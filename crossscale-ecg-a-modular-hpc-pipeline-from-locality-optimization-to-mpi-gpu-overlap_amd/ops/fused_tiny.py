@@ -1,9 +1,17 @@
 """Fused TinyECG training / inference on gfx950 (Python side of csrc/kernels/tiny_ecg_step.hip).
 
-One HIP launch computes every sample's forward+backward out of LDS and writes per-sample parameter
-gradients into a slab; a second launch reduces the slab and applies SGD+momentum to the flat fp32
-master weights.  ``FusedTinyTrainer`` captures a whole FedAvg local round (``steps`` x 2 launches)
-into one native hipGraph and replays it with a single ``hipGraphLaunch``.
+Each workgroup computes one sample's forward+backward out of LDS.  ``FusedTinyTrainer`` runs a whole FedAvg
+local round as
+
+* ONE persistent launch (``persistent=True``; needs every workgroup of the batch resident at once): the step
+  loop runs inside the kernel, per-sample gradient rows and the updated parameters move between
+  workgroups as tagged write-through granules, every workgroup owns (reduces + SGD-updates) one column
+  slice of the flat parameters; or
+* two launches per step (gradient slab, then slab reduction + SGD; the default, fastest measured), or one
+  launch per step with an in-kernel reduction tree (``single_launch``),
+
+captured into one native hipGraph and replayed with a single ``hipGraphLaunch`` per round.  All three
+paths sum in a fixed order: the persistent round reproduces the two-launch path bit for bit.
 
 Reference semantics per step: Module_3/TRUE_FL_M3/part3_fedavg_overlap_mpi_gpu.py:103-132
 (train_step_G0/G1), batches as Module_3/shard_dataset.py:118-136, optimizer SGD(lr=1e-2, momentum=0.9).
@@ -114,7 +122,7 @@ class FusedTinyTrainer:
     def __init__(self, model: TinyECG, x_gpu: torch.Tensor, y_gpu: torch.Tensor, batch_size: int,
                  steps_per_round: int, lr: float = 1e-2, momentum: float = 0.9, weight_decay: float = 0.0,
                  nesterov: bool = False, seed: Optional[int] = None, use_graph: bool = True,
-                 single_launch: bool = False, precision: str = "bf16"):
+                 single_launch: bool = False, precision: str = "bf16", persistent: Optional[bool] = None):
         self.device = x_gpu.device
         self.precision = precision
         self.prec = prec_id(precision)
@@ -149,6 +157,17 @@ class FusedTinyTrainer:
         smem = lib.ecg_tiny_smem_bytes(self.x.shape[1], self.prec)
         if smem > 160 * 1024:
             raise ValueError(f"window length {self.x.shape[1]} too long for the fused kernel ({smem} B LDS)")
+        # persistent round: one launch per local round.  Opt-in: measured on MI355X at B=256 it runs 14.7 us/step
+        # against 13.7 for the two-launch graph - its two granule hand-offs per step cost more than the two kernel
+        # boundaries and the reduce launch they replace (profiles/r1_round_kernel/).
+        fits = bool(lib.ecg_tiny_round_fits(self.x.shape[1], self.nc, self.B, self.prec))
+        if persistent and not fits:
+            raise ValueError(f"persistent round needs all {self.B} workgroups resident at once (B <= #CUs)")
+        self.persistent = bool(persistent) and fits and not self.single_launch
+        self.status = torch.zeros(4, dtype=torch.int32, device=self.device)  # sticky give-up code
+        self.ws = None
+        if self.persistent:
+            self.ws = torch.empty(lib.ecg_tiny_round_ws_bytes(self.nc, self.B), dtype=torch.uint8, device=self.device)
 
     # ------------------------------------------------------------------ graph management
     def _graph_for(self, n: int) -> C.c_void_p:
@@ -158,11 +177,18 @@ class FusedTinyTrainer:
         g = C.c_void_p()
         lib = _lib.kernels()
         torch.cuda.synchronize(self.device)
-        st = lib.ecg_round_graph_create(C.byref(g), self.x.data_ptr(), self.x.shape[1], self.x.stride(0),
-                                        self.idx_table.data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
-                                        self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
-                                        n, self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd,
-                                        int(self.nesterov), *self._fuse_ptrs(), self.prec)
+        if self.persistent:
+            st = lib.ecg_round_graph_create_persistent(
+                C.byref(g), self.x.data_ptr(), self.x.shape[1], self.x.stride(0), self.idx_table.data_ptr(),
+                self.y32.data_ptr(), self.params.data_ptr(), self.mom.data_ptr(), self.nc, self.B, n,
+                self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd, int(self.nesterov), self.ws.data_ptr(),
+                self.ws.numel(), self.status.data_ptr(), self.prec)
+        else:
+            st = lib.ecg_round_graph_create(C.byref(g), self.x.data_ptr(), self.x.shape[1], self.x.stride(0),
+                                            self.idx_table.data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
+                                            self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
+                                            n, self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd,
+                                            int(self.nesterov), *self._fuse_ptrs(), self.prec)
         _lib.check(st, "ecg_round_graph_create")
         self._graphs[n] = g
         return g
@@ -192,6 +218,22 @@ class FusedTinyTrainer:
                                      *self._fuse_ptrs(), self.prec, _lib.stream_ptr(self.device))
         _lib.check(st, "ecg_tiny_train_step")
 
+    def _eager_round(self, n: int, stamps: Optional[torch.Tensor] = None):
+        """The persistent round as a direct launch (``stamps``: diagnostic phase clock of step 1)."""
+        lib = _lib.kernels()
+        st = lib.ecg_tiny_train_round(self.x.data_ptr(), self.x.shape[1], self.x.stride(0), self.idx_table.data_ptr(),
+                                      self.y32.data_ptr(), self.params.data_ptr(), self.mom.data_ptr(), self.nc,
+                                      self.B, n, self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd,
+                                      int(self.nesterov), self.ws.data_ptr(), self.ws.numel(), self.status.data_ptr(),
+                                      self.prec, _lib.ptr(stamps), _lib.stream_ptr(self.device))
+        _lib.check(st, "ecg_tiny_train_round")
+
+    def check_status(self) -> None:
+        """Raise if a persistent round gave up (a bounded spin timed out: workgroups not co-resident)."""
+        code = int(self.status[0].item())
+        if code:
+            raise _lib.NativeError(f"persistent TinyECG round gave up: {_lib.ROUND_GIVE_UP.get(code, code)}")
+
     def run_round(self, n_steps: Optional[int] = None, reset_loss: bool = True) -> None:
         """Enqueue ``n_steps`` (default ``steps_per_round``) local SGD steps on the current stream (async)."""
         n = self.S if n_steps is None else int(n_steps)
@@ -205,6 +247,8 @@ class FusedTinyTrainer:
             g = self._graph_for(n)
             _lib.check(_lib.kernels().ecg_round_graph_launch(g, _lib.stream_ptr(self.device)),
                        "ecg_round_graph_launch")
+        elif self.persistent:
+            self._eager_round(n)
         else:
             for s in range(n):
                 self._eager_step(s)
@@ -213,6 +257,7 @@ class FusedTinyTrainer:
 
     def avg_loss(self) -> float:
         """Mean per-step loss since the last reset (synchronises)."""
+        self.check_status()
         return float(self.loss_acc.item()) / (self.B * max(1, getattr(self, "_loss_steps", self.S)))
 
     def reset_momentum(self):

@@ -6,9 +6,12 @@
 //   Linear(16->C)  ->  softmax-CE  ->  head grads  ->  dconv2 wgrad (MFMA, dh2 kept in the MFMA
 //   accumulator layout and used directly as the A operand; h1 read as the B operand with the gfx950
 //   transposing LDS read ds_read_b64_tr_b16)  ->  dconv2 dgrad (MFMA)  ->  ReLU mask  ->  dconv1 wgrad.
-// It writes this sample's parameter-gradient contribution (1,458 floats for C=2) plus its loss into
-// one row of a partial slab; ``slab_reduce_sgd`` then sums the rows and applies SGD+momentum to the
-// flat fp32 master weights.  Two launches per step, graph-replayed for a whole FedAvg local round.
+// The sample's parameter gradient (1,458 floats for C=2) plus its loss form one row.  The rows of a step are
+// summed and SGD+momentum is applied to the flat fp32 master weights in one of three ways:
+//   * two launches per step: rows -> slab, then ``slab_reduce_sgd_kernel``; graph-replayed per local round;
+//   * one launch per step: an in-kernel last-arriver reduction tree (``FusedOpt``);
+//   * one launch per local ROUND (``tiny_ecg_round_kernel``, the default whenever the batch's workgroups fit
+//     on the device at once): see the comment above that kernel.
 //
 // Reference semantics being reproduced (per step): Module_3/TRUE_FL_M3/part3_fedavg_overlap_mpi_gpu.py:103-132
 // (train_step_G0/G1: fwd, cross_entropy(mean), backward, SGD(lr=1e-2, momentum=0.9).step()) on the
@@ -124,7 +127,8 @@ __device__ __forceinline__ s16x4 lds_tr16(const __bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
 }
 
-// MODE 0: full training step (grads -> slab row).  MODE 1: forward only (logits -> out [B, nc]).
+// ------------------------------------------------------------------------------------------------------------
+// The per-sample computation (phases 0-5), shared by the per-step kernel and the persistent round kernel.
 //
 // Backward algebra used (h2 = relu(conv2(h1)), pooled = mean_t h2, g[co] = dL/dpooled[co] / L):
 //   dh2[t][co]       = g[co] * m[t][co]          with m = relu'(h2) in {0, 1} (exact in bf16)
@@ -133,90 +137,86 @@ __device__ __forceinline__ s16x4 lds_tr16(const __bf16* p) {
 //   dh1[t][ci]       = sum_{co,k} m[t-k+2][co] * (g[co] w2[co][ci][k])   (g folded into the B operand)
 // so the M MFMAs of waves 1.. run concurrently with the head on wave 0, and every MFMA operand that
 // carries activation gradients is the exact 0/1 mask.
-template <int WAVES, int MODE, bool F32>
-__global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
-    const float* __restrict__ X, int L, long ldx,        // dataset windows [N, ldx], window length L
-    const int* __restrict__ idx,                         // [B] rows of X for this step (nullptr: b)
-    const int* __restrict__ Y,                           // [N] int32 labels (unused in MODE 1)
-    const float* __restrict__ params, int nc,            // flat fp32 params
-    float* __restrict__ out, int out_stride,             // MODE0: slab [B][out_stride]; MODE1: logits
-    float inv_B, unsigned long long* __restrict__ stamps,   // stamps: diagnostic phase clock (nullptr = off)
-    FusedOpt opt) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+template <int WAVES, bool F32>
+struct TinySample {
   using AT = std::conditional_t<F32, float, __bf16>;  // activation / MFMA operand type
-  const Smem sm = make_smem(L, WAVES, nc, F32);
-  const Layout lay = make_layout(nc);
-  const int Lp = sm.Lp;
-  const int NP = Lp / 32;  // tile pairs (32 time steps each)
+  static constexpr int NT = WAVES * 64;
+  Smem sm;
+  Layout lay;
+  int L, Lp, NP, nc;
+  int tid, lane, w, h, c;  // h: lane quarter, c: channel owned by this lane in C-layout phases
+  float* xs;               // [Lp + 16]: xs[i] = x[i - 3] (conv1 halo)
+  AT* h1s;                 // row (t+2): h1[t][ci]
+  AT* ms;                  // row (t+4): m[t][co] = relu'(h2) in {0,1}
+  float* ps;               // fp32 copy of the flat params
+  __bf16* fragF;           // [3][64][8] conv2 fwd B operand
+  __bf16* fragD;           // [3][64][8] conv2 dgrad B operand
+  float* fragF32;          // fp32 path: [20][64] fwd B operand
+  float* fragD32;          // fp32 path: [20][64] dgrad B operand
+  float* red;
+  uint32_t mask1 = 0u;     // relu'(h1) bits of this lane's conv1 outputs (phase 1 -> phase 4)
 
-  float* xs = reinterpret_cast<float*>(smem + sm.xs_off);
-  AT* h1s = reinterpret_cast<AT*>(smem + sm.h1_off);    // row (t+2): h1[t][ci]
-  AT* ms = reinterpret_cast<AT*>(smem + sm.dh2_off);    // row (t+4): m[t][co] = relu'(h2) in {0,1}
-  float* ps = reinterpret_cast<float*>(smem + sm.ps_off);       // fp32 copy of the flat params
-  __bf16* fragF = reinterpret_cast<__bf16*>(smem + sm.frag_off); // [3][64][8] conv2 fwd B operand
-  __bf16* fragD = fragF + 3 * 64 * 8;                            // [3][64][8] conv2 dgrad B operand
-  float* fragF32 = reinterpret_cast<float*>(smem + sm.frag_off);  // fp32 path: [20][64] fwd B operand
-  float* fragD32 = fragF32 + F32_KSTEPS * 64;                     // fp32 path: [20][64] dgrad B operand
-  float* red = reinterpret_cast<float*>(smem + sm.red_off);
+  __device__ __forceinline__ TinySample(unsigned char* smem, int L_, int nc_)
+      : sm(make_smem(L_, WAVES, nc_, F32)), lay(make_layout(nc_)), L(L_), nc(nc_) {
+    Lp = sm.Lp;
+    NP = Lp / 32;
+    xs = reinterpret_cast<float*>(smem + sm.xs_off);
+    h1s = reinterpret_cast<AT*>(smem + sm.h1_off);
+    ms = reinterpret_cast<AT*>(smem + sm.dh2_off);
+    ps = reinterpret_cast<float*>(smem + sm.ps_off);
+    fragF = reinterpret_cast<__bf16*>(smem + sm.frag_off);
+    fragD = fragF + 3 * 64 * 8;
+    fragF32 = reinterpret_cast<float*>(smem + sm.frag_off);
+    fragD32 = fragF32 + F32_KSTEPS * 64;
+    red = reinterpret_cast<float*>(smem + sm.red_off);
+    tid = threadIdx.x;
+    lane = tid & 63;
+    w = tid >> 6;
+    h = lane >> 4;
+    c = lane & 15;
+  }
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int w = tid >> 6;
-  const int h = lane >> 4;   // lane quarter
-  const int c = lane & 15;   // channel owned by this lane in C-layout phases
-  const int b = blockIdx.x;
-#define ECG_STAMP(k) \
-  if (stamps && tid == 0) stamps[(long)b * 16 + (k)] = __builtin_amdgcn_s_memtime();
-  if (stamps && tid == 0) stamps[(long)b * 16 + 15] = __builtin_amdgcn_s_memrealtime();
-  ECG_STAMP(0)
-
-  // ---------------- phase 0: stage params + x into LDS, zero halos ------------------------------
-  int ylab = 0;
-  {
-    const long row = idx ? (long)idx[b] : (long)b;
-    if (MODE == 0) ylab = Y[row];  // label prefetched with the window (used by the head)
-    const float* xrow = X + row * ldx;
-    for (int i = tid; i < Lp + 16; i += WAVES * 64) {
+  // ---- phase 0: window, parameters, constant pads
+  __device__ __forceinline__ void stage_x(const float* __restrict__ xrow) {
+    for (int i = tid; i < Lp + 16; i += NT) {
       const int t = i - 3;
       xs[i] = (t >= 0 && t < L) ? xrow[t] : 0.f;
     }
   }
-  {
-    // params: coalesced 16-B loads of the whole (tiny) parameter vector; every later weight access is LDS.
-    const int P4 = lay.P >> 2;
-    for (int i = tid; i < P4; i += WAVES * 64)
-      reinterpret_cast<float4*>(ps)[i] = reinterpret_cast<const float4*>(params)[i];
-    for (int i = (P4 << 2) + tid; i < lay.P; i += WAVES * 64) ps[i] = params[i];
-    // conv2 weights w2[co][ci][k] -> bf16 MFMA B fragments in lane order (read back with one
-    // ds_read_b128 per fragment).  fwd: B[r][co], r = 16k + ci; dgrad: B[r][ci], r = 16k + co;
-    // element (r, col) lives at frag[s = r>>5][lane = 16*((r&31)>>3) + col][j = r&7].
-    for (int e = tid; e < C * C * K2; e += WAVES * 64) {
+
+  // One flat parameter -> its fp32 LDS copy and, for conv2 weights w2[co][ci][k], the MFMA B fragments in
+  // lane order (read back with one ds_read_b128 per fragment).  bf16: fwd B[r][co], r = 16k + ci; dgrad
+  // B[r][ci], r = 16k + co; element (r, col) lives at frag[s = r>>5][lane = 16*((r&31)>>3) + col][j = r&7].
+  // fp32 (16x16x4): element (r, col) at frag[s = r>>2][lane = 16*(r&3) + col].
+  __device__ __forceinline__ void put_param(int i, float v) {
+    ps[i] = v;
+    const int e = i - lay.w2;
+    if (e >= 0 && e < C * C * K2) {
       const int co = e / (C * K2), ci = (e / K2) % C, k = e % K2;
       const int rf = 16 * k + ci, rd = 16 * k + co;
       if constexpr (F32) {
-        // 16x16x4 f32 operand: element (r, col) at frag[s = r>>2][lane = 16*(r&3) + col]
-        const float v = params[lay.w2 + e];
         fragF32[(rf >> 2) * 64 + 16 * (rf & 3) + co] = v;
         fragD32[(rd >> 2) * 64 + 16 * (rd & 3) + ci] = v;
       } else {
-        const __bf16 v = ecg::to_bf16(params[lay.w2 + e]);
-        fragF[((rf >> 5) * 64 + 16 * ((rf & 31) >> 3) + co) * 8 + (rf & 7)] = v;
-        fragD[((rd >> 5) * 64 + 16 * ((rd & 31) >> 3) + ci) * 8 + (rd & 7)] = v;
+        const __bf16 bv = ecg::to_bf16(v);
+        fragF[((rf >> 5) * 64 + 16 * ((rf & 31) >> 3) + co) * 8 + (rf & 7)] = bv;
+        fragD[((rd >> 5) * 64 + 16 * ((rd & 31) >> 3) + ci) * 8 + (rd & 7)] = bv;
       }
     }
-    // bf16: r in [80, 96) (the 6th, padding tap) is zero: s = 2, lane quarters 2 and 3
+  }
+
+  // bf16: r in [80, 96) (the 6th, padding tap) of both fragment sets is zero; h1 halo rows 0,1 (t=-2,-1) and
+  // [Lp+2, Lp+8), mask halo rows [0,4) and [Lp+4, Lp+8) are zero.  No phase writes them, so once per launch.
+  __device__ __forceinline__ void zero_pads() {
     if constexpr (!F32)
-      for (int e = tid; e < 2 * 32 * 8; e += WAVES * 64) {
+      for (int e = tid; e < 2 * 32 * 8; e += NT) {
         const int which = e >> 8, l = 32 + ((e >> 3) & 31), j = e & 7;
         (which ? fragD : fragF)[(2 * 64 + l) * 8 + j] = ecg::to_bf16(0.f);
       }
-  }
-  {
-    // h1 halo rows: index 0,1 (t=-2,-1) and [Lp+2, Lp+8) ; mask halo rows: [0,4) and [Lp+4, Lp+8)
     constexpr int DW = C * (int)sizeof(AT) / 4;  // dwords per activation row
     uint32_t* h1w = reinterpret_cast<uint32_t*>(h1s);
     uint32_t* mw = reinterpret_cast<uint32_t*>(ms);
-    for (int i = tid; i < 8 * DW; i += WAVES * 64) {  // 8 rows
+    for (int i = tid; i < 8 * DW; i += NT) {  // 8 rows
       const int r = i / DW, d = i % DW;
       const int hr = r < 2 ? r : Lp + 2 + (r - 2);
       h1w[hr * DW + d] = 0u;
@@ -224,12 +224,10 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
       mw[dr * DW + d] = 0u;
     }
   }
-  __syncthreads();
-  ECG_STAMP(1)
 
-  // ---------------- phase 1: conv1 + bias + ReLU (VALU) into h1s (bf16) ------------------------
-  uint32_t mask1 = 0u;
-  {
+  // ---- phase 1: conv1 + bias + ReLU (VALU) into h1s
+  __device__ __forceinline__ void conv1() {
+    mask1 = 0u;
     float w1r[K1];
 #pragma unroll
     for (int k = 0; k < K1; ++k) w1r[k] = ps[lay.w1 + c * K1 + k];
@@ -262,11 +260,9 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
       }
     }
   }
-  __syncthreads();
-  ECG_STAMP(2)
 
-  // ---------------- phase 2: conv2 (MFMA) + bias + ReLU -> pool partials, mask m -> LDS ---------
-  {
+  // ---- phase 2: conv2 (MFMA) + bias + ReLU -> pool partials, mask m -> LDS
+  __device__ __forceinline__ void conv2() {
     bf16x8 Bf[3];
     float Wf[F32_KSTEPS];
     if constexpr (F32) {
@@ -323,99 +319,98 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
       red[red_cnt(WAVES) + w * 16 + lane] = cnt;
     }
   }
-  __syncthreads();
-  ECG_STAMP(3)
 
-  // ---------------- phase 3: wave 0 = head;  waves 1.. = M (mask-weighted conv2 wgrad, MFMA) ------
-  if (w == 0) {
-    if (lane < 16) {
-      float pooled = 0.f;
+  // ---- phase 3: wave 0 = head (TRAIN: softmax-CE + head grads; else logits -> out[b]);
+  //               waves 1.. = M (mask-weighted conv2 wgrad, MFMA), training only
+  template <bool TRAIN>
+  __device__ __forceinline__ void head_and_M(int ylab, float inv_B, float* out, int out_stride, int b) {
+    if (w == 0) {
+      if (lane < 16) {
+        float pooled = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < WAVES; ++ww) pooled += red[RED_POOL + ww * 16 + lane];
-      red[RED_POOLED + lane] = pooled * (1.0f / (float)L);
-    }
-    // every lane picks up the 16 pooled channels (LDS broadcast reads; same-wave write -> read order)
-    float pv[C];
-#pragma unroll
-    for (int q4 = 0; q4 < C / 4; ++q4) {
-      const float4 v = reinterpret_cast<const float4*>(red + RED_POOLED)[q4];
-      pv[4 * q4] = v.x; pv[4 * q4 + 1] = v.y; pv[4 * q4 + 2] = v.z; pv[4 * q4 + 3] = v.w;
-    }
-    // lane n (< nc) of each 16-lane group computes logit n
-    const int n = c;
-    float logit = -INFINITY;
-    if (n < nc) {
-      logit = ps[lay.bh + n];
-#pragma unroll
-      for (int co = 0; co < C; ++co) logit = fmaf(ps[lay.wh + n * C + co], pv[co], logit);
-    }
-    if (MODE == 1) {
-      if (lane < nc) out[(long)b * out_stride + n] = logit;
-    } else {
-      float m = logit;
-#pragma unroll
-      for (int off = 8; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
-      const float e = (n < nc) ? __expf(logit - m) : 0.f;
-      float ssum = e;
-#pragma unroll
-      for (int off = 8; off >= 1; off >>= 1) ssum += __shfl_xor(ssum, off, 64);
-      const int y = ylab;
-      const float logit_y = __shfl(logit, (lane & 48) + y, 64);
-      const float loss = m + __logf(ssum) - logit_y;
-      const float dlogit = (n < nc) ? (e / ssum - (n == y ? 1.f : 0.f)) * inv_B : 0.f;
-      float* hg = red + red_head(WAVES);  // [wh, P] of this sample's row, stored with the rest in phase 5
-      if (lane < nc) {
-#pragma unroll
-        for (int co = 0; co < C; ++co) hg[n * C + co] = dlogit * pv[co];
-        hg[nc * C + n] = dlogit;
+        for (int ww = 0; ww < WAVES; ++ww) pooled += red[RED_POOL + ww * 16 + lane];
+        red[RED_POOLED + lane] = pooled * (1.0f / (float)L);
       }
-      if (lane == 0) hg[nc * C + nc] = loss;
-      // dpooled[co] = sum_n dlogit[n] * Wh[n][co]; lane co (< 16)
-      float dp = 0.f;
-      for (int nn = 0; nn < nc; ++nn) dp = fmaf(__shfl(dlogit, nn, 64), ps[lay.wh + nn * C + c], dp);
-      if (lane < 16) red[RED_G + c] = dp * (1.0f / (float)L);
-    }
-  } else if (MODE == 0 && w <= 5 * msplit(WAVES)) {
-    // work item (tap k, pair range part): M_k[co][ci] = sum_t m[t][co] * h1[t+k-2][ci]
-    constexpr int S = msplit(WAVES);
-    const int item = w - 1, k = item / S, part = item % S;
-    const int per = (NP + S - 1) / S;
-    const int p0 = part * per, p1 = p0 + per < NP ? p0 + per : NP;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (F32) {
-      // 16x16x4 f32: lane holds A[co = l&15][t = 4s + h] and B[t][ci = l&15]
-      for (int pair = p0; pair < p1; ++pair) {
+      // every lane picks up the 16 pooled channels (LDS broadcast reads; same-wave write -> read order)
+      float pv[C];
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const int t = 32 * pair + 4 * s + h;
-          const float a = ms[(t + 4) * C + (lane & 15)];
-          const float bb = h1s[(t + k - 2 + 2) * C + (lane & 15)];
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb, acc, 0, 0, 0);
+      for (int q4 = 0; q4 < C / 4; ++q4) {
+        const float4 v = reinterpret_cast<const float4*>(red + RED_POOLED)[q4];
+        pv[4 * q4] = v.x; pv[4 * q4 + 1] = v.y; pv[4 * q4 + 2] = v.z; pv[4 * q4 + 3] = v.w;
+      }
+      // lane n (< nc) of each 16-lane group computes logit n
+      const int n = c;
+      float logit = -INFINITY;
+      if (n < nc) {
+        logit = ps[lay.bh + n];
+#pragma unroll
+        for (int co = 0; co < C; ++co) logit = fmaf(ps[lay.wh + n * C + co], pv[co], logit);
+      }
+      if constexpr (!TRAIN) {
+        if (lane < nc) out[(long)b * out_stride + n] = logit;
+      } else {
+        float m = logit;
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+        const float e = (n < nc) ? __expf(logit - m) : 0.f;
+        float ssum = e;
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) ssum += __shfl_xor(ssum, off, 64);
+        const int y = ylab;
+        const float logit_y = __shfl(logit, (lane & 48) + y, 64);
+        const float loss = m + __logf(ssum) - logit_y;
+        const float dlogit = (n < nc) ? (e / ssum - (n == y ? 1.f : 0.f)) * inv_B : 0.f;
+        float* hg = red + red_head(WAVES);  // [wh, P] of this sample's row, stored with the rest in phase 5
+        if (lane < nc) {
+#pragma unroll
+          for (int co = 0; co < C; ++co) hg[n * C + co] = dlogit * pv[co];
+          hg[nc * C + n] = dlogit;
+        }
+        if (lane == 0) hg[nc * C + nc] = loss;
+        // dpooled[co] = sum_n dlogit[n] * Wh[n][co]; lane co (< 16)
+        float dp = 0.f;
+        for (int nn = 0; nn < nc; ++nn) dp = fmaf(__shfl(dlogit, nn, 64), ps[lay.wh + nn * C + c], dp);
+        if (lane < 16) red[RED_G + c] = dp * (1.0f / (float)L);
+      }
+    } else if (TRAIN && w <= 5 * msplit(WAVES)) {
+      // work item (tap k, pair range part): M_k[co][ci] = sum_t m[t][co] * h1[t+k-2][ci]
+      constexpr int S = msplit(WAVES);
+      const int item = w - 1, k = item / S, part = item % S;
+      const int per = (NP + S - 1) / S;
+      const int p0 = part * per, p1 = p0 + per < NP ? p0 + per : NP;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (F32) {
+        // 16x16x4 f32: lane holds A[co = l&15][t = 4s + h] and B[t][ci = l&15]
+        for (int pair = p0; pair < p1; ++pair) {
+#pragma unroll
+          for (int s = 0; s < 8; ++s) {
+            const int t = 32 * pair + 4 * s + h;
+            const float a = ms[(t + 4) * C + (lane & 15)];
+            const float bb = h1s[(t + k - 2 + 2) * C + (lane & 15)];
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb, acc, 0, 0, 0);
+          }
+        }
+      } else {
+        const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
+        for (int pair = p0; pair < p1; ++pair) {
+          const int ta = 32 * pair + 8 * h + q;  // time of row q of this lane-quarter's first 4x16 block
+          // A[co][t] (lane: co = l&15, t = 32*pair + 8h + j): transposing reads of the [t][co] mask image
+          const bf16x8 A = cat44(lds_tr16(ms + (ta + 4) * C + p4), lds_tr16(ms + (ta + 4 + 4) * C + p4));
+          // B[t][ci] = h1[t + k - 2][ci]
+          const bf16x8 Bm =
+              cat44(lds_tr16(h1s + (ta + k - 2 + 2) * C + p4), lds_tr16(h1s + (ta + k - 2 + 4 + 2) * C + p4));
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bm, acc, 0, 0, 0);
         }
       }
-    } else {
-      const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
-      for (int pair = p0; pair < p1; ++pair) {
-        const int ta = 32 * pair + 8 * h + q;  // time of row q of this lane-quarter's first 4x16 block
-        // A[co][t] (lane: co = l&15, t = 32*pair + 8h + j): transposing reads of the [t][co] mask image
-        const bf16x8 A = cat44(lds_tr16(ms + (ta + 4) * C + p4), lds_tr16(ms + (ta + 4 + 4) * C + p4));
-        // B[t][ci] = h1[t + k - 2][ci]
-        const bf16x8 Bm =
-            cat44(lds_tr16(h1s + (ta + k - 2 + 2) * C + p4), lds_tr16(h1s + (ta + k - 2 + 4 + 2) * C + p4));
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bm, acc, 0, 0, 0);
-      }
-    }
-    // acc[i] = M_k[co = 4h+i][ci = c]
-    float* pm = red + red_m(WAVES) + part * 1280;
+      // acc[i] = M_k[co = 4h+i][ci = c]
+      float* pm = red + red_m(WAVES) + part * 1280;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) pm[(4 * h + i) * (C * K2) + c * K2 + k] = acc[i];
+      for (int i = 0; i < 4; ++i) pm[(4 * h + i) * (C * K2) + c * K2 + k] = acc[i];
+    }
   }
-  if (MODE == 1) return;
-  __syncthreads();
-  ECG_STAMP(4)
 
-  // ---------------- phase 4: conv2 dgrad (MFMA, A = mask, B = g-scaled w2) * relu'(h1), conv1 wgrad
-  {
+  // ---- phase 4: conv2 dgrad (MFMA, A = mask, B = g-scaled w2) * relu'(h1), conv1 wgrad
+  __device__ __forceinline__ void dgrad() {
     // B[r][ci] = g[co] * w2[co][ci][k], r = 32s + 8h + j -> k = r>>4, co = r&15 = 8(h&1) + j
     float gq[8];
 #pragma unroll
@@ -488,13 +483,9 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
       if (lane < 16) red[red_dw1(WAVES) + w * 128 + c * 8 + k] = v;
     }
   }
-  __syncthreads();
-  ECG_STAMP(5)
 
-  // ---------------- phase 5: combine partials, scale by g, write this sample's gradient row -----
-  const __amdgpu_buffer_rsrc_t slab_r = make_rsrc(out, (long)gridDim.x * out_stride * 4);
-  const int rowbase = b * out_stride;
-  for (int i = tid; i <= lay.P; i += WAVES * 64) {
+  // ---- phase 5: element i (0..P; P = loss) of this sample's gradient row, from the phase partials
+  __device__ __forceinline__ float row_value(int i) const {
     float v = 0.f;
     if (i >= lay.wh) {
       v = red[red_head(WAVES) + (i - lay.wh)];
@@ -517,13 +508,71 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
       for (int ww = 0; ww < WAVES; ++ww) v += red[red_cnt(WAVES) + ww * 16 + co];
       v *= red[RED_G + co];
     }
-    st_wt(slab_r, rowbase + i, v);
+    return v;
   }
-  ECG_STAMP(6)
+};
+
+// MODE 0: full training step (grads -> slab row).  MODE 1: forward only (logits -> out [B, nc]).
+// MODE 2: diagnostic - every workgroup computes its training step twice; the second pass runs with warm
+//         instruction / scalar / data caches (phase stamps of both passes: scripts/diag_step_phases.py).
+template <int WAVES, int MODE, bool F32>
+__global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
+    const float* __restrict__ X, int L, long ldx,        // dataset windows [N, ldx], window length L
+    const int* __restrict__ idx,                         // [B] rows of X for this step (nullptr: b)
+    const int* __restrict__ Y,                           // [N] int32 labels (unused in MODE 1)
+    const float* __restrict__ params, int nc,            // flat fp32 params
+    float* __restrict__ out, int out_stride,             // MODE0/2: slab [B][out_stride]; MODE1: logits
+    float inv_B, unsigned long long* __restrict__ stamps,   // stamps: diagnostic phase clock (nullptr = off)
+    FusedOpt opt) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  TinySample<WAVES, F32> S(smem, L, nc);
+  constexpr bool TRAIN = MODE != 1;
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x;
+  const __amdgpu_buffer_rsrc_t slab_r = make_rsrc(out, (long)gridDim.x * out_stride * 4);
+  const int rowbase = b * out_stride;
+  if (stamps && tid == 0) stamps[(long)b * 16 + 15] = __builtin_amdgcn_s_memrealtime();
+#pragma unroll 1
+  for (int rep = 0; rep < (MODE == 2 ? 2 : 1); ++rep) {
+#define ECG_STAMP(k) \
+  if (stamps && tid == 0) stamps[(long)b * 16 + 7 * rep + (k)] = __builtin_amdgcn_s_memtime();
+    ECG_STAMP(0)
+    // phase 0: stage params + x into LDS, zero pads
+    int ylab = 0;
+    {
+      const long row = idx ? (long)idx[b] : (long)b;
+      if (TRAIN) ylab = Y[row];  // label prefetched with the window (used by the head)
+      S.stage_x(X + row * ldx);
+    }
+    for (int i = tid; i < S.lay.P; i += S.NT) S.put_param(i, params[i]);
+    S.zero_pads();
+    __syncthreads();
+    ECG_STAMP(1)
+    S.conv1();
+    __syncthreads();
+    ECG_STAMP(2)
+    S.conv2();
+    __syncthreads();
+    ECG_STAMP(3)
+    S.template head_and_M<TRAIN>(ylab, inv_B, out, out_stride, b);
+    if (!TRAIN) return;
+    __syncthreads();
+    ECG_STAMP(4)
+    S.dgrad();
+    __syncthreads();
+    ECG_STAMP(5)
+    // phase 5: combine partials, scale by g, write this sample's gradient row (write-through: the
+    // single-launch reduction below reads it inside this launch)
+    for (int i = tid; i <= S.lay.P; i += S.NT) st_wt(slab_r, rowbase + i, S.row_value(i));
+    ECG_STAMP(6)
+#undef ECG_STAMP
+    if (MODE == 2) __syncthreads();  // the second pass reuses the LDS
+  }
   if (stamps && tid == 0) stamps[(long)b * 16 + 14] = __builtin_amdgcn_s_memrealtime();
-  if (opt.ctl != nullptr) {
+  if (MODE == 0 && opt.ctl != nullptr) {
     // ---------------- phase 6: two-level deterministic cross-sample reduction + SGD --------------
-    int* flag = reinterpret_cast<int*>(red + RED_FLAG);
+    const Layout& lay = S.lay;
+    int* flag = reinterpret_cast<int*>(S.red + RED_FLAG);
     const int G = opt.G;
     const int NG = G < kMaxGroups ? G : kMaxGroups;
     const int g = b % NG;
@@ -618,10 +667,11 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
       }
     }
     if (tid <= kMaxGroups) __hip_atomic_store(&opt.ctl[tid], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ECG_STAMP(7)
-    if (stamps && tid == 0) stamps[(long)b * 16 + 13] = __builtin_amdgcn_s_memrealtime();
+    if (stamps && tid == 0) {
+      stamps[(long)b * 16 + 7] = __builtin_amdgcn_s_memtime();
+      stamps[(long)b * 16 + 13] = __builtin_amdgcn_s_memrealtime();
+    }
   }
-#undef ECG_STAMP
 }
 
 // Sum the per-sample gradient rows and apply SGD (+momentum, weight decay, nesterov) in place.
@@ -675,6 +725,244 @@ __global__ __launch_bounds__(RED_COLS * RED_ROWG) void slab_reduce_sgd_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// Persistent round: ONE launch runs ``steps`` training steps of one FedAvg client, B workgroups (one per
+// sample of a step) that are all resident at once (the host takes this path only when B <= #CUs).
+//   * A step's code runs with warm instruction / scalar caches: a fresh launch pays the cold fetch of the
+//     whole step body again in every phase (scripts/diag_step_phases.py: cold vs warm passes).
+//   * Per step, workgroup b publishes its gradient row as {tag = step + 1, value} 8-byte granules (MI355X
+//     guide, Guideline 16 R2: the data is the flag; two granules per 16-byte write-through store).  It then
+//     OWNS the column slice [b*cw, b*cw + cw): it sweeps those granules of all B rows until every tag
+//     matches, sums each column in exactly the order of slab_reduce_sgd_kernel (so parameters, momentum and
+//     loss are bitwise those of the two-launch path), applies SGD to its slice (the authoritative parameter
+//     and momentum values of the slice stay in its LDS for the whole round) and publishes the new parameters
+//     as granules.  Every workgroup sweeps the parameter granules before its next step.  No counters, no
+//     fences, no grid barrier: two one-hop hand-offs per step.
+//   * The next step's window and label are loaded into registers before the exchange and land under it.
+//   * Every spin is bounded: after kSpinTicks the workgroup records a give-up code in ``status`` (sticky,
+//     read by the host) and leaves; its peers then time out too, so the launch always drains.
+//   * Tags are zeroed by a memset of the granule workspace before every launch (a memset node in the
+//     captured round graph); the slice owners write params / momentum / loss back when the round ends.
+typedef unsigned long long u64;
+typedef __attribute__((address_space(1))) u64 gu64;
+typedef __attribute__((address_space(1))) int gi32;
+
+constexpr unsigned long long kSpinTicks = 50000000ull;  // 0.5 s of s_memrealtime (100 MHz); a round takes ~1 ms
+constexpr int kGiveUpParams = 1, kGiveUpRows = 2;
+
+struct RoundArgs {
+  const float* X;
+  long ldx;
+  const int* idx_table;  // [steps][G] dataset rows of every step
+  const int* Y;          // [N] int32 labels
+  float* params;         // flat fp32 master weights: read at entry, each slice written back by its owner
+  float* mom;            // momentum (nullptr when momentum == 0)
+  float* loss_acc;       // += sum over the round's samples of the loss
+  u64* rowg;             // [G][gstride] gradient-row granules
+  u64* parg;             // [gstride] parameter granules
+  int* status;           // [0]: sticky give-up code (0 = ok)
+  unsigned long long* stamps;  // diagnostic: phase clock of step 1 (warm), [G][16]; nullptr = off
+  int L, nc, G, steps, gstride;
+  float inv_B, lr, momentum, wd;
+  int nesterov;
+};
+
+__host__ __device__ inline int round_gstride(int nc) { return (make_layout(nc).P + 1 + 15) / 16 * 16; }
+__host__ __device__ inline int round_cols(int nc, int G) { return (make_layout(nc).P + 1 + G - 1) / G; }
+// extra LDS of the round kernel: vals [cw][G], part [cw][16], own params [cw], own momentum [cw], give-up flag
+__host__ __device__ inline int round_ext_bytes(int nc, int G) {
+  const int cw = round_cols(nc, G);
+  return ((G * cw + cw * 16 + 2 * cw + 4) * 4 + 15) / 16 * 16;
+}
+inline long round_ws_bytes(int nc, int G) { return ((long)G + 1) * round_gstride(nc) * 8; }
+
+__device__ __forceinline__ u64 get_granule(const u64* g) {
+  return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void put_granule(u64* g, unsigned tag, float v) {
+  __hip_atomic_store((gu64*)g, ((u64)tag << 32) | __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Sweep granules at(e), e = tid + k*NT (clamped to n-1, so no branch around a load), until every tag equals
+// ``tag``; the values land in v[k].  Wave-uniform result; false when the spin ran out of time.
+template <int NT, int KMAX, typename At>
+__device__ __forceinline__ bool sweep(At at, int n, unsigned tag, float (&v)[KMAX], unsigned long long t0) {
+  const int tid = threadIdx.x;
+  for (int spins = 0;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const u64 x = get_granule(at(min(tid + k * NT, n - 1)));
+      v[k] = __builtin_bit_cast(float, (unsigned)x);
+      ok = ok && (unsigned)(x >> 32) == tag;
+    }
+    if (__all(ok)) return true;
+    if ((spins & 31) == 31 && __builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+template <int WAVES, bool F32>
+__global__ __launch_bounds__(WAVES * 64) void tiny_ecg_round_kernel(RoundArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  using TS = TinySample<WAVES, F32>;
+  constexpr int NT = TS::NT;
+  constexpr int KMAX = (2048 + NT - 1) / NT;                                 // granules per thread per sweep
+  constexpr int XR = (32 * MAX_PAIRS_PER_WAVE * WAVES + 16 + NT - 1) / NT;   // window floats per thread
+  TS S(smem, a.L, a.nc);
+  const int tid = threadIdx.x, b = blockIdx.x, G = a.G;
+  const int P = S.lay.P, ncols = P + 1;
+  const int cw0 = round_cols(a.nc, G);
+  const int col0 = min(ncols, b * cw0), cw = min(ncols, col0 + cw0) - col0;  // owned columns (may be 0)
+  float* vals = reinterpret_cast<float*>(smem + S.sm.bytes);  // [cw0][G] owned columns of every row
+  float* part = vals + G * cw0;                                // [cw0][16] ordered partial sums
+  float* ownp = part + cw0 * 16;                               // [cw0] owned parameters (loss sum for col P)
+  float* ownm = ownp + cw0;                                    // [cw0] owned momentum
+  int* gflag = reinterpret_cast<int*>(ownm + cw0);             // [0]: give-up code of this workgroup
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const __amdgpu_buffer_rsrc_t row_r = make_rsrc(a.rowg, (long)G * a.gstride * 8);
+
+  S.zero_pads();
+  for (int i = tid; i < cw; i += NT) {
+    const int col = col0 + i;
+    ownp[i] = col < P ? a.params[col] : a.loss_acc[0];
+    ownm[i] = (col < P && a.mom) ? a.mom[col] : 0.f;
+  }
+  if (tid == 0) gflag[0] = 0;
+
+  float xr[XR];
+  int ynext = 0;
+  auto prefetch = [&](int s) {  // window + label of step s into registers (clamped loads, no branches)
+    const long row = a.idx_table[(long)s * G + b];
+    ynext = a.Y[row];
+    const float* xrow = a.X + row * a.ldx;
+#pragma unroll
+    for (int k = 0; k < XR; ++k) {
+      const int i = tid + k * NT, t = i - 3;
+      const float v = xrow[min(max(t, 0), S.L - 1)];
+      xr[k] = (i < S.Lp + 16 && t >= 0 && t < S.L) ? v : 0.f;
+    }
+  };
+  auto give_up = [&]() -> bool {  // block-uniform after a barrier
+    if (gflag[0] == 0) return false;
+    if (tid == 0) __hip_atomic_store((gi32*)a.status, gflag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  };
+  prefetch(0);
+  for (int s = 0; s < a.steps; ++s) {
+    const bool stamp = a.stamps != nullptr && s == 1 && tid == 0;
+#define ECG_RSTAMP(k) \
+  if (stamp) a.stamps[(long)b * 16 + (k)] = __builtin_amdgcn_s_memtime();
+    ECG_RSTAMP(0)
+    // ---- parameters of this step: the launch's input (step 0) or the granules the slice owners published
+    if (s == 0) {
+      for (int i = tid; i < P; i += NT) S.put_param(i, a.params[i]);
+    } else {
+      float v[KMAX];
+      if (!sweep<NT, KMAX>([&](int e) { return a.parg + e; }, P, (unsigned)s, v, t0)) gflag[0] = kGiveUpParams;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        const int i = tid + k * NT;
+        if (i < P) S.put_param(i, v[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < XR; ++k) {
+      const int i = tid + k * NT;
+      if (i < S.Lp + 16) S.xs[i] = xr[k];
+    }
+    const int ylab = ynext;
+    __syncthreads();
+    if (give_up()) return;
+    ECG_RSTAMP(1)
+    S.conv1();
+    __syncthreads();
+    ECG_RSTAMP(2)
+    S.conv2();
+    __syncthreads();
+    ECG_RSTAMP(3)
+    S.template head_and_M<true>(ylab, a.inv_B, nullptr, 0, b);
+    __syncthreads();
+    ECG_RSTAMP(4)
+    S.dgrad();
+    if (s + 1 < a.steps) prefetch(s + 1);  // lands under the exchange below
+    __syncthreads();
+    ECG_RSTAMP(5)
+    // ---- publish this sample's gradient row: granules {s+1, value}, two per 16-byte write-through store
+    for (int p = tid; 2 * p < ncols; p += NT) {
+      const int i = 2 * p;
+      const float v0 = S.row_value(i), v1 = i + 1 < ncols ? S.row_value(i + 1) : 0.f;
+      typedef int i32x4 __attribute__((ext_vector_type(4)));
+      const i32x4 q = {__builtin_bit_cast(int, v0), s + 1, __builtin_bit_cast(int, v1), s + 1};
+      __builtin_amdgcn_raw_buffer_store_b128(q, row_r, (b * a.gstride + i) * 8, 0, 16);
+    }
+    // ---- gather the owned columns of every row
+    const int n = G * cw;
+    if (n > 0) {  // block-uniform
+      float v[KMAX];
+      auto at = [&](int e) { return a.rowg + (long)(e / cw) * a.gstride + col0 + e % cw; };
+      if (!sweep<NT, KMAX>(at, n, (unsigned)(s + 1), v, t0)) gflag[0] = kGiveUpRows;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        const int e = tid + k * NT;
+        if (e < n) vals[(e % cw) * G + e / cw] = v[k];
+      }
+    }
+    __syncthreads();
+    if (give_up()) return;
+    ECG_RSTAMP(6)
+    // ---- column sums in slab_reduce_sgd_kernel's order: 16 row groups (rows rg, rg+16, ... in chunks of 16,
+    // pairwise), then the 16 group sums in order
+    for (int q = tid; q < cw * 16; q += NT) {
+      const int cl = q >> 4, rg = q & 15;
+      const float* colv = vals + cl * G;
+      float acc = 0.f;
+      int r = rg;
+      for (; r + 16 * 15 < G; r += 16 * 16) {
+#pragma unroll
+        for (int j = 0; j < 16; j += 2) acc += colv[r + 16 * j] + colv[r + 16 * (j + 1)];
+      }
+      for (; r < G; r += 16) acc += colv[r];
+      part[q] = acc;
+    }
+    __syncthreads();
+    // ---- SGD on the owned slice, publish the new parameters for the next step
+    for (int cl = tid; cl < cw; cl += NT) {
+      float gsum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) gsum += part[cl * 16 + j];
+      const int col = col0 + cl;
+      if (col == P) {
+        ownp[cl] += gsum;  // the round's loss sum (loss_acc)
+      } else {
+        const float p = ownp[cl];
+        float d = gsum + a.wd * p;
+        if (a.momentum != 0.f) {
+          const float bm = a.momentum * ownm[cl] + d;
+          ownm[cl] = bm;
+          d = a.nesterov ? d + a.momentum * bm : bm;
+        }
+        const float pn = p - a.lr * d;
+        ownp[cl] = pn;
+        if (s + 1 < a.steps) put_granule(a.parg + col, (unsigned)(s + 1), pn);
+      }
+    }
+    ECG_RSTAMP(7)
+#undef ECG_RSTAMP
+  }
+  // ---- the round's result: each owner writes back its slice (same thread that updated it)
+  for (int cl = tid; cl < cw; cl += NT) {
+    const int col = col0 + cl;
+    if (col < P) {
+      a.params[col] = ownp[cl];
+      if (a.mom) a.mom[col] = ownm[cl];
+    } else {
+      a.loss_acc[0] = ownp[cl];
+    }
+  }
+}
+
 unsigned long long* g_stamps = nullptr;  // diagnostic phase stamps (ecg_tiny_set_stamps)
 
 template <int WAVES, int MODE, bool F32>
@@ -714,7 +1002,7 @@ int check_step_args(int L, int nc, int B, int out_stride, int mode, bool f32 = f
   const int Lp = (L + 31) / 32 * 32;
   if (Lp > 32 * 4 * 8 || make_smem(L, 8, MAX_CLASSES, f32).bytes > kMaxLds) return ecg::kTooLarge;  // op-by-op path
   const Layout lay = make_layout(nc);
-  if (mode == 0 && out_stride < lay.P + 1) return ecg::kBadArg;
+  if (mode != 1 && out_stride < lay.P + 1) return ecg::kBadArg;
   if (mode == 1 && out_stride < nc) return ecg::kBadArg;
   return ecg::kOk;
 }
@@ -723,6 +1011,8 @@ template <bool F32>
 int dispatch_prec(int mode, const float* X, int L, long ldx, const int* idx, const int* Y, const float* params,
                   int nc, float* out, int out_stride, int B, float inv_B, const FusedOpt& opt, hipStream_t stream) {
   const int waves = pick_waves(L, F32);
+  if (mode == 2)  // diagnostic (one wave count is enough)
+    return launch_step<8, 2, F32>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream);
   if (mode == 0)
     return waves == 8
                ? launch_step<8, 0, F32>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream)
@@ -760,6 +1050,86 @@ int reduce_dispatch(const float* slab, int G, int stride, int P, float* params, 
   return ecg::kOk;
 }
 
+// ---- persistent round: residency check and launch
+template <int WAVES, bool F32>
+int round_smem(int L, int nc, int G) {
+  return make_smem(L, WAVES, nc, F32).bytes + round_ext_bytes(nc, G);
+}
+
+template <int WAVES, bool F32>
+bool round_fits_cfg(int L, int nc, int G) {
+  const int smem = round_smem<WAVES, F32>(L, nc, G);
+  if (smem > kMaxLds) return false;
+  auto kern = tiny_ecg_round_kernel<WAVES, F32>;
+  if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)
+    return false;
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, WAVES * 64, smem) != hipSuccess)
+    return false;
+  // The protocol needs every workgroup resident at once.  The occupancy answer can be one block per CU too
+  // high (MI355X guide, residency), so only grids of at most one workgroup per CU take this path.
+  return per_cu >= 1 && G <= cus;
+}
+
+bool round_fits(int L, int nc, int G, bool f32) {
+  if (check_step_args(L, nc, G, make_layout(nc).P + 1, 0, f32) != ecg::kOk) return false;
+  const int waves = pick_waves(L, f32);
+  if (f32) return waves == 8 ? round_fits_cfg<8, true>(L, nc, G) : round_fits_cfg<16, true>(L, nc, G);
+  return waves == 8 ? round_fits_cfg<8, false>(L, nc, G) : round_fits_cfg<16, false>(L, nc, G);
+}
+
+template <int WAVES, bool F32>
+int launch_round_cfg(const RoundArgs& a, hipStream_t stream) {
+  const int smem = round_smem<WAVES, F32>(a.L, a.nc, a.G);
+  auto kern = tiny_ecg_round_kernel<WAVES, F32>;
+  ECG_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
+  hipLaunchKernelGGL(kern, dim3(a.G), dim3(WAVES * 64), smem, stream, a);
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
+}
+
+// memset of the granule tags + the round kernel (both captured when called under stream capture)
+int round_dispatch(const RoundArgs& a, void* ws, long ws_bytes, int prec, hipStream_t stream) {
+  if (prec != 0 && prec != 1) return ecg::kBadArg;
+  if (!ws || !a.status || !a.loss_acc || !a.params || (a.momentum != 0.f && !a.mom) || a.steps <= 0)
+    return ecg::kBadArg;
+  if (ws_bytes < round_ws_bytes(a.nc, a.G) || !round_fits(a.L, a.nc, a.G, prec == 1)) return ecg::kBadArg;
+  ECG_HIP_CHECK(hipMemsetAsync(ws, 0, round_ws_bytes(a.nc, a.G), stream));
+  const int waves = pick_waves(a.L, prec == 1);
+  if (prec == 1) return waves == 8 ? launch_round_cfg<8, true>(a, stream) : launch_round_cfg<16, true>(a, stream);
+  return waves == 8 ? launch_round_cfg<8, false>(a, stream) : launch_round_cfg<16, false>(a, stream);
+}
+
+RoundArgs make_round_args(const float* X, int L, long ldx, const int* idx_table, const int* Y, float* params,
+                          float* mom, int nc, int B, int steps, float* loss_acc, float lr, float momentum, float wd,
+                          int nesterov, void* ws, int* status, unsigned long long* stamps) {
+  RoundArgs a{};
+  a.X = X;
+  a.ldx = ldx;
+  a.idx_table = idx_table;
+  a.Y = Y;
+  a.params = params;
+  a.mom = mom;
+  a.loss_acc = loss_acc;
+  a.gstride = round_gstride(nc);
+  a.rowg = static_cast<u64*>(ws);
+  a.parg = a.rowg + (long)B * a.gstride;
+  a.status = status;
+  a.stamps = stamps;
+  a.L = L;
+  a.nc = nc;
+  a.G = B;
+  a.steps = steps;
+  a.inv_B = 1.0f / (float)B;
+  a.lr = lr;
+  a.momentum = momentum;
+  a.wd = wd;
+  a.nesterov = nesterov;
+  return a;
+}
+
 struct RoundGraph {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
@@ -772,7 +1142,8 @@ struct RoundGraph {
 ECG_API int ecg_tiny_param_count(int nc) { return make_layout(nc).P; }
 
 // Diagnostic: when set, every fused-step workgroup b writes s_memtime at each phase boundary to
-// stamps[b*16 + k] (k = 0..8) and s_memrealtime at entry/exit to [b*16+15] / [b*16+14].
+// stamps[b*16 + k] (k = 0..6; MODE 2's second pass: 7..13; single-launch final reducer: 7) and
+// s_memrealtime at entry/exit to [b*16+15] / [b*16+14].
 ECG_API int ecg_tiny_set_stamps(unsigned long long* stamps) {
   g_stamps = stamps;
   return ecg::kOk;
@@ -787,6 +1158,13 @@ ECG_API int ecg_tiny_step_grads(const float* X, int L, long ldx, const int* idx,
                                 const float* params, int nc, float* slab, int slab_stride, int B, float inv_B,
                                 int prec, hipStream_t stream) {
   return step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, inv_B, no_fuse(), stream);
+}
+
+// Diagnostic twin of ecg_tiny_step_grads: every workgroup computes its sample twice (cold, then warm caches).
+ECG_API int ecg_tiny_step_grads_twice(const float* X, int L, long ldx, const int* idx, const int* Y,
+                                      const float* params, int nc, float* slab, int slab_stride, int B, float inv_B,
+                                      int prec, hipStream_t stream) {
+  return step_dispatch(2, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, inv_B, no_fuse(), stream);
 }
 
 // Inference: logits[B][nc] for windows X[idx[b]].
@@ -825,15 +1203,28 @@ ECG_API int ecg_tiny_train_step(const float* X, int L, long ldx, const int* idx,
                          nesterov, 1, stream);
 }
 
-// Capture ``steps`` consecutive fused steps (batch s reads idx_table + s*B) into one hipGraph.
-// All pointers are baked into the graph: callers keep the buffers alive and refill idx_table in place.
-ECG_API int ecg_round_graph_create(void** handle, const float* X, int L, long ldx, const int* idx_table,
-                                   const int* Y, float* params, float* mom, int nc, float* slab, int slab_stride,
-                                   int B, int steps, float* loss_acc, float lr, float momentum, float wd,
-                                   int nesterov, int* ctl, float* gslab, int prec) {
-  if (!handle || steps <= 0) return ecg::kBadArg;
-  int st = check_step_args(L, nc, B, slab_stride, 0, prec == 1);
-  if (st) return st;
+// ---- persistent round (tiny_ecg_round_kernel)
+// Bytes of the granule workspace (tags zeroed by the launcher before every launch).
+ECG_API long ecg_tiny_round_ws_bytes(int nc, int B) { return round_ws_bytes(nc, B); }
+
+// 1 when a round of batch B can run as one persistent launch on the current device (every workgroup resident).
+ECG_API int ecg_tiny_round_fits(int L, int nc, int B, int prec) { return round_fits(L, nc, B, prec == 1) ? 1 : 0; }
+
+// ``steps`` training steps (batch s reads idx_table + s*B) as ONE launch (+ the workspace memset).  ``status``
+// (int32, zero-initialised by the caller) receives a sticky non-zero code if a bounded spin gave up.
+ECG_API int ecg_tiny_train_round(const float* X, int L, long ldx, const int* idx_table, const int* Y, float* params,
+                                 float* mom, int nc, int B, int steps, float* loss_acc, float lr, float momentum,
+                                 float wd, int nesterov, void* ws, long ws_bytes, int* status, int prec,
+                                 unsigned long long* stamps, hipStream_t stream) {
+  const RoundArgs a = make_round_args(X, L, ldx, idx_table, Y, params, mom, nc, B, steps, loss_acc, lr, momentum, wd,
+                                      nesterov, ws, status, stamps);
+  return round_dispatch(a, ws, ws_bytes, prec, stream);
+}
+
+static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws, long ws_bytes, int prec,
+                         const float* X, int L, long ldx, const int* idx_table, const int* Y, float* params,
+                         float* mom, int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr,
+                         float momentum, float wd, int nesterov, int* ctl, float* gslab) {
   hipStream_t cap;
   ECG_HIP_CHECK(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
   RoundGraph* rg = new RoundGraph();
@@ -844,9 +1235,14 @@ ECG_API int ecg_round_graph_create(void** handle, const float* X, int L, long ld
     (void)hipStreamDestroy(cap);
     return ecg::kHipError;
   }
-  for (int s = 0; s < steps && st == 0; ++s)
-    st = ecg_tiny_train_step(X, L, ldx, idx_table + (long)s * B, Y, params, mom, nc, slab, slab_stride, B, loss_acc,
-                             lr, momentum, wd, nesterov, ctl, gslab, prec, cap);
+  int st = 0;
+  if (pa) {
+    st = round_dispatch(*pa, ws, ws_bytes, prec, cap);
+  } else {
+    for (int s = 0; s < steps && st == 0; ++s)
+      st = ecg_tiny_train_step(X, L, ldx, idx_table + (long)s * B, Y, params, mom, nc, slab, slab_stride, B,
+                               loss_acc, lr, momentum, wd, nesterov, ctl, gslab, prec, cap);
+  }
   e = hipStreamEndCapture(cap, &rg->graph);
   (void)hipStreamDestroy(cap);
   if (st != 0 || e != hipSuccess) {
@@ -862,6 +1258,31 @@ ECG_API int ecg_round_graph_create(void** handle, const float* X, int L, long ld
   }
   *handle = rg;
   return ecg::kOk;
+}
+
+// Capture ``steps`` consecutive fused steps (batch s reads idx_table + s*B) into one hipGraph.
+// All pointers are baked into the graph: callers keep the buffers alive and refill idx_table in place.
+ECG_API int ecg_round_graph_create(void** handle, const float* X, int L, long ldx, const int* idx_table,
+                                   const int* Y, float* params, float* mom, int nc, float* slab, int slab_stride,
+                                   int B, int steps, float* loss_acc, float lr, float momentum, float wd,
+                                   int nesterov, int* ctl, float* gslab, int prec) {
+  if (!handle || steps <= 0) return ecg::kBadArg;
+  int st = check_step_args(L, nc, B, slab_stride, 0, prec == 1);
+  if (st) return st;
+  return capture_round(handle, steps, nullptr, nullptr, 0, prec, X, L, ldx, idx_table, Y, params, mom, nc, slab,
+                       slab_stride, B, loss_acc, lr, momentum, wd, nesterov, ctl, gslab);
+}
+
+// The persistent round (workspace memset + one launch) captured as a hipGraph, replayed once per round.
+ECG_API int ecg_round_graph_create_persistent(void** handle, const float* X, int L, long ldx, const int* idx_table,
+                                              const int* Y, float* params, float* mom, int nc, int B, int steps,
+                                              float* loss_acc, float lr, float momentum, float wd, int nesterov,
+                                              void* ws, long ws_bytes, int* status, int prec) {
+  if (!handle || steps <= 0) return ecg::kBadArg;
+  const RoundArgs a = make_round_args(X, L, ldx, idx_table, Y, params, mom, nc, B, steps, loss_acc, lr, momentum, wd,
+                                      nesterov, ws, status, nullptr);
+  return capture_round(handle, steps, &a, ws, ws_bytes, prec, X, L, ldx, idx_table, Y, params, mom, nc, nullptr, 0,
+                       B, loss_acc, lr, momentum, wd, nesterov, nullptr, nullptr);
 }
 
 ECG_API int ecg_round_graph_launch(void* handle, hipStream_t stream) {

@@ -1,12 +1,15 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-phase cycle breakdown of the fused TinyECG step (s_memtime stamps, wave 0 of each WG).
+"""Diagnostic: where the fused TinyECG step spends its cycles (s_memtime stamps, wave 0 of each WG).
 
 Phases: 0 stage x/params | 1 conv1 | 2 conv2 fwd + mask | 3 head || mask-weighted wgrad | 4 dgrad2 + wgrad1 |
-5 row store | 6 (final reducer only) reduction tree + SGD.  Also hipEvent times of the single-launch step,
-the gradient-only kernel, the two-launch path and graph rounds.  Stamped runs are slower than real ones:
-read shares, not totals.
+5 row store.  Reports
+  * hipEvent times of the gradient-only kernel, the two-launch and single-launch rounds and the persistent round;
+  * the per-step kernel's phases cold (first pass of a launch) and warm (MODE 2: the same workgroup computes
+    its sample again right after, with warm instruction / scalar / data caches);
+  * the persistent round kernel's phases in a warm step (step 1): 0 param sweep + stage | 1..4 as above |
+    5 row publish + owned-column sweep | 6 ordered sums + SGD + publish.
+Stamped runs are slower than real ones: read shares, not totals.
 """
-import ctypes as C
 import os
 import statistics
 import sys
@@ -20,6 +23,8 @@ from crossscale_ecg.ops import _lib  # noqa: E402
 from crossscale_ecg.ops.fused_tiny import tiny_step_grads, labels_int32, slab_stride, FusedTinyTrainer  # noqa: E402
 
 NAMES = ["stage", "conv1", "conv2+mask", "head||M", "dgrad2+wgrad1", "row store"]
+ROUND_NAMES = ["params+stage", "conv1", "conv2+mask", "head||M", "dgrad2+wgrad1", "publish+gather",
+               "col sums+sgd"]
 
 
 def ev_time(fn, n):
@@ -35,6 +40,15 @@ def ev_time(fn, n):
     return e0.elapsed_time(e1) / n * 1e3
 
 
+def phase_table(s, k0, names, label):
+    print(label)
+    for k, name in enumerate(names):
+        d = (s[:, k0 + k + 1] - s[:, k0 + k]).double().tolist()
+        print(f"  phase {k} {name:>14s}: median {statistics.median(d):8.0f} cyc  max {max(d):8.0f}")
+    tot = (s[:, k0 + len(names)] - s[:, k0]).double().tolist()
+    print(f"  total            : median {statistics.median(tot):8.0f} cyc")
+
+
 def main():
     dev = torch.device("cuda:0")
     B, L, N = 256, int(os.environ.get("DIAG_L", 500)), 20000
@@ -47,44 +61,50 @@ def main():
     lib = _lib.kernels()
     slab = torch.empty(B, slab_stride(2), device=dev)
     print(f"gradient-only kernel (eager loop): {ev_time(lambda: tiny_step_grads(flat, x, y32, idx, B, 2, slab), 200):.2f} us")
-    for single in (True, False):
+    for name, kw in (("two-launch  ", dict(persistent=False)), ("single-launch", dict(single_launch=True)),
+                     ("persistent  ", dict(persistent=True))):
         m = TinyECG().to(dev)
-        tr = FusedTinyTrainer(m, x, y, B, 50, seed=0, single_launch=single)
+        tr = FusedTinyTrainer(m, x, y, B, 50, seed=0, **kw)
         tr.run_round()
         torch.cuda.synchronize()
-        t = ev_time(lambda: tr.run_round(), 10) / 50
+        t = ev_time(lambda: tr.run_round(), 20) / 50
         tr.use_graph = False
         te = ev_time(lambda: tr.run_round(), 4) / 50
-        print(f"{'single-launch' if single else 'two-launch  '} step: graph {t:.2f} us/step, eager {te:.2f} us/step")
+        tr.check_status()
+        print(f"{name} round: graph {t:.2f} us/step, eager {te:.2f} us/step")
         tr.close()
-    # stamped run of the single-launch step
-    m = TinyECG().to(dev)
-    tr = FusedTinyTrainer(m, x, y, B, 1, seed=0, use_graph=False)
+
+    # cold vs warm passes of the per-step kernel (MODE 2)
     st = torch.zeros(B * 16, dtype=torch.int64, device=dev)
     lib.ecg_tiny_set_stamps(st.data_ptr())
     for _ in range(5):
         st.zero_()
-        tr.run_round()
+        _lib.check(lib.ecg_tiny_step_grads_twice(x.data_ptr(), L, x.stride(0), idx.data_ptr(), y32.data_ptr(),
+                                                 flat.data_ptr(), 2, slab.data_ptr(), slab.shape[1], B, 1.0 / B, 0,
+                                                 _lib.stream_ptr(dev)), "twice")
     torch.cuda.synchronize()
     lib.ecg_tiny_set_stamps(None)
-    tr.close()
     s = st.view(B, 16).cpu()
     cyc = (s[:, 6] - s[:, 0]).double()
-    rt = (s[:, 14] - s[:, 15]).double() * 10.0  # 100 MHz -> ns
-    ghz = statistics.median((cyc / rt).tolist())
-    print(f"in-kernel clock ~{ghz:.2f} GHz; WG lifetime to row store median {statistics.median(rt.tolist()) / 1e3:.2f} us "
-          f"({statistics.median(cyc.tolist()):.0f} cycles)")
-    for k in range(6):
-        d = (s[:, k + 1] - s[:, k]).double().tolist()
-        print(f"  phase {k} {NAMES[k]:>14s}: median {statistics.median(d):8.0f} cyc  max {max(d):8.0f}")
-    fin = (s[:, 7] != 0).nonzero().flatten().tolist()
-    t0 = s[:, 15].min()
-    if fin:
-        f = fin[0]
-        print(f"  final reducer WG {f}: tree+SGD {int(s[f, 7] - s[f, 6])} cyc; kernel span to final end "
-              f"{(s[f, 13] - t0).item() * 10 / 1e3:.2f} us")
-    print(f"  WG start spread {(s[:, 15].max() - t0).item() * 10 / 1e3:.2f} us, last row store "
-          f"{(s[:, 14].max() - t0).item() * 10 / 1e3:.2f} us")
+    rt = (s[:, 14] - s[:, 15]).double() * 10.0  # 100 MHz -> ns (both passes)
+    ghz = statistics.median(((s[:, 13] - s[:, 0]).double() / rt).tolist())
+    print(f"in-kernel clock ~{ghz:.2f} GHz")
+    phase_table(s, 0, NAMES, "per-step kernel, COLD pass (fresh launch):")
+    phase_table(s, 7, NAMES, "per-step kernel, WARM pass (same workgroup, immediately after):")
+    print(f"  cold total median {statistics.median(cyc.tolist()):.0f} cyc")
+
+    # persistent round, warm step 1
+    m = TinyECG().to(dev)
+    tr = FusedTinyTrainer(m, x, y, B, 4, seed=0, use_graph=False, persistent=True)
+    tr.sampler.fill(tr.idx_table)
+    rs = torch.zeros(B * 16, dtype=torch.int64, device=dev)
+    for _ in range(5):
+        rs.zero_()
+        tr._eager_round(4, stamps=rs)
+    torch.cuda.synchronize()
+    tr.check_status()
+    phase_table(rs.view(B, 16).cpu(), 0, ROUND_NAMES, "persistent round kernel, step 1 (warm):")
+    tr.close()
 
 
 if __name__ == "__main__":
