@@ -49,7 +49,7 @@ __host__ __device__ inline Layout make_layout(int nc) {
 // LDS carve (bytes), all offsets multiples of 16.
 struct Smem {
   int Lp;  // L rounded up to 32 (tile pairs)
-  int xs_off, h1_off, dh2_off, ps_off, frag_off, red_off, bytes;
+  int xs_off, xcol_off, h1_off, dh2_off, ps_off, frag_off, red_off, bytes;
 };
 
 // red region (floats): per-wave partials are written with plain stores and summed after a barrier
@@ -102,8 +102,9 @@ __host__ __device__ inline Smem make_smem(int L, int waves, int nc = MAX_CLASSES
   Smem s;
   s.Lp = (L + 31) / 32 * 32;
   s.xs_off = 0;
-  const int xs_bytes = ((s.Lp + 16) * 4 + 15) / 16 * 16;
-  s.h1_off = s.xs_off + xs_bytes;
+  // fp32 window xs[Lp + 16]; bf16 adds the conv1 im2col rows xcol[Lp + 1][8] (row Lp = zeros)
+  s.xcol_off = s.xs_off + ((s.Lp + 16) * 4 + 15) / 16 * 16;
+  s.h1_off = s.xcol_off + (f32 ? 0 : (s.Lp + 1) * 16);
   const int act_bytes = (s.Lp + 8) * C * (f32 ? 4 : 2);  // [Lp+8][16] in the activation type
   s.dh2_off = s.h1_off + act_bytes;
   s.ps_off = s.dh2_off + act_bytes;
@@ -127,6 +128,21 @@ __device__ __forceinline__ s16x4 lds_tr16(const __bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
 }
 
+// Broadcast lane ``src``'s value to the whole wave (v_readlane_b32: the result is an SGPR; src wave-uniform).
+__device__ __forceinline__ float lane_bcast(float v, int src) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+}
+
+// Sum over the 16 lanes of a DPP row (inclusive row_shr scan 1, 2, 4, 8; out-of-row sources read 0):
+// lane 15 of each row ends with the row's total.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
+  return v;
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // The per-sample computation (phases 0-5), shared by the per-step kernel and the persistent round kernel.
 //
@@ -137,6 +153,14 @@ __device__ __forceinline__ s16x4 lds_tr16(const __bf16* p) {
 //   dh1[t][ci]       = sum_{co,k} m[t-k+2][co] * (g[co] w2[co][ci][k])   (g folded into the B operand)
 // so the M MFMAs of waves 1.. run concurrently with the head on wave 0, and every MFMA operand that
 // carries activation gradients is the exact 0/1 mask.
+//
+// bf16 path (AMP): every conv runs on MFMA with the TIME axis as the N dimension, so a lane's accumulator holds
+// 4 consecutive channels of one time step and every epilogue is one 8-byte LDS access:
+//   conv1       out^T[co][t] = W1ext[co][kk] x xcol[t][kk]   (kk < 7: taps, kk = 7: bias x "t < L", K padded to 32)
+//   conv2       out^T[co][t] = W2[co][(k,ci)] x h1col[(k,ci)][t]
+//   conv2 dgrad dh1^T[ci][t] = (g W2)[ci][(k,co)] x m[(k,co)][t], times relu'(h1), written over h1
+//   conv1 wgrad dW1ext[ci][kk] = dh1^T[ci][t] x xcol[t][kk]   (both operands by transposing reads; kk = 7 -> db1)
+// The fp32 path keeps conv1 / conv1-wgrad on VALU (exact f32) and the time-major MFMA orientation.
 template <int WAVES, bool F32>
 struct TinySample {
   using AT = std::conditional_t<F32, float, __bf16>;  // activation / MFMA operand type
@@ -146,6 +170,7 @@ struct TinySample {
   int L, Lp, NP, nc;
   int tid, lane, w, h, c;  // h: lane quarter, c: channel owned by this lane in C-layout phases
   float* xs;               // [Lp + 16]: xs[i] = x[i - 3] (conv1 halo)
+  __bf16* xcol;            // bf16 path: [Lp + 1][8]: {x[t-3..t+3], t < L} (0 for t >= L), row Lp = zeros
   AT* h1s;                 // row (t+2): h1[t][ci]
   AT* ms;                  // row (t+4): m[t][co] = relu'(h2) in {0,1}
   float* ps;               // fp32 copy of the flat params
@@ -161,6 +186,7 @@ struct TinySample {
     Lp = sm.Lp;
     NP = Lp / 32;
     xs = reinterpret_cast<float*>(smem + sm.xs_off);
+    xcol = reinterpret_cast<__bf16*>(smem + sm.xcol_off);
     h1s = reinterpret_cast<AT*>(smem + sm.h1_off);
     ms = reinterpret_cast<AT*>(smem + sm.dh2_off);
     ps = reinterpret_cast<float*>(smem + sm.ps_off);
@@ -177,11 +203,33 @@ struct TinySample {
   }
 
   // ---- phase 0: window, parameters, constant pads
-  __device__ __forceinline__ void stage_x(const float* __restrict__ xrow) {
-    for (int i = tid; i < Lp + 16; i += NT) {
-      const int t = i - 3;
-      xs[i] = (t >= 0 && t < L) ? xrow[t] : 0.f;
+  // The window goes global -> registers (load_x) -> LDS (put_x), so the persistent round can issue the loads of
+  // the next step's window early: xs elements i = tid + k*NT, one coalesced load each.
+  static constexpr int XK = (32 * MAX_PAIRS_PER_WAVE * WAVES + 16 + NT - 1) / NT;
+  struct XRegs {
+    float v[XK];
+  };
+  __device__ __forceinline__ void load_x(const float* __restrict__ xrow, XRegs& r) const {
+#pragma unroll
+    for (int k = 0; k < XK; ++k) {
+      const int i = tid + k * NT, t = i - 3;
+      if (k * NT < Lp + 16) {  // wave-uniform; the load itself is clamped, never branched
+        const float v = xrow[min(max(t, 0), L - 1)];
+        r.v[k] = (i < Lp + 16 && t >= 0 && t < L) ? v : 0.f;
+      }
     }
+  }
+  __device__ __forceinline__ void put_x(const XRegs& r) {
+#pragma unroll
+    for (int k = 0; k < XK; ++k) {
+      const int i = tid + k * NT;
+      if (i < Lp + 16) xs[i] = r.v[k];
+    }
+  }
+  __device__ __forceinline__ void stage_x(const float* __restrict__ xrow) {
+    XRegs r;
+    load_x(xrow, r);
+    put_x(r);
   }
 
   // One flat parameter -> its fp32 LDS copy and, for conv2 weights w2[co][ci][k], the MFMA B fragments in
@@ -205,14 +253,17 @@ struct TinySample {
     }
   }
 
-  // bf16: r in [80, 96) (the 6th, padding tap) of both fragment sets is zero; h1 halo rows 0,1 (t=-2,-1) and
-  // [Lp+2, Lp+8), mask halo rows [0,4) and [Lp+4, Lp+8) are zero.  No phase writes them, so once per launch.
+  // bf16: r in [80, 96) (the 6th, padding tap) of both fragment sets and the im2col row Lp are zero; h1 halo
+  // rows 0,1 (t=-2,-1) and [Lp+2, Lp+8), mask halo rows [0,4) and [Lp+4, Lp+8) are zero.  No phase writes
+  // them, so once per launch.
   __device__ __forceinline__ void zero_pads() {
-    if constexpr (!F32)
+    if constexpr (!F32) {
       for (int e = tid; e < 2 * 32 * 8; e += NT) {
         const int which = e >> 8, l = 32 + ((e >> 3) & 31), j = e & 7;
         (which ? fragD : fragF)[(2 * 64 + l) * 8 + j] = ecg::to_bf16(0.f);
       }
+      if (tid < 4) reinterpret_cast<uint32_t*>(xcol + Lp * 8)[tid] = 0u;  // im2col zero row
+    }
     constexpr int DW = C * (int)sizeof(AT) / 4;  // dwords per activation row
     uint32_t* h1w = reinterpret_cast<uint32_t*>(h1s);
     uint32_t* mw = reinterpret_cast<uint32_t*>(ms);
@@ -225,8 +276,45 @@ struct TinySample {
     }
   }
 
-  // ---- phase 1: conv1 + bias + ReLU (VALU) into h1s
+  // ---- phase 1: conv1 + bias + ReLU into h1s (bf16: MFMA over the im2col rows; fp32: VALU)
   __device__ __forceinline__ void conv1() {
+    if constexpr (!F32) {
+      // A = W1ext[co][kk]: quarter 0 holds kk 0..7 (taps, then the bias), quarters 1..3 the zero K padding
+      bf16x8 Aw;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = j < K1 ? ps[lay.w1 + c * K1 + j] : ps[lay.b1 + c];
+        Aw[j] = ecg::to_bf16(h == 0 ? v : 0.f);
+      }
+      // B = xcol[t][kk]: quarter 0 reads the im2col row of its time step, quarters 1..3 the zero row.  Each wave
+      // builds the rows of its own tiles from xs first (same-wave LDS order; phase 4 reads them after barriers).
+      const __bf16* xb = xcol + (h == 0 ? (lane & 15) * 8 : Lp * 8);
+      const int tstride = h == 0 ? 16 * 8 : 0;
+      const int ntiles = Lp / 16;
+#pragma unroll
+      for (int pi = 0; pi < 2 * MAX_PAIRS_PER_WAVE; ++pi) {
+        const int tile = w + pi * WAVES;
+        if (tile < ntiles) {
+          {  // this wave's im2col rows of the tile: lane (n, h) writes columns 2h, 2h+1 of row t = 16*tile + n
+            const int t = 16 * tile + (lane & 15), j0 = 2 * h;
+            const bool tv = t < L;
+            const float v0 = xs[t + j0], v1 = j0 + 1 < K1 ? xs[t + j0 + 1] : 1.f;  // column 7: bias x 1
+            bf16x2 pr;
+            pr[0] = ecg::to_bf16(tv ? v0 : 0.f);
+            pr[1] = ecg::to_bf16(tv ? v1 : 0.f);
+            *reinterpret_cast<bf16x2*>(xcol + t * 8 + j0) = pr;
+          }
+          const bf16x8 Bx = *reinterpret_cast<const bf16x8*>(xb + tile * tstride);
+          const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Aw, Bx, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          // acc[i] = conv1(x)[t = 16*tile + (lane&15)][co = 4h + i] + bias (exactly 0 for t >= L)
+          bf16x4 o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = (AT)fmaxf(acc[i], 0.f);
+          *reinterpret_cast<bf16x4*>(h1s + (16 * tile + (lane & 15) + 2) * C + 4 * h) = o;
+        }
+      }
+      return;
+    }
     mask1 = 0u;
     float w1r[K1];
 #pragma unroll
@@ -263,6 +351,63 @@ struct TinySample {
 
   // ---- phase 2: conv2 (MFMA) + bias + ReLU -> pool partials, mask m -> LDS
   __device__ __forceinline__ void conv2() {
+    if constexpr (!F32) {
+      // out^T[co][t]: A = W2[co][(k,ci)] (the fragments are lane-order symmetric: the same registers serve as
+      // B[(k,ci)][co] or A[co][(k,ci)]), B = h1col[(k,ci)][t] read straight from the [t][ci] rows
+      bf16x8 Wf[3];
+#pragma unroll
+      for (int s = 0; s < 3; ++s) Wf[s] = *reinterpret_cast<const bf16x8*>(fragF + (s * 64 + lane) * 8);
+      float b2v[4], pool[4], cnt[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        b2v[i] = ps[lay.b2 + 4 * h + i];
+        pool[i] = cnt[i] = 0.f;
+      }
+#pragma unroll
+      for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
+        const int pair = w + pi * WAVES;
+        if (pair < NP) {
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const int t0 = 32 * pair + 16 * half;
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+              const int tap = 2 * s + (h >> 1);
+              const int r = t0 + (lane & 15) + tap - 2;  // h1 time index
+              const bf16x8 Bh = *reinterpret_cast<const bf16x8*>(h1s + (r + 2) * C + 8 * (h & 1));
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Wf[s], Bh, acc, 0, 0, 0);
+            }
+            // acc[i] = conv2(h1)[t = t0 + (lane&15)][co = 4h + i]
+            const int t = t0 + (lane & 15);
+            const bool tv = t < L;
+            bf16x4 mk;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float v = tv ? fmaxf(acc[i] + b2v[i], 0.f) : 0.f;
+              const bool on = v > 0.f;
+              pool[i] += v;
+              cnt[i] += on ? 1.f : 0.f;
+              mk[i] = ecg::to_bf16(on ? 1.f : 0.f);
+            }
+            *reinterpret_cast<bf16x4*>(ms + (t + 4) * C + 4 * h) = mk;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pool[i] = row16_sum(pool[i]);
+        cnt[i] = row16_sum(cnt[i]);
+      }
+      if ((lane & 15) == 15) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          red[RED_POOL + w * 16 + 4 * h + i] = pool[i];
+          red[red_cnt(WAVES) + w * 16 + 4 * h + i] = cnt[i];
+        }
+      }
+      return;
+    }
     bf16x8 Bf[3];
     float Wf[F32_KSTEPS];
     if constexpr (F32) {
@@ -325,51 +470,58 @@ struct TinySample {
   template <bool TRAIN>
   __device__ __forceinline__ void head_and_M(int ylab, float inv_B, float* out, int out_stride, int b) {
     if (w == 0) {
-      if (lane < 16) {
-        float pooled = 0.f;
+      // Wave 0 runs the head with cross-lane traffic through v_readlane (SGPR broadcasts), not LDS shuffles.
+      // pooled[c] (every quarter computes all 16 channels; only the broadcasts of lanes 0..15 are used)
+      float pp[WAVES];
 #pragma unroll
-        for (int ww = 0; ww < WAVES; ++ww) pooled += red[RED_POOL + ww * 16 + lane];
-        red[RED_POOLED + lane] = pooled * (1.0f / (float)L);
-      }
-      // every lane picks up the 16 pooled channels (LDS broadcast reads; same-wave write -> read order)
+      for (int ww = 0; ww < WAVES; ++ww) pp[ww] = red[RED_POOL + ww * 16 + c];
+      float pooled = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < WAVES; ++ww) pooled += pp[ww];
+      pooled *= 1.0f / (float)L;
       float pv[C];
 #pragma unroll
-      for (int q4 = 0; q4 < C / 4; ++q4) {
-        const float4 v = reinterpret_cast<const float4*>(red + RED_POOLED)[q4];
-        pv[4 * q4] = v.x; pv[4 * q4 + 1] = v.y; pv[4 * q4 + 2] = v.z; pv[4 * q4 + 3] = v.w;
-      }
-      // lane n (< nc) of each 16-lane group computes logit n
+      for (int co = 0; co < C; ++co) pv[co] = lane_bcast(pooled, co);
+      // logit n = c (< nc) on every quarter
       const int n = c;
       float logit = -INFINITY;
       if (n < nc) {
+        const float4* whr = reinterpret_cast<const float4*>(ps + lay.wh + n * C);
         logit = ps[lay.bh + n];
 #pragma unroll
-        for (int co = 0; co < C; ++co) logit = fmaf(ps[lay.wh + n * C + co], pv[co], logit);
+        for (int q4 = 0; q4 < C / 4; ++q4) {
+          const float4 wv4 = whr[q4];
+          logit = fmaf(wv4.x, pv[4 * q4], logit);
+          logit = fmaf(wv4.y, pv[4 * q4 + 1], logit);
+          logit = fmaf(wv4.z, pv[4 * q4 + 2], logit);
+          logit = fmaf(wv4.w, pv[4 * q4 + 3], logit);
+        }
       }
       if constexpr (!TRAIN) {
         if (lane < nc) out[(long)b * out_stride + n] = logit;
       } else {
-        float m = logit;
-#pragma unroll
-        for (int off = 8; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+        // softmax-CE over the nc logits of lanes 0..nc-1 (wave-uniform scalar loop)
+        float m = -INFINITY;
+        for (int nn = 0; nn < nc; ++nn) m = fmaxf(m, lane_bcast(logit, nn));
         const float e = (n < nc) ? __expf(logit - m) : 0.f;
-        float ssum = e;
-#pragma unroll
-        for (int off = 8; off >= 1; off >>= 1) ssum += __shfl_xor(ssum, off, 64);
-        const int y = ylab;
-        const float logit_y = __shfl(logit, (lane & 48) + y, 64);
-        const float loss = m + __logf(ssum) - logit_y;
+        float ssum = 0.f;
+        for (int nn = 0; nn < nc; ++nn) ssum += lane_bcast(e, nn);
+        const int y = __builtin_amdgcn_readfirstlane(ylab);
+        const float loss = m + __logf(ssum) - lane_bcast(logit, y);
         const float dlogit = (n < nc) ? (e / ssum - (n == y ? 1.f : 0.f)) * inv_B : 0.f;
         float* hg = red + red_head(WAVES);  // [wh, P] of this sample's row, stored with the rest in phase 5
         if (lane < nc) {
+          float4* hr = reinterpret_cast<float4*>(hg + n * C);
 #pragma unroll
-          for (int co = 0; co < C; ++co) hg[n * C + co] = dlogit * pv[co];
+          for (int q4 = 0; q4 < C / 4; ++q4)
+            hr[q4] = make_float4(dlogit * pv[4 * q4], dlogit * pv[4 * q4 + 1], dlogit * pv[4 * q4 + 2],
+                                 dlogit * pv[4 * q4 + 3]);
           hg[nc * C + n] = dlogit;
         }
         if (lane == 0) hg[nc * C + nc] = loss;
         // dpooled[co] = sum_n dlogit[n] * Wh[n][co]; lane co (< 16)
         float dp = 0.f;
-        for (int nn = 0; nn < nc; ++nn) dp = fmaf(__shfl(dlogit, nn, 64), ps[lay.wh + nn * C + c], dp);
+        for (int nn = 0; nn < nc; ++nn) dp = fmaf(lane_bcast(dlogit, nn), ps[lay.wh + nn * C + c], dp);
         if (lane < 16) red[RED_G + c] = dp * (1.0f / (float)L);
       }
     } else if (TRAIN && w <= 5 * msplit(WAVES)) {
@@ -392,15 +544,25 @@ struct TinySample {
         }
       } else {
         const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
-        for (int pair = p0; pair < p1; ++pair) {
+        auto mfma_pair = [&](int pair, f32x4 a) {
           const int ta = 32 * pair + 8 * h + q;  // time of row q of this lane-quarter's first 4x16 block
           // A[co][t] (lane: co = l&15, t = 32*pair + 8h + j): transposing reads of the [t][co] mask image
           const bf16x8 A = cat44(lds_tr16(ms + (ta + 4) * C + p4), lds_tr16(ms + (ta + 4 + 4) * C + p4));
           // B[t][ci] = h1[t + k - 2][ci]
           const bf16x8 Bm =
               cat44(lds_tr16(h1s + (ta + k - 2 + 2) * C + p4), lds_tr16(h1s + (ta + k - 2 + 4 + 2) * C + p4));
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bm, acc, 0, 0, 0);
+          return __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bm, a, 0, 0, 0);
+        };
+        // two independent accumulation chains so the next pair's transposing reads overlap this pair's MFMA
+        f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
+        int pair = p0;
+        for (; pair + 1 < p1; pair += 2) {
+          acc = mfma_pair(pair, acc);
+          acc2 = mfma_pair(pair + 1, acc2);
         }
+        if (pair < p1) acc = mfma_pair(pair, acc);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] += acc2[i];
       }
       // acc[i] = M_k[co = 4h+i][ci = c]
       float* pm = red + red_m(WAVES) + part * 1280;
@@ -420,6 +582,55 @@ struct TinySample {
     }
     bf16x8 Bd[3];
     float Wd[F32_KSTEPS];
+    if constexpr (!F32) {
+      // (g W2) fragments, used as A[ci][(k,co)]
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const bf16x8 raw = *reinterpret_cast<const bf16x8*>(fragD + (s * 64 + lane) * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Bd[s][j] = ecg::to_bf16(ecg::from_bf16(raw[j]) * gq[j]);
+      }
+      const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
+      const __bf16* xzero = xcol + Lp * 8;
+      f32x4 wacc = {0.f, 0.f, 0.f, 0.f};  // dW1ext[ci = 4h + i][kk = lane & 15] over this wave's pairs
+#pragma unroll
+      for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
+        const int pair = w + pi * WAVES;
+        if (pair < NP) {
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const int t0 = 32 * pair + 16 * half;
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+              const int k = 2 * s + (h >> 1);
+              const int r = t0 + (lane & 15) - k + 2;  // mask time index
+              const bf16x8 Am = *reinterpret_cast<const bf16x8*>(ms + (r + 4) * C + 8 * (h & 1));
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Bd[s], Am, acc, 0, 0, 0);
+            }
+            // acc[i] = dh1[t = t0 + (lane&15)][ci = 4h + i]; times relu'(h1), written over h1 (this wave's rows)
+            AT* hp = h1s + (t0 + (lane & 15) + 2) * C + 4 * h;
+            const bf16x4 hv = *reinterpret_cast<const bf16x4*>(hp);
+            bf16x4 dv;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dv[i] = ecg::to_bf16((float)hv[i] > 0.f ? acc[i] : 0.f);
+            *reinterpret_cast<bf16x4*>(hp) = dv;
+          }
+          // conv1 wgrad over the pair's 32 steps: A[ci][t] = dh1 (transposing reads of the rows just written by
+          // this wave), B[t][kk] = xcol (columns 8..15 come from the zero row)
+          const int ta = 32 * pair + 8 * h + q;
+          const bf16x8 Ad = cat44(lds_tr16(h1s + (ta + 2) * C + p4), lds_tr16(h1s + (ta + 2 + 4) * C + p4));
+          const __bf16* xa = p4 < 8 ? xcol + ta * 8 + p4 : xzero;
+          const __bf16* xb = p4 < 8 ? xcol + (ta + 4) * 8 + p4 : xzero;
+          wacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ad, cat44(lds_tr16(xa), lds_tr16(xb)), wacc, 0, 0, 0);
+        }
+      }
+      if ((lane & 15) < 8) {  // kk < 7: dW1[ci][kk]; kk = 7: db1[ci]
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[red_dw1(WAVES) + w * 128 + (4 * h + i) * 8 + (lane & 15)] = wacc[i];
+      }
+      return;
+    }
     if constexpr (F32) {
       // 16x16x4 f32: B[r][ci], r = 4s + h = 16k + co
 #pragma unroll
@@ -561,9 +772,13 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     S.dgrad();
     __syncthreads();
     ECG_STAMP(5)
-    // phase 5: combine partials, scale by g, write this sample's gradient row (write-through: the
-    // single-launch reduction below reads it inside this launch)
-    for (int i = tid; i <= S.lay.P; i += S.NT) st_wt(slab_r, rowbase + i, S.row_value(i));
+    // phase 5: combine partials, scale by g, write this sample's gradient row.  The single-launch reduction
+    // below reads it inside this launch (write-through stores); otherwise the kernel boundary publishes it.
+    if (opt.ctl != nullptr) {
+      for (int i = tid; i <= S.lay.P; i += S.NT) st_wt(slab_r, rowbase + i, S.row_value(i));
+    } else {
+      for (int i = tid; i <= S.lay.P; i += S.NT) out[rowbase + i] = S.row_value(i);
+    }
     ECG_STAMP(6)
 #undef ECG_STAMP
     if (MODE == 2) __syncthreads();  // the second pass reuses the LDS
@@ -809,7 +1024,6 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_round_kernel(RoundArgs a)
   using TS = TinySample<WAVES, F32>;
   constexpr int NT = TS::NT;
   constexpr int KMAX = (2048 + NT - 1) / NT;                                 // granules per thread per sweep
-  constexpr int XR = (32 * MAX_PAIRS_PER_WAVE * WAVES + 16 + NT - 1) / NT;   // window floats per thread
   TS S(smem, a.L, a.nc);
   const int tid = threadIdx.x, b = blockIdx.x, G = a.G;
   const int P = S.lay.P, ncols = P + 1;
@@ -831,18 +1045,12 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_round_kernel(RoundArgs a)
   }
   if (tid == 0) gflag[0] = 0;
 
-  float xr[XR];
+  typename TS::XRegs xr;
   int ynext = 0;
-  auto prefetch = [&](int s) {  // window + label of step s into registers (clamped loads, no branches)
+  auto prefetch = [&](int s) {  // window + label of step s into registers
     const long row = a.idx_table[(long)s * G + b];
     ynext = a.Y[row];
-    const float* xrow = a.X + row * a.ldx;
-#pragma unroll
-    for (int k = 0; k < XR; ++k) {
-      const int i = tid + k * NT, t = i - 3;
-      const float v = xrow[min(max(t, 0), S.L - 1)];
-      xr[k] = (i < S.Lp + 16 && t >= 0 && t < S.L) ? v : 0.f;
-    }
+    S.load_x(a.X + row * a.ldx, xr);
   };
   auto give_up = [&]() -> bool {  // block-uniform after a barrier
     if (gflag[0] == 0) return false;
@@ -867,11 +1075,7 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_round_kernel(RoundArgs a)
         if (i < P) S.put_param(i, v[k]);
       }
     }
-#pragma unroll
-    for (int k = 0; k < XR; ++k) {
-      const int i = tid + k * NT;
-      if (i < S.Lp + 16) S.xs[i] = xr[k];
-    }
+    S.put_x(xr);
     const int ylab = ynext;
     __syncthreads();
     if (give_up()) return;
