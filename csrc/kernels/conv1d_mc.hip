@@ -97,121 +97,17 @@ struct FwdCfg {
   static constexpr int smem(int nbuf) { return stage_bytes(nbuf) > EP_BYTES ? stage_bytes(nbuf) : EP_BYTES; }
 };
 
-// NBUF = 2: double-buffered LDS, one barrier per K tile (2 workgroups / CU at 128x128).
-// NBUF = 1: one LDS buffer, two barriers per K tile, half the LDS -> 3 workgroups / CU, i.e. 1.5x the
-//           register-staged tiles in flight per CU for this HBM-latency-bound loop.
-template <int BM, int BN, int EPI, int NBUF>
-__global__ __launch_bounds__(THREADS, NBUF == 1 ? 3 : 2) void conv1d_nlc_fwd_kernel(FwdArgs a, int MT, int NT) {
+// Forward / data-grad epilogue shared by both main loops: accumulators -> LDS (fp32, per-wave region, two halves
+// of WM/2 rows) -> row-major pass with 8 channels per lane: + bias, + residual (optionally ReLU-masked), ReLU,
+// bf16 round, and the per-channel BatchNorm partials of the rounded values (stat_mode 0) or the BN-backward
+// partials (stat_mode 1).  The staging buffers must be dead (all waves past the main loop's last barrier).
+template <int BM, int BN, int EPI>
+__device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, f32x4 (&acc)[BM / 32][BN / 32], unsigned char* smem,
+                                             int m0, int n0, int mt, int MT, int Lrow, int M, int P, int ph) {
   using Cfg = FwdCfg<BM, BN>;
-  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NA = Cfg::NA, NB = Cfg::NB;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __bf16* const lds = reinterpret_cast<__bf16*>(smem);  // [buf][A (BM rows) | B (BN rows)][LDS_ROW]
+  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1, wc = wv & 1;
-  // bijective XCD remap of the 1-D grid (blockIdx % 8 = blocks sharing an XCD)
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int mt = wgid / NT, nt = wgid % NT;
-  const int K = a.Kw * a.Cin;
-  // Strided data-grad (in_dil = s > 1) is phase-decomposed: output rows u = i*s + ph of one phase share the
-  // taps k = k0 + j*s (k0 = (pad - ph) mod s) that hit non-inserted input rows, so the zero half of the
-  // dilated input is never multiplied.  M tiles are per phase; K tiles run over the phase's taps only.
-  const int P = a.in_dil;
-  const int ph = P > 1 ? mt / a.tpp : 0;
-  const int m0 = (P > 1 ? mt - ph * a.tpp : mt) * BM, n0 = nt * BN;
-  const int CB = a.Cin / BK;
-  const int k0 = P > 1 ? ((a.pad - ph) % P + P) % P : 0;
-  const int nk = P > 1 ? (k0 < a.Kw ? (a.Kw - k0 + P - 1) / P : 0) * CB : K / BK;
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // One register set: tile t+1's global loads are in flight during tile t's MFMAs.  (Measured alternatives,
-  // profiles/r1_resnet/conv_microbench_*: a second register set (tile t+2 in flight) costs occupancy and runs
-  // 35 % slower; B fragments loaded straight from L2 into registers, bypassing LDS, 25-35 % slower.)
-  uint4 ra0[NA], rb0[NB];
-  // per-thread A rows are fixed across K tiles: precompute each row's sample base and first input position
-  const int Lrow = P > 1 ? a.Lph : a.Lout;  // rows per sample in this kernel's (phase-local) M index
-  const int M = a.B * Lrow;
-  long abase[NA];
-  int apos[NA];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) {
-    const int e = tid + i * THREADS, m = m0 + (e >> 3);
-    const int b = m / Lrow, t = m % Lrow;
-    const int u = P > 1 ? t * P + ph : t;  // output position
-    abase[i] = (long)b * a.Lin * a.Cin + (e & 7) * 8;
-    apos[i] = (m < M && u < a.Lout) ? u * a.stride - a.pad : INT_MIN / 2;  // invalid rows never pass the check
-  }
-  const __bf16* wb = a.w + (long)(n0 + (tid >> 3)) * (a.Kw * a.Cin) + (tid & 7) * 8;
-  const int Lext = a.in_dil > 1 ? (a.Lin - 1) * a.in_dil + 1 : a.Lin;  // extent of the (dilated) input
-  auto ld_set = [&](uint4* ra, uint4* rb, int t) {
-    const int tc = t < nk ? t : nk - 1;
-    const int k = k0 + (tc / CB) * P, c0 = (tc % CB) * BK;
-    const int kk = k * a.Cin + c0;
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      int u = apos[i] + k;
-      bool ok = u >= 0 && u < Lext;
-      if (a.in_dil > 1) {
-        ok = ok && (u % a.in_dil == 0);
-        u /= a.in_dil;
-      }
-      ra[i] = ok ? *reinterpret_cast<const uint4*>(a.x + abase[i] + (long)u * a.Cin + c0) : make_uint4(0u, 0u, 0u, 0u);
-    }
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-      rb[i] = *reinterpret_cast<const uint4*>(wb + (long)i * (THREADS / 8) * (a.Kw * a.Cin) + kk);
-  };
-  auto st_set = [&](__bf16* base, const uint4* ra, const uint4* rb) {
-#pragma unroll
-    for (int i = 0; i < NA; ++i) store_one(base, tid + i * THREADS, ra[i]);
-#pragma unroll
-    for (int i = 0; i < NB; ++i) store_one(base + Cfg::A_EL, tid + i * THREADS, rb[i]);
-  };
-  auto mma = [&](const __bf16* As) {
-    const __bf16* Bs = As + Cfg::A_EL;
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8 af[FM], bfr[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(As + (wr * WM + i * 16 + (lane & 15)) * LDS_ROW + ks * 32 +
-                                                 8 * (lane >> 4));
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (wc * WN + j * 16 + (lane & 15)) * LDS_ROW + ks * 32 +
-                                                  8 * (lane >> 4));
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-  };
-  __bf16* const L0 = lds;
-  __bf16* const L1 = lds + (NBUF == 2 ? Cfg::A_EL + Cfg::B_EL : 0);
-  if (nk > 0) {  // block-uniform (a phase without taps leaves acc = 0)
-    ld_set(ra0, rb0, 0);
-    st_set(L0, ra0, rb0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      ld_set(ra0, rb0, kt + 1);
-      if constexpr (NBUF == 2) {
-        mma((kt & 1) ? L1 : L0);
-        st_set((kt & 1) ? L0 : L1, ra0, rb0);
-      } else {
-        mma(L0);
-        __syncthreads();  // every wave is done reading the buffer
-        st_set(L0, ra0, rb0);
-      }
-      __syncthreads();
-    }
-  }
-  // ---- epilogue: fragments -> LDS (fp32, per-wave region, two halves of WM/2 rows) -> row-major pass with
-  // 8 channels per lane.  The staging buffers are dead after the last barrier.
   constexpr int EP_LD = Cfg::EP_LD, HR = WM / 2;
   float* ep = reinterpret_cast<float*>(smem) + wv * HR * EP_LD;
   constexpr int CG = WN / 8, RSTEP = 64 / CG, ITEMS = HR / RSTEP;
@@ -331,6 +227,228 @@ __global__ __launch_bounds__(THREADS, NBUF == 1 ? 3 : 2) void conv1d_nlc_fwd_ker
   }
 }
 
+// NBUF = 2: double-buffered LDS, one barrier per K tile (2 workgroups / CU at 128x128).
+// NBUF = 1: one LDS buffer, two barriers per K tile, half the LDS -> 3 workgroups / CU, i.e. 1.5x the
+//           register-staged tiles in flight per CU for this HBM-latency-bound loop.
+template <int BM, int BN, int EPI, int NBUF>
+__global__ __launch_bounds__(THREADS, NBUF == 1 ? 3 : 2) void conv1d_nlc_fwd_kernel(FwdArgs a, int MT, int NT) {
+  using Cfg = FwdCfg<BM, BN>;
+  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NA = Cfg::NA, NB = Cfg::NB;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __bf16* const lds = reinterpret_cast<__bf16*>(smem);  // [buf][A (BM rows) | B (BN rows)][LDS_ROW]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  // bijective XCD remap of the 1-D grid (blockIdx % 8 = blocks sharing an XCD)
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int mt = wgid / NT, nt = wgid % NT;
+  const int K = a.Kw * a.Cin;
+  // Strided data-grad (in_dil = s > 1) is phase-decomposed: output rows u = i*s + ph of one phase share the
+  // taps k = k0 + j*s (k0 = (pad - ph) mod s) that hit non-inserted input rows, so the zero half of the
+  // dilated input is never multiplied.  M tiles are per phase; K tiles run over the phase's taps only.
+  const int P = a.in_dil;
+  const int ph = P > 1 ? mt / a.tpp : 0;
+  const int m0 = (P > 1 ? mt - ph * a.tpp : mt) * BM, n0 = nt * BN;
+  const int CB = a.Cin / BK;
+  const int k0 = P > 1 ? ((a.pad - ph) % P + P) % P : 0;
+  const int nk = P > 1 ? (k0 < a.Kw ? (a.Kw - k0 + P - 1) / P : 0) * CB : K / BK;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // One register set: tile t+1's global loads are in flight during tile t's MFMAs.  (Measured alternatives,
+  // profiles/r1_resnet/conv_microbench_*: a second register set (tile t+2 in flight) costs occupancy and runs
+  // 35 % slower; B fragments loaded straight from L2 into registers, bypassing LDS, 25-35 % slower.)
+  uint4 ra0[NA], rb0[NB];
+  // per-thread A rows are fixed across K tiles: precompute each row's sample base and first input position
+  const int Lrow = P > 1 ? a.Lph : a.Lout;  // rows per sample in this kernel's (phase-local) M index
+  const int M = a.B * Lrow;
+  long abase[NA];
+  int apos[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int e = tid + i * THREADS, m = m0 + (e >> 3);
+    const int b = m / Lrow, t = m % Lrow;
+    const int u = P > 1 ? t * P + ph : t;  // output position
+    abase[i] = (long)b * a.Lin * a.Cin + (e & 7) * 8;
+    apos[i] = (m < M && u < a.Lout) ? u * a.stride - a.pad : INT_MIN / 2;  // invalid rows never pass the check
+  }
+  const __bf16* wb = a.w + (long)(n0 + (tid >> 3)) * (a.Kw * a.Cin) + (tid & 7) * 8;
+  const int Lext = a.in_dil > 1 ? (a.Lin - 1) * a.in_dil + 1 : a.Lin;  // extent of the (dilated) input
+  auto ld_set = [&](uint4* ra, uint4* rb, int t) {
+    const int tc = t < nk ? t : nk - 1;
+    const int k = k0 + (tc / CB) * P, c0 = (tc % CB) * BK;
+    const int kk = k * a.Cin + c0;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      int u = apos[i] + k;
+      bool ok = u >= 0 && u < Lext;
+      if (a.in_dil > 1) {
+        ok = ok && (u % a.in_dil == 0);
+        u /= a.in_dil;
+      }
+      ra[i] = ok ? *reinterpret_cast<const uint4*>(a.x + abase[i] + (long)u * a.Cin + c0) : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      rb[i] = *reinterpret_cast<const uint4*>(wb + (long)i * (THREADS / 8) * (a.Kw * a.Cin) + kk);
+  };
+  auto st_set = [&](__bf16* base, const uint4* ra, const uint4* rb) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) store_one(base, tid + i * THREADS, ra[i]);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) store_one(base + Cfg::A_EL, tid + i * THREADS, rb[i]);
+  };
+  auto mma = [&](const __bf16* As) {
+    const __bf16* Bs = As + Cfg::A_EL;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(As + (wr * WM + i * 16 + (lane & 15)) * LDS_ROW + ks * 32 +
+                                                 8 * (lane >> 4));
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (wc * WN + j * 16 + (lane & 15)) * LDS_ROW + ks * 32 +
+                                                  8 * (lane >> 4));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  __bf16* const L0 = lds;
+  __bf16* const L1 = lds + (NBUF == 2 ? Cfg::A_EL + Cfg::B_EL : 0);
+  if (nk > 0) {  // block-uniform (a phase without taps leaves acc = 0)
+    ld_set(ra0, rb0, 0);
+    st_set(L0, ra0, rb0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      ld_set(ra0, rb0, kt + 1);
+      if constexpr (NBUF == 2) {
+        mma((kt & 1) ? L1 : L0);
+        st_set((kt & 1) ? L0 : L1, ra0, rb0);
+      } else {
+        mma(L0);
+        __syncthreads();  // every wave is done reading the buffer
+        st_set(L0, ra0, rb0);
+      }
+      __syncthreads();
+    }
+  }
+  fwd_epilogue<BM, BN, EPI>(a, acc, smem, m0, n0, mt, MT, Lrow, M, P, ph);
+}
+
+// LDS-DMA main loop (forward and non-dilated data-grad): every 16-byte piece of the A (activation rows) and B
+// (weight rows) tiles goes global -> LDS with buffer_load ... lds (no register staging), two LDS stages, one
+// barrier per 64-deep K step.  LDS image per operand: [row][64 bf16] (128-byte rows, no padding); 16-byte chunk
+// cc of row r lives at chunk cc ^ ((r >> 1) & 7), so the 16 rows one ds_read_b128 lane group reads hit 16
+// distinct 16-byte slots of the 256-byte bank row.  The DMA writes lane-linear (lane l -> row l/8, chunk l%8 of
+// its 8-row piece), so the XOR is applied to the SOURCE chunk (MI355X guide rule 21).  Padding rows and the M
+// tail use an out-of-range buffer offset: the range check lands zeros.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned char* lds_piece) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_piece, 16, (int)voff, 0, 0,
+                                           0);
+}
+
+template <int BM, int BN, int EPI>
+__global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_dma_kernel(FwdArgs a, int MT, int NT) {
+  using Cfg = FwdCfg<BM, BN>;
+  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
+  constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
+  constexpr int AP = BM / 32, BP = BN / 32;  // 8-row DMA pieces per wave per stage
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int mt = wgid / NT, nt = wgid % NT;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int CB = a.Cin / BK, nk = a.Kw * CB, K = a.Kw * a.Cin;
+  const int M = a.B * a.Lout;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (long)a.B * a.Lin * a.Cin * 2);
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, (long)a.Cout * K * 2);
+  // this lane's rows: piece p = wv + 4*i covers tile rows 8p..8p+7; lane -> row 8p + lane/8, LDS chunk lane%8
+  unsigned abase[AP];
+  int apos[AP];
+#pragma unroll
+  for (int i = 0; i < AP; ++i) {
+    const int r = 8 * (wv + 4 * i) + (lane >> 3), m = m0 + r;
+    const int b = m / a.Lout, t = m - b * a.Lout;
+    const int cs = (lane & 7) ^ ((r >> 1) & 7);  // source chunk landing in this lane's LDS slot
+    abase[i] = (unsigned)(((long)b * a.Lin * a.Cin + cs * 8) * 2);
+    apos[i] = m < M ? t * a.stride - a.pad : INT_MIN / 2;
+  }
+  unsigned wbase[BP];
+#pragma unroll
+  for (int i = 0; i < BP; ++i) {
+    const int r = 8 * (wv + 4 * i) + (lane >> 3);
+    const int cs = (lane & 7) ^ ((r >> 1) & 7);
+    wbase[i] = (unsigned)(((long)(n0 + r) * K + cs * 8) * 2);
+  }
+  auto issue = [&](int kt, int st) {
+    const int k = kt / CB, c0 = (kt - k * CB) * BK;
+    unsigned char* As = smem + st * STAGE;
+#pragma unroll
+    for (int i = 0; i < AP; ++i) {
+      const int u = apos[i] + k;
+      const unsigned voff = (u >= 0 && u < a.Lin) ? abase[i] + (unsigned)((u * a.Cin + c0) * 2) : 0x7ffffff0u;
+      dma16(xr, voff, As + (wv + 4 * i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < BP; ++i) dma16(wrs, wbase[i] + (unsigned)((k * a.Cin + c0) * 2), As + A_BYTES + (wv + 4 * i) * 1024);
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](int st) {
+    const unsigned char* As = smem + st * STAGE;
+    const unsigned char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int cc = 4 * ks + (lane >> 4);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wr * WM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + r * 128 + ((cc ^ ((r >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = wc * WN + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + n * 128 + ((cc ^ ((n >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  if (nk > 0) {
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);  // lands during this step's MFMAs
+      mma(kt & 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next stage has landed (this wave's pieces) ...
+      __syncthreads();                                  // ... for every wave, and nobody reads stage kt any more
+    }
+  }
+  fwd_epilogue<BM, BN, EPI>(a, acc, smem, m0, n0, mt, MT, a.Lout, M, 1, 0);
+}
+
 // Tile choice: 128x128 when that still gives >= 2 workgroups per CU (256 CUs), else 128x64, else 64x64.
 inline void pick_fwd_tile(long M, int Cout, int* bm, int* bn) {
   const long mt128 = (M + 127) / 128;
@@ -354,6 +472,35 @@ inline int conv_nbuf() {
     nb = (e && atoi(e) == 2) ? 2 : 1;
   }
   return nb;
+}
+
+// ECG_CONV_DMA=0 selects the register-staged main loop for every conv (read once; default: LDS-DMA loop when
+// the input is not dilated).
+inline bool conv_dma() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ECG_CONV_DMA");
+    v = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return v == 1;
+}
+
+template <int BM, int BN, int EPI>
+int launch_fwd_dma(const FwdArgs& a, hipStream_t stream) {
+  using Cfg = FwdCfg<BM, BN>;
+  constexpr int STAGE_BYTES = 2 * (BM + BN) * 128;
+  constexpr int SMEM = STAGE_BYTES > Cfg::EP_BYTES ? STAGE_BYTES : Cfg::EP_BYTES;
+  static bool attr = false;
+  if (!attr) {
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_dma_kernel<BM, BN, EPI>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
+    attr = true;
+  }
+  const int MT = (int)(((long)a.B * a.Lout + BM - 1) / BM), NT = a.Cout / BN;
+  hipLaunchKernelGGL((conv1d_nlc_fwd_dma_kernel<BM, BN, EPI>), dim3((unsigned)(MT * NT)), dim3(THREADS), SMEM, stream,
+                     a, MT, NT);
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
 }
 
 template <int BM, int BN, int EPI, int NBUF>
@@ -384,6 +531,10 @@ int launch_fwd_cfg(const FwdArgs& a, hipStream_t stream) {
 
 template <int BM, int BN>
 int launch_fwd(const FwdArgs& a, hipStream_t stream) {
+  // the DMA loop addresses bytes with 32-bit buffer offsets
+  const bool dma_ok = a.in_dil == 1 && (long)a.B * a.Lin * a.Cin * 2 < 0x7fff0000L && (long)a.Cout * a.Kw * a.Cin * 2 < 0x7fff0000L;
+  if (conv_dma() && dma_ok)
+    return a.stat_mode == 1 ? launch_fwd_dma<BM, BN, 1>(a, stream) : launch_fwd_dma<BM, BN, 0>(a, stream);
   if (conv_nbuf() == 2)
     return a.stat_mode == 1 ? launch_fwd_cfg<BM, BN, 1, 2>(a, stream) : launch_fwd_cfg<BM, BN, 0, 2>(a, stream);
   return a.stat_mode == 1 ? launch_fwd_cfg<BM, BN, 1, 1>(a, stream) : launch_fwd_cfg<BM, BN, 0, 1>(a, stream);

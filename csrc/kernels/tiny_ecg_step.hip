@@ -903,6 +903,10 @@ __global__ __launch_bounds__(RED_COLS * RED_ROWG) void slab_reduce_sgd_kernel(
   __shared__ float part[RED_ROWG][RED_COLS + 1];
   const int cl = threadIdx.x % RED_COLS, rg = threadIdx.x / RED_COLS;
   const int col = blockIdx.x * RED_COLS + cl;
+  // the updating threads fetch their parameter / momentum before the slab reads: one round trip, not two
+  const bool upd = rg == 0 && col < P && apply;
+  const float p0 = upd ? params[col] : 0.f;
+  const float m0 = (upd && momentum != 0.f) ? mom[col] : 0.f;
   float s = 0.f;
   if (col <= P) {
     const float* base = slab + col;
@@ -927,10 +931,10 @@ __global__ __launch_bounds__(RED_COLS * RED_ROWG) void slab_reduce_sgd_kernel(
     } else {
       if (grad_out) grad_out[col] = gsum;
       if (apply) {
-        float p = params[col];
+        const float p = p0;
         float d = gsum + wd * p;
         if (momentum != 0.f) {
-          float bm = momentum * mom[col] + d;
+          const float bm = momentum * m0 + d;
           mom[col] = bm;
           d = nesterov ? d + momentum * bm : bm;
         }
