@@ -32,6 +32,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_fwd", [vp, vp, vp, vp] + [i32] * 10 + [vp])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad", [vp, vp, vp] + [i32] * 9 + [vp])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_tiles", [i32, i32, i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_set_big", [i32])
     lib._conv_mc_bound = True
 
 
@@ -39,6 +40,12 @@ def _lib_k():
     lib = _lib.kernels()
     _bind(lib)
     return lib
+
+
+def set_tile_family(big: int) -> int:
+    """Largest forward tile family of the LDS-DMA loop (0: 128-row tiles, 1: + 256x128, 2: + 256x256); returns the
+    previous one.  Step plans built before a change keep the tiling they were built with: set it first."""
+    return _lib_k().ecg_conv1d_nlc_set_big(int(big))
 
 
 def fwd_raw(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor], stride: int, pad: int,

@@ -358,8 +358,9 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned voff, u
                                            0);
 }
 
+// 256-row tiles (256x256: 128 KB of stages, 256 accumulator registers per lane) run one workgroup per CU.
 template <int BM, int BN, int EPI>
-__global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_dma_kernel(FwdArgs a, int MT, int NT) {
+__global__ __launch_bounds__(THREADS, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_dma_kernel(FwdArgs a, int MT, int NT) {
   using Cfg = FwdCfg<BM, BN>;
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
@@ -374,7 +375,11 @@ __global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_dma_kernel(FwdArgs 
   const int m0 = mt * BM, n0 = nt * BN;
   const int CB = a.Cin / BK, nk = a.Kw * CB, K = a.Kw * a.Cin;
   const int M = a.B * a.Lout;
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, (long)a.B * a.Lin * a.Cin * 2);
+  // The activation resource starts at the tile's first sample, so 32-bit offsets cover any batch size (the host
+  // checks that one tile's sample span fits); records are capped below the out-of-range padding offset.
+  const int b0 = m0 / a.Lout;
+  const long xrem = (long)(a.B - b0) * a.Lin * a.Cin * 2;
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + (long)b0 * a.Lin * a.Cin, xrem < 0x7fff0000L ? xrem : 0x7fff0000L);
   const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, (long)a.Cout * K * 2);
   // this lane's rows: piece p = wv + 4*i covers tile rows 8p..8p+7; lane -> row 8p + lane/8, LDS chunk lane%8
   unsigned abase[AP];
@@ -384,7 +389,7 @@ __global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_dma_kernel(FwdArgs 
     const int r = 8 * (wv + 4 * i) + (lane >> 3), m = m0 + r;
     const int b = m / a.Lout, t = m - b * a.Lout;
     const int cs = (lane & 7) ^ ((r >> 1) & 7);  // source chunk landing in this lane's LDS slot
-    abase[i] = (unsigned)(((long)b * a.Lin * a.Cin + cs * 8) * 2);
+    abase[i] = m < M ? (unsigned)(((long)(b - b0) * a.Lin * a.Cin + cs * 8) * 2) : 0u;
     apos[i] = m < M ? t * a.stride - a.pad : INT_MIN / 2;
   }
   unsigned wbase[BP];
@@ -449,10 +454,22 @@ __global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_fwd_dma_kernel(FwdArgs 
   fwd_epilogue<BM, BN, EPI>(a, acc, smem, m0, n0, mt, MT, a.Lout, M, 1, 0);
 }
 
-// Tile choice: 128x128 when that still gives >= 2 workgroups per CU (256 CUs), else 128x64, else 64x64.
-inline void pick_fwd_tile(long M, int Cout, int* bm, int* bn) {
-  const long mt128 = (M + 127) / 128;
-  if (Cout % 128 == 0 && mt128 * (Cout / 128) >= 512) {
+inline bool conv_dma();
+inline int conv_big();
+
+// Tile choice: with the LDS-DMA loop (undilated input) 256x256 / 256x128 when that gives >= 2 tiles per CU
+// (one workgroup per CU), else 128x128 when that still gives >= 2 workgroups per CU (256 CUs), else 128x64,
+// else 64x64.
+inline void pick_fwd_tile(long M, int Cout, int in_dil, int* bm, int* bn) {
+  const long mt128 = (M + 127) / 128, mt256 = (M + 255) / 256;
+  const int big = (in_dil == 1 && conv_dma()) ? conv_big() : 0;
+  if (big >= 2 && Cout % 256 == 0 && mt256 * (Cout / 256) >= 512) {
+    *bm = 256;
+    *bn = 256;
+  } else if (big >= 1 && Cout % 128 == 0 && mt256 * (Cout / 128) >= 512) {
+    *bm = 256;
+    *bn = 128;
+  } else if (Cout % 128 == 0 && mt128 * (Cout / 128) >= 512) {
     *bm = 128;
     *bn = 128;
   } else if (mt128 * (Cout / 64) >= 512) {
@@ -483,6 +500,17 @@ inline bool conv_dma() {
     v = (e && atoi(e) == 0) ? 0 : 1;
   }
   return v == 1;
+}
+
+// ECG_CONV_BIG=0|1|2: largest forward tile family (0: 128-row tiles only, 1: + 256x128, 2: + 256x256); read
+// once, overridable with ecg_conv1d_nlc_set_big (tests; plans built before a change keep their tiling).
+int g_conv_big = -1;
+inline int conv_big() {
+  if (g_conv_big < 0) {
+    const char* e = getenv("ECG_CONV_BIG");
+    g_conv_big = e ? atoi(e) : 0;
+  }
+  return g_conv_big;
 }
 
 template <int BM, int BN, int EPI>
@@ -531,13 +559,17 @@ int launch_fwd_cfg(const FwdArgs& a, hipStream_t stream) {
 
 template <int BM, int BN>
 int launch_fwd(const FwdArgs& a, hipStream_t stream) {
-  // the DMA loop addresses bytes with 32-bit buffer offsets
-  const bool dma_ok = a.in_dil == 1 && (long)a.B * a.Lin * a.Cin * 2 < 0x7fff0000L && (long)a.Cout * a.Kw * a.Cin * 2 < 0x7fff0000L;
+  // the DMA loop addresses bytes with 32-bit buffer offsets from the tile's first sample
+  const bool dma_ok = a.in_dil == 1 && (long)(BM / a.Lout + 2) * a.Lin * a.Cin * 2 < 0x7fff0000L &&
+                      (long)a.Cout * a.Kw * a.Cin * 2 < 0x7fff0000L;
   if (conv_dma() && dma_ok)
     return a.stat_mode == 1 ? launch_fwd_dma<BM, BN, 1>(a, stream) : launch_fwd_dma<BM, BN, 0>(a, stream);
-  if (conv_nbuf() == 2)
-    return a.stat_mode == 1 ? launch_fwd_cfg<BM, BN, 1, 2>(a, stream) : launch_fwd_cfg<BM, BN, 0, 2>(a, stream);
-  return a.stat_mode == 1 ? launch_fwd_cfg<BM, BN, 1, 1>(a, stream) : launch_fwd_cfg<BM, BN, 0, 1>(a, stream);
+  if constexpr (BM > 128) return ecg::kBadArg;  // 256-row tiles exist only as DMA kernels (the picker ensures it)
+  else {
+    if (conv_nbuf() == 2)
+      return a.stat_mode == 1 ? launch_fwd_cfg<BM, BN, 1, 2>(a, stream) : launch_fwd_cfg<BM, BN, 0, 2>(a, stream);
+    return a.stat_mode == 1 ? launch_fwd_cfg<BM, BN, 1, 1>(a, stream) : launch_fwd_cfg<BM, BN, 0, 1>(a, stream);
+  }
 }
 
 // ------------------------------------------------------------------------------------------- weight grad
@@ -770,23 +802,32 @@ ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bia
     a.srstd_d = static_cast<const float*>(bnb[6]);
   }
   int bm, bn;
-  pick_fwd_tile((long)B * Lout, Cout, &bm, &bn);
+  pick_fwd_tile((long)B * Lout, Cout, in_dil, &bm, &bn);
+  if (bm == 256 && bn == 256) return launch_fwd<256, 256>(a, stream);
+  if (bm == 256) return launch_fwd<256, 128>(a, stream);
   if (bm == 128 && bn == 128) return launch_fwd<128, 128>(a, stream);
   if (bm == 128) return launch_fwd<128, 64>(a, stream);
   return launch_fwd<64, 64>(a, stream);
 }
 
+// Select the forward tile family (see conv_big); returns the previous setting.
+ECG_API int ecg_conv1d_nlc_set_big(int big) {
+  const int prev = conv_big();
+  g_conv_big = big < 0 ? 0 : (big > 2 ? 2 : big);
+  return prev;
+}
+
 // Number of M tiles (rows of the BN-statistics partials) the forward kernel uses for this shape.
 ECG_API int ecg_conv1d_nlc_fwd_stat_tiles(long M, int Cout) {
   int bm, bn;
-  pick_fwd_tile(M, Cout, &bm, &bn);
+  pick_fwd_tile(M, Cout, 1, &bm, &bn);
   return (int)((M + bm - 1) / bm);
 }
 
 // Same for a call with batch B, output length Lout and input dilation in_dil (phase-decomposed data-grad).
 ECG_API int ecg_conv1d_nlc_fwd_stat_tiles_ex(int B, int Lout, int Cout, int in_dil) {
   int bm, bn;
-  pick_fwd_tile((long)B * Lout, Cout, &bm, &bn);
+  pick_fwd_tile((long)B * Lout, Cout, in_dil, &bm, &bn);
   if (in_dil <= 1) return (int)(((long)B * Lout + bm - 1) / bm);
   const int Lph = (Lout + in_dil - 1) / in_dil;
   return in_dil * (int)(((long)B * Lph + bm - 1) / bm);

@@ -52,6 +52,23 @@ def test_conv1d_nlc_forward_backward(B, L, Cin, Cout, K, s, p):
     assert _rel(b.grad, br.grad) < 1e-2
 
 
+BIG_CASES = [  # shapes that select the 256-row DMA tiles once the big-tile family is enabled
+    (2048, 64, 128, 256, 3, 1, 1),  # 256x256
+    (2100, 63, 128, 128, 3, 1, 1),  # 256x128, ragged last M tile
+    (1030, 128, 64, 512, 3, 1, 1),  # 256x256 (2 N tiles), ragged; dgrad on 256x64 -> 128-row tiles
+]
+
+
+@pytest.mark.parametrize("B,L,Cin,Cout,K,s,p", BIG_CASES)
+def test_conv1d_nlc_big_tiles(B, L, Cin, Cout, K, s, p):
+    from crossscale_ecg.ops.conv_mc import set_tile_family
+    prev = set_tile_family(2)
+    try:
+        test_conv1d_nlc_forward_backward(B, L, Cin, Cout, K, s, p)
+    finally:
+        set_tile_family(prev)
+
+
 def _grads(m, x, y, amp=False):
     m.zero_grad(set_to_none=True)
     with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
