@@ -43,8 +43,9 @@ def _lib_k():
 
 
 def set_tile_family(big: int) -> int:
-    """Largest forward tile family of the LDS-DMA loop (0: 128-row tiles, 1: + 256x128, 2: + 256x256); returns the
-    previous one.  Step plans built before a change keep the tiling they were built with: set it first."""
+    """256-row forward tiles of the LDS-DMA loop (0: 128-row tiles only, 1 (default): + 256x256, 2: + 256x128);
+    returns the previous setting.  Step plans built before a change keep the tiling they were built with: set it
+    first."""
     return _lib_k().ecg_conv1d_nlc_set_big(int(big))
 
 

@@ -86,13 +86,15 @@ __device__ __forceinline__ void store_one(__bf16* lds, int e, uint4 v) {
 // run on one XCD, so the A panel (the activations) is read from HBM once per XCD-L2.
 // Epilogue: accumulators -> LDS (fp32) -> row-major pass with 16-B loads/stores: + bias, + residual
 // (optionally ReLU-masked), ReLU, bf16 round, and per-channel BN partials of the rounded values.
-template <int BM, int BN>
+// NWR = waves along M (2 x NWR waves per workgroup, 64 * 2 * NWR threads); the register-staged kernel uses 2.
+template <int BM, int BN, int NWR = 2>
 struct FwdCfg {
-  static constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  static constexpr int NW = 2 * NWR, NTHR = 64 * NW;
+  static constexpr int WM = BM / NWR, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   static constexpr int NA = BM * 8 / THREADS, NB = BN * 8 / THREADS;
   static constexpr int A_EL = BM * LDS_ROW, B_EL = BN * LDS_ROW;
   static constexpr int EP_LD = WN + 4;
-  static constexpr int EP_BYTES = 4 * (WM / 2) * EP_LD * 4 + 2 * 3 * BN * 4;  // epilogue staged in two halves
+  static constexpr int EP_BYTES = NW * (WM / 2) * EP_LD * 4 + NWR * 3 * BN * 4;  // epilogue staged in two halves
   static constexpr int stage_bytes(int nbuf) { return nbuf * (A_EL + B_EL) * 2; }
   static constexpr int smem(int nbuf) { return stage_bytes(nbuf) > EP_BYTES ? stage_bytes(nbuf) : EP_BYTES; }
 };
@@ -101,10 +103,11 @@ struct FwdCfg {
 // of WM/2 rows) -> row-major pass with 8 channels per lane: + bias, + residual (optionally ReLU-masked), ReLU,
 // bf16 round, and the per-channel BatchNorm partials of the rounded values (stat_mode 0) or the BN-backward
 // partials (stat_mode 1).  The staging buffers must be dead (all waves past the main loop's last barrier).
-template <int BM, int BN, int EPI>
-__device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, f32x4 (&acc)[BM / 32][BN / 32], unsigned char* smem,
-                                             int m0, int n0, int mt, int MT, int Lrow, int M, int P, int ph) {
-  using Cfg = FwdCfg<BM, BN>;
+template <int BM, int BN, int EPI, int NWR = 2>
+__device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, f32x4 (&acc)[BM / NWR / 16][BN / 32],
+                                             unsigned char* smem, int m0, int n0, int mt, int MT, int Lrow, int M,
+                                             int P, int ph) {
+  using Cfg = FwdCfg<BM, BN, NWR>;
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1, wc = wv & 1;
@@ -210,7 +213,7 @@ __device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, f32x4 (&acc)[BM /
         s2[e] += __shfl_xor(s2[e], off);
         if (ds) s3[e] += __shfl_xor(s3[e], off);
       }
-    float* sred = reinterpret_cast<float*>(smem) + 4 * HR * EP_LD;  // [wr][stat][BN]
+    float* sred = reinterpret_cast<float*>(smem) + Cfg::NW * HR * EP_LD;  // [wr][stat][BN]
     if (lane < CG) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -220,9 +223,12 @@ __device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, f32x4 (&acc)[BM /
       }
     }
     __syncthreads();
-    for (int i = tid; i < NS * BN; i += THREADS) {
+    for (int i = tid; i < NS * BN; i += Cfg::NTHR) {
       const int st = i / BN, c = i % BN;
-      a.stats[((long)st * MT + mt) * a.Cout + n0 + c] = sred[st * BN + c] + sred[(3 + st) * BN + c];
+      float v = 0.f;
+#pragma unroll
+      for (int r = 0; r < NWR; ++r) v += sred[(3 * r + st) * BN + c];
+      a.stats[((long)st * MT + mt) * a.Cout + n0 + c] = v;
     }
   }
 }
@@ -358,13 +364,15 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned voff, u
                                            0);
 }
 
-// 256-row tiles (256x256: 128 KB of stages, 256 accumulator registers per lane) run one workgroup per CU.
-template <int BM, int BN, int EPI>
-__global__ __launch_bounds__(THREADS, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_dma_kernel(FwdArgs a, int MT, int NT) {
-  using Cfg = FwdCfg<BM, BN>;
-  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
+// NWR = waves along M: 2 -> 4 waves (2x2), 4 -> 8 waves (4x2, 2 per SIMD at one workgroup per CU).  256-row
+// tiles need one workgroup per CU (2 x 64 KB of stages at 256x256).
+template <int BM, int BN, int EPI, int NWR>
+__global__ __launch_bounds__(128 * NWR, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_dma_kernel(FwdArgs a, int MT, int NT) {
+  using Cfg = FwdCfg<BM, BN, NWR>;
+  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NW = Cfg::NW;
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
-  constexpr int AP = BM / 32, BP = BN / 32;  // 8-row DMA pieces per wave per stage
+  constexpr int AP = BM / (8 * NW), BP = BN / (8 * NW);  // 8-row DMA pieces per wave per stage
+  static_assert(AP * 8 * NW == BM && BP * 8 * NW == BN, "tile rows must split into 8-row pieces over the waves");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1, wc = wv & 1;
@@ -386,7 +394,7 @@ __global__ __launch_bounds__(THREADS, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_dma
   int apos[AP];
 #pragma unroll
   for (int i = 0; i < AP; ++i) {
-    const int r = 8 * (wv + 4 * i) + (lane >> 3), m = m0 + r;
+    const int r = 8 * (wv + NW * i) + (lane >> 3), m = m0 + r;
     const int b = m / a.Lout, t = m - b * a.Lout;
     const int cs = (lane & 7) ^ ((r >> 1) & 7);  // source chunk landing in this lane's LDS slot
     abase[i] = m < M ? (unsigned)(((long)(b - b0) * a.Lin * a.Cin + cs * 8) * 2) : 0u;
@@ -395,7 +403,7 @@ __global__ __launch_bounds__(THREADS, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_dma
   unsigned wbase[BP];
 #pragma unroll
   for (int i = 0; i < BP; ++i) {
-    const int r = 8 * (wv + 4 * i) + (lane >> 3);
+    const int r = 8 * (wv + NW * i) + (lane >> 3);
     const int cs = (lane & 7) ^ ((r >> 1) & 7);
     wbase[i] = (unsigned)(((long)(n0 + r) * K + cs * 8) * 2);
   }
@@ -406,10 +414,11 @@ __global__ __launch_bounds__(THREADS, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_dma
     for (int i = 0; i < AP; ++i) {
       const int u = apos[i] + k;
       const unsigned voff = (u >= 0 && u < a.Lin) ? abase[i] + (unsigned)((u * a.Cin + c0) * 2) : 0x7ffffff0u;
-      dma16(xr, voff, As + (wv + 4 * i) * 1024);
+      dma16(xr, voff, As + (wv + NW * i) * 1024);
     }
 #pragma unroll
-    for (int i = 0; i < BP; ++i) dma16(wrs, wbase[i] + (unsigned)((k * a.Cin + c0) * 2), As + A_BYTES + (wv + 4 * i) * 1024);
+    for (int i = 0; i < BP; ++i)
+      dma16(wrs, wbase[i] + (unsigned)((k * a.Cin + c0) * 2), As + A_BYTES + (wv + NW * i) * 1024);
   };
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -451,22 +460,23 @@ __global__ __launch_bounds__(THREADS, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_dma
       __syncthreads();                                  // ... for every wave, and nobody reads stage kt any more
     }
   }
-  fwd_epilogue<BM, BN, EPI>(a, acc, smem, m0, n0, mt, MT, a.Lout, M, 1, 0);
+  fwd_epilogue<BM, BN, EPI, NWR>(a, acc, smem, m0, n0, mt, MT, a.Lout, M, 1, 0);
 }
 
 inline bool conv_dma();
 inline int conv_big();
 
-// Tile choice: with the LDS-DMA loop (undilated input) 256x256 / 256x128 when that gives >= 2 tiles per CU
-// (one workgroup per CU), else 128x128 when that still gives >= 2 workgroups per CU (256 CUs), else 128x64,
+// Tile choice: with the LDS-DMA loop (undilated input) 256x256 (8 waves of 64x128) when that gives >= 2 tiles
+// per CU (one workgroup per CU; half the L2->LDS bytes per MAC of 128x128: 1.04 vs 0.87 PF/s on the
+// ResNet layer4 shape, profiles/r1_resnet/cmb_p3_big*.log), [256x128 opt-in: measured slower], else 128x128 when that still gives >= 2 workgroups per CU (256 CUs), else 128x64,
 // else 64x64.
 inline void pick_fwd_tile(long M, int Cout, int in_dil, int* bm, int* bn) {
   const long mt128 = (M + 127) / 128, mt256 = (M + 255) / 256;
   const int big = (in_dil == 1 && conv_dma()) ? conv_big() : 0;
-  if (big >= 2 && Cout % 256 == 0 && mt256 * (Cout / 256) >= 512) {
+  if (big >= 1 && Cout % 256 == 0 && mt256 * (Cout / 256) >= 512) {
     *bm = 256;
     *bn = 256;
-  } else if (big >= 1 && Cout % 128 == 0 && mt256 * (Cout / 128) >= 512) {
+  } else if (big >= 2 && Cout % 128 == 0 && mt256 * (Cout / 128) >= 512) {
     *bm = 256;
     *bn = 128;
   } else if (Cout % 128 == 0 && mt128 * (Cout / 128) >= 512) {
@@ -502,31 +512,33 @@ inline bool conv_dma() {
   return v == 1;
 }
 
-// ECG_CONV_BIG=0|1|2: largest forward tile family (0: 128-row tiles only, 1: + 256x128, 2: + 256x256); read
+// ECG_CONV_BIG=0|1|2: 256-row forward tiles (0: 128-row tiles only, 1 (default): + 256x256, 2: + 256x128); read
 // once, overridable with ecg_conv1d_nlc_set_big (tests; plans built before a change keep their tiling).
 int g_conv_big = -1;
 inline int conv_big() {
   if (g_conv_big < 0) {
     const char* e = getenv("ECG_CONV_BIG");
-    g_conv_big = e ? atoi(e) : 0;
+    g_conv_big = e ? atoi(e) : 1;
   }
   return g_conv_big;
 }
 
 template <int BM, int BN, int EPI>
 int launch_fwd_dma(const FwdArgs& a, hipStream_t stream) {
-  using Cfg = FwdCfg<BM, BN>;
+  constexpr int NWR = BM >= 256 ? 4 : 2;  // 256-row tiles: 8 waves of 64 x BN/2
+  using Cfg = FwdCfg<BM, BN, NWR>;
   constexpr int STAGE_BYTES = 2 * (BM + BN) * 128;
   constexpr int SMEM = STAGE_BYTES > Cfg::EP_BYTES ? STAGE_BYTES : Cfg::EP_BYTES;
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
   static bool attr = false;
   if (!attr) {
-    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_dma_kernel<BM, BN, EPI>,
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_dma_kernel<BM, BN, EPI, NWR>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
     attr = true;
   }
   const int MT = (int)(((long)a.B * a.Lout + BM - 1) / BM), NT = a.Cout / BN;
-  hipLaunchKernelGGL((conv1d_nlc_fwd_dma_kernel<BM, BN, EPI>), dim3((unsigned)(MT * NT)), dim3(THREADS), SMEM, stream,
-                     a, MT, NT);
+  hipLaunchKernelGGL((conv1d_nlc_fwd_dma_kernel<BM, BN, EPI, NWR>), dim3((unsigned)(MT * NT)), dim3(Cfg::NTHR), SMEM,
+                     stream, a, MT, NT);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
