@@ -32,6 +32,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_fwd", [vp, vp, vp, vp] + [i32] * 10 + [vp])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad", [vp, vp, vp] + [i32] * 9 + [vp])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_tiles", [i32, i32, i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_wgrad_target_wgs", [i32, i32, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_set_big", [i32])
     lib._conv_mc_bound = True
 
@@ -77,8 +78,9 @@ def wgrad_raw(dy: torch.Tensor, x: torch.Tensor, K: int, stride: int, pad: int,
     chunks = (R + 63) // 64
     lib = _lib_k()
     tiles = lib.ecg_conv1d_nlc_wgrad_tiles(Cout, K, Cin)
-    if splits is None:  # ~4 workgroups per CU, >= 8 row chunks per workgroup, <= 256 partial slices
-        splits = max(1, min(256, max(1, chunks // 8), max(1, 1024 // max(1, tiles))))
+    if splits is None:  # target workgroup count, >= 8 row chunks per workgroup, <= 256 partial slices
+        target = lib.ecg_conv1d_nlc_wgrad_target_wgs(Cout, K, Cin)
+        splits = max(1, min(256, max(1, chunks // 8), max(1, target // max(1, tiles))))
     part = torch.empty((splits, Cout, K * Cin), dtype=torch.float32, device=dy.device)
     st = _lib_k().ecg_conv1d_nlc_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr(), splits, B, Lin, Cin, Lout, Cout, K,
                                        stride, pad, _lib.stream_ptr(dy.device))

@@ -49,6 +49,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_plan_stem_rows", [])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles", [ctypes.c_long, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_tiles", [i32, i32, i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_wgrad_target_wgs", [i32, i32, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles_ex", [i32, i32, i32, i32])
     lib._plan_bound = True
     if lib.ecg_plan_op_words() != OP_WORDS or lib.ecg_plan_wentry_bytes() != 40:
@@ -187,10 +188,12 @@ class ResNetStepEngine:
 
         # ---- wgrad split plan + workspace
         def wsplits(R, Cout, K, Cin):
-            # ~1024 workgroups, >= 8 row chunks each, <= 256 partial slices (the reduce reads S x |dW|)
+            # the kernel's target workgroup count, >= 8 row chunks each, <= 256 partial slices (the reduce reads
+            # S x |dW|)
             chunks = (R + 63) // 64
             tiles = self.lib.ecg_conv1d_nlc_wgrad_tiles(Cout, K, Cin)
-            return max(1, min(256, max(1, chunks // 8), max(1, 1024 // tiles)))
+            target = self.lib.ecg_conv1d_nlc_wgrad_target_wgs(Cout, K, Cin)
+            return max(1, min(256, max(1, chunks // 8), max(1, target // tiles)))
 
         ws_need = 0
         for (Li, Ci, Lo, Co, s), blk in zip(shapes, blocks):

@@ -512,7 +512,8 @@ inline bool conv_dma() {
   return v == 1;
 }
 
-// ECG_CONV_BIG=0|1|2: 256-row forward tiles (0: 128-row tiles only, 1 (default): + 256x256, 2: + 256x128); read
+// ECG_CONV_BIG=0|1|2: 256-row tiles (0: 128-row tiles only, 1 (default): + 256x256 forward, 2: + 256x128 forward
+// and 256x256 weight-gradient); read
 // once, overridable with ecg_conv1d_nlc_set_big (tests; plans built before a change keep their tiling).
 int g_conv_big = -1;
 inline int conv_big() {
@@ -620,15 +621,18 @@ __device__ __forceinline__ s16x4 tr16(const __bf16* p) {
 // loads are in flight during this chunk's MFMAs) into ONE LDS buffer (two barriers per chunk), which keeps
 // three workgroups resident per CU; 1-D grid, split-major so the workgroups on one XCD share the same
 // activation rows; partial tiles leave through an LDS-staged float4 epilogue.
-template <int BM, int BN>
+// NWR = waves along C_out (2 x NWR waves): 2 for the 128/64 tiles (3 workgroups / CU), 4 for 256x256 (8 waves of
+// 64 x 128, one workgroup / CU, half the L2->LDS bytes per MAC).
+template <int BM, int BN, int NWR = 2>
 struct WgCfg {
-  static constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-  static constexpr int ROW_A = BM + 4, ROW_B = BN + 4;  // bf16 per LDS row (8-B aligned tr reads)
-  static constexpr int NA = BM / 32, NB = BN / 32;      // 16-B loads per thread per chunk
+  static constexpr int NW = 2 * NWR, NTHR = 64 * NW;
+  static constexpr int WM = BM / NWR, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  static constexpr int ROW_A = BM + 4, ROW_B = BN + 4;     // bf16 per LDS row (8-B aligned tr reads)
+  static constexpr int NA = 8 * BM / NTHR, NB = 8 * BN / NTHR;  // 16-B loads per thread per chunk
   static constexpr int A_EL = 64 * ROW_A, B_EL = 64 * ROW_B;
-  static constexpr int STAGE_BYTES = (A_EL + B_EL) * 2;  // one buffer (two barriers per chunk): 3 WGs / CU
+  static constexpr int STAGE_BYTES = (A_EL + B_EL) * 2;  // one buffer (two barriers per chunk)
   static constexpr int EP_LD = WN + 4;
-  static constexpr int EP_BYTES = 4 * (WM / 2) * EP_LD * 4;  // epilogue staged in two halves
+  static constexpr int EP_BYTES = NW * (WM / 2) * EP_LD * 4;  // epilogue staged in two halves
   static constexpr int SMEM = STAGE_BYTES > EP_BYTES ? STAGE_BYTES : EP_BYTES;
 };
 
@@ -637,10 +641,12 @@ __device__ __forceinline__ void st_split(__bf16* p, uint4 v) {  // 8-B aligned 1
   *reinterpret_cast<uint2*>(p + 4) = make_uint2(v.z, v.w);
 }
 
-template <int BM, int BN>
-__global__ __launch_bounds__(THREADS, 3) void conv1d_nlc_wgrad_kernel(WgradArgs a, int TM, int TN, int splits) {
-  using Cfg = WgCfg<BM, BN>;
+template <int BM, int BN, int NWR>
+__global__ __launch_bounds__(128 * NWR, NWR == 2 ? 3 : 1) void conv1d_nlc_wgrad_kernel(WgradArgs a, int TM, int TN,
+                                                                                       int splits) {
+  using Cfg = WgCfg<BM, BN, NWR>;
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NA = Cfg::NA, NB = Cfg::NB;
+  constexpr int THREADS = Cfg::NTHR;  // shadows the 4-wave default
   constexpr int ROW_A = Cfg::ROW_A, ROW_B = Cfg::ROW_B;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __bf16* const lds = reinterpret_cast<__bf16*>(smem);
@@ -771,19 +777,26 @@ __global__ __launch_bounds__(THREADS, 3) void conv1d_nlc_wgrad_kernel(WgradArgs 
 
 template <int BM, int BN>
 int launch_wgrad(const WgradArgs& a, int splits, hipStream_t stream) {
-  using Cfg = WgCfg<BM, BN>;
+  constexpr int NWR = BM >= 256 ? 4 : 2;
+  using Cfg = WgCfg<BM, BN, NWR>;
+  static_assert(Cfg::SMEM <= 160 * 1024, "LDS budget");
   static bool attr = false;
   if (!attr) {
-    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_wgrad_kernel<BM, BN>,
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_wgrad_kernel<BM, BN, NWR>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, Cfg::SMEM));
     attr = true;
   }
   const int TM = a.Cout / BM, TN = a.Kw * a.Cin / BN;
-  hipLaunchKernelGGL((conv1d_nlc_wgrad_kernel<BM, BN>), dim3((unsigned)(TM * TN * splits)), dim3(THREADS),
+  hipLaunchKernelGGL((conv1d_nlc_wgrad_kernel<BM, BN, NWR>), dim3((unsigned)(TM * TN * splits)), dim3(Cfg::NTHR),
                      Cfg::SMEM, stream, a, TM, TN, splits);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
+
+// 256x256 weight-gradient tiles (opt-in, ECG_CONV_BIG >= 2, both channel counts multiples of 256): measured
+// -6 %..+6 % against 128x128 on the ResNet shapes (profiles/r1_resnet/cmb_p4_big*.log) - the register-staged
+// single-buffer loop, not the L2->LDS traffic, bounds this kernel.
+inline bool wgrad_big(int Cout, int Cin) { return conv_big() >= 2 && Cout % 256 == 0 && Cin % 256 == 0; }
 
 }  // namespace
 
@@ -864,6 +877,7 @@ ECG_API int ecg_conv1d_nlc_wgrad(const void* dy, const void* x, float* part, int
   WgradArgs a{static_cast<const __bf16*>(dy), static_cast<const __bf16*>(x), part, B, Lin, Cin, Lout, Cout, Kw,
               stride, pad, cps, make_fastdiv(Lout)};
   const bool bm128 = Cout % 128 == 0, bn128 = Cin % 128 == 0;
+  if (wgrad_big(Cout, Cin)) return launch_wgrad<256, 256>(a, splits, stream);
   if (bm128 && bn128) return launch_wgrad<128, 128>(a, splits, stream);
   if (bm128) return launch_wgrad<128, 64>(a, splits, stream);
   if (bn128) return launch_wgrad<64, 128>(a, splits, stream);
@@ -872,6 +886,14 @@ ECG_API int ecg_conv1d_nlc_wgrad(const void* dy, const void* x, float* part, int
 
 // Workgroup tiles (C_out tiles x tap*C_in tiles) the weight-gradient kernel uses for this shape (split sizing).
 ECG_API int ecg_conv1d_nlc_wgrad_tiles(int Cout, int Kw, int Cin) {
-  const int bm = Cout % 128 == 0 ? 128 : 64, bn = Cin % 128 == 0 ? 128 : 64;
+  const bool big = wgrad_big(Cout, Cin);
+  const int bm = big ? 256 : (Cout % 128 == 0 ? 128 : 64), bn = big ? 256 : (Cin % 128 == 0 ? 128 : 64);
   return (Cout / bm) * (Kw * Cin / bn);
+}
+
+// Workgroups the weight-gradient launch should aim for (tiles x splits): ~4 resident per CU for the 4-wave
+// tiles, ~2 rounds of one per CU for the 8-wave 256x256 tile.
+ECG_API int ecg_conv1d_nlc_wgrad_target_wgs(int Cout, int Kw, int Cin) {
+  (void)Kw;
+  return wgrad_big(Cout, Cin) ? 512 : 1024;
 }
