@@ -78,6 +78,7 @@ def _bind_kernels(lib: C.CDLL) -> None:
                                        vp, i32, vp, vp])
     _sig(lib, "ecg_round_graph_create_persistent", [C.POINTER(vp), vp, i32, i64, vp, vp, vp, vp, i32, i32, i32, vp,
                                                     f32, f32, f32, i32, vp, i64, vp, i32])
+    _sig(lib, "ecg_tiny_force_waves", [i32])
     _sig(lib, "ecg_tiny_ctl_ints", [])
     _sig(lib, "ecg_tiny_gslab_rows", [])
     _sig(lib, "ecg_tiny_set_stamps", [vp])

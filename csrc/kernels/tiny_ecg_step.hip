@@ -1190,19 +1190,21 @@ constexpr int kMaxLds = 160 * 1024;
 
 // 16 waves (one tile pair each at L=500) when the per-wave partial slots fit in LDS, else 8.
 // ECG_TINY_WAVES=8|16 overrides (tuning); the choice never changes results beyond fp32 summation order.
-// bf16: 8 waves measured fastest at L=500 (profiles/r1_fused_step_v3); fp32: 16 waves (4x more MFMA
-// instructions per tile on v_mfma_f32_16x16x4_f32, so the extra waves pay).
+// Both precisions take 16 waves once there are >= 16 time tiles: bf16 12.57 vs 12.73 us/step at L=500 with the
+// MFMA conv1 (profiles/r1_round_kernel/ab_waves.log; 8 waves had been faster before conv1 moved to MFMA), fp32
+// has 4x more MFMA instructions per tile on v_mfma_f32_16x16x4_f32.
+int g_forced_waves = -1;  // ECG_TINY_WAVES, or ecg_tiny_force_waves (tests)
 int pick_waves(int L, bool f32) {
   const int Lp = (L + 31) / 32 * 32;
-  static int forced = -1;
-  if (forced < 0) {
+  if (g_forced_waves < 0) {
     const char* e = getenv("ECG_TINY_WAVES");
-    forced = e ? atoi(e) : 0;
+    g_forced_waves = e ? atoi(e) : 0;
   }
+  const int forced = g_forced_waves;
   const bool fit16 = Lp <= 32 * 4 * 16 && make_smem(L, 16, MAX_CLASSES, f32).bytes <= kMaxLds;
   if (forced == 16 && fit16) return 16;
   if (forced == 8) return 8;
-  return (f32 && fit16 && Lp / 32 >= 16) ? 16 : 8;
+  return (fit16 && Lp / 32 >= 16) ? 16 : 8;
 }
 
 int check_step_args(int L, int nc, int B, int out_stride, int mode, bool f32 = false) {
@@ -1281,9 +1283,13 @@ bool round_fits_cfg(int L, int nc, int G) {
   return per_cu >= 1 && G <= cus;
 }
 
+// The persistent round keeps 8 waves in bf16 (14.0 vs 18.5 us/step at 16: its per-step hand-offs are spun on
+// by every wave, profiles/r1_round_kernel/diag_*).
+int round_waves(int L, bool f32) { return f32 ? pick_waves(L, true) : 8; }
+
 bool round_fits(int L, int nc, int G, bool f32) {
   if (check_step_args(L, nc, G, make_layout(nc).P + 1, 0, f32) != ecg::kOk) return false;
-  const int waves = pick_waves(L, f32);
+  const int waves = round_waves(L, f32);
   if (f32) return waves == 8 ? round_fits_cfg<8, true>(L, nc, G) : round_fits_cfg<16, true>(L, nc, G);
   return waves == 8 ? round_fits_cfg<8, false>(L, nc, G) : round_fits_cfg<16, false>(L, nc, G);
 }
@@ -1305,7 +1311,7 @@ int round_dispatch(const RoundArgs& a, void* ws, long ws_bytes, int prec, hipStr
     return ecg::kBadArg;
   if (ws_bytes < round_ws_bytes(a.nc, a.G) || !round_fits(a.L, a.nc, a.G, prec == 1)) return ecg::kBadArg;
   ECG_HIP_CHECK(hipMemsetAsync(ws, 0, round_ws_bytes(a.nc, a.G), stream));
-  const int waves = pick_waves(a.L, prec == 1);
+  const int waves = round_waves(a.L, prec == 1);
   if (prec == 1) return waves == 8 ? launch_round_cfg<8, true>(a, stream) : launch_round_cfg<16, true>(a, stream);
   return waves == 8 ? launch_round_cfg<8, false>(a, stream) : launch_round_cfg<16, false>(a, stream);
 }
@@ -1355,6 +1361,15 @@ ECG_API int ecg_tiny_param_count(int nc) { return make_layout(nc).P; }
 ECG_API int ecg_tiny_set_stamps(unsigned long long* stamps) {
   g_stamps = stamps;
   return ecg::kOk;
+}
+
+// Force the per-step kernel's wave count (8 or 16; 0 = automatic); returns the previous setting.  Tests use it
+// to compare paths at the same per-sample summation order.  Graphs captured before a change keep their kernel.
+ECG_API int ecg_tiny_force_waves(int waves) {
+  pick_waves(32, false);  // resolve the environment default first
+  const int prev = g_forced_waves;
+  g_forced_waves = (waves == 8 || waves == 16) ? waves : 0;
+  return prev;
 }
 
 ECG_API int ecg_tiny_smem_bytes(int L, int prec) {

@@ -56,6 +56,7 @@ BIG_CASES = [  # shapes that select the 256-row DMA tiles once the big-tile fami
     (2048, 64, 128, 256, 3, 1, 1),  # 256x256
     (2100, 63, 128, 128, 3, 1, 1),  # 256x128, ragged last M tile
     (1030, 128, 64, 512, 3, 1, 1),  # 256x256 (2 N tiles), ragged; dgrad on 256x64 -> 128-row tiles
+    (64, 32, 256, 256, 3, 1, 1),  # 256x256 weight-grad (family 2)
 ]
 
 

@@ -184,17 +184,24 @@ def test_persistent_round_matches_two_launch(B, precision):
     """One persistent launch per round (granule hand-offs, column-slice owners apply SGD) == two launches per
     step: every owner sums its columns in the slab-reduce kernel's order, so weights, momentum and loss agree
     bit for bit, over several rounds (the granule tags are re-zeroed before every launch)."""
+    from crossscale_ecg.ops import _lib
     from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
     dev, x, y, model, _ = _setup(B=B, N=max(4 * B, 64))
     m2 = TinyECG().to(dev)
     m2.load_state_dict(model.state_dict())
-    a = FusedTinyTrainer(model, x, y, B, 6, seed=3, use_graph=True, persistent=True, precision=precision)
-    b = FusedTinyTrainer(m2, x, y, B, 6, seed=3, use_graph=False, persistent=False, precision=precision)
-    assert a.persistent and not b.persistent
-    for _ in range(3):
-        a.run_round()
-        b.run_round()
-    torch.cuda.synchronize()
+    lib = _lib.kernels()
+    # the per-step kernel at the persistent kernel's wave count (bf16: 8), so per-sample sums match bit for bit
+    prev = lib.ecg_tiny_force_waves(8 if precision == "bf16" else 0)
+    try:
+        a = FusedTinyTrainer(model, x, y, B, 6, seed=3, use_graph=True, persistent=True, precision=precision)
+        b = FusedTinyTrainer(m2, x, y, B, 6, seed=3, use_graph=False, persistent=False, precision=precision)
+        assert a.persistent and not b.persistent
+        for _ in range(3):
+            a.run_round()
+            b.run_round()
+        torch.cuda.synchronize()
+    finally:
+        lib.ecg_tiny_force_waves(prev)
     a.check_status()
     assert torch.equal(a.params, b.params), (a.params - b.params).abs().max()
     assert torch.equal(a.mom, b.mom), (a.mom - b.mom).abs().max()
