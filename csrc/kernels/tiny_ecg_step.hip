@@ -748,7 +748,9 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
 #define ECG_STAMP(k) \
   if (stamps && tid == 0) stamps[(long)b * 16 + 7 * rep + (k)] = __builtin_amdgcn_s_memtime();
     ECG_STAMP(0)
-    // phase 0: stage params + x into LDS, zero pads
+    // phase 0: stage params + x into LDS, zero pads.  (Measured: pre-gathering a round's windows into contiguous
+    // buffers inside the round graph, to drop the dependent idx -> row load, costs more than it saves:
+    // 12.98 vs 12.52 us/step, profiles/r1_round_kernel/ab_pregather.log.)
     int ylab = 0;
     {
       const long row = idx ? (long)idx[b] : (long)b;
