@@ -31,9 +31,45 @@ def _as_2d(x: torch.Tensor) -> torch.Tensor:
     return x.contiguous()
 
 
+_HIP_FNS = {}  # dtype -> bound C function (after the first call)
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
+def _conv1d_hip_fast(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None) -> torch.Tensor | None:
+    """Per-call fast path of the hip backend (the Module-2 benchmark times single calls, so Python overhead is
+    part of the measured number, as the torch side's dispatch is part of its): no intermediate tensors, one
+    raw-stream query.  Returns None when the operands need the general path (conversions, copies, checks)."""
+    d = x.dim()
+    if (_raw_stream is None or not x.is_cuda or not x.is_contiguous() or (d == 3 and x.shape[1] != 1)
+            or d not in (2, 3) or w.dtype != torch.float32 or not w.is_contiguous() or w.device != x.device):
+        return None
+    if not _HIP_FNS:
+        lib = _lib.kernels()  # raises if the HIP library is missing: no silent fallback on a GPU tensor
+        _HIP_FNS.update({torch.float32: lib.conv1d_batch_hip, torch.bfloat16: lib.conv1d_batch_hip_bf16})
+    fn = _HIP_FNS.get(x.dtype)
+    if fn is None:
+        return None
+    B, L, K = x.shape[0], x.shape[-1], w.numel()
+    outL = L - K + 1
+    if K < 1 or outL < 1:
+        return None
+    if out is None:
+        out = torch.empty((B, 1, outL) if d == 3 else (B, outL), dtype=x.dtype, device=x.device)
+    elif out.dtype != x.dtype or out.numel() != B * outL or not out.is_contiguous() or out.device != x.device:
+        return None
+    st = fn(x.data_ptr(), w.data_ptr(), out.data_ptr(), B, L, K, _raw_stream(x.device.index))
+    if st:
+        _lib.check(st, "conv1d_batch_hip")
+    return out if out.dim() == d else out.view((B, 1, outL) if d == 3 else (B, outL))
+
+
 def conv1d_valid(x: torch.Tensor, w: torch.Tensor, backend: str = "auto", out: torch.Tensor | None = None,
                  nthreads: int | None = None) -> torch.Tensor:
     """y[b, i] = sum_k x[b, i+k] w[k] for x [B, L] (or [B,1,L]), w [K] -> y [B, L-K+1] (same rank as x)."""
+    if backend == "hip" or (backend == "auto" and x.is_cuda):
+        y = _conv1d_hip_fast(x, w, out)
+        if y is not None:
+            return y
     keep3 = x.dim() == 3
     x2 = _as_2d(x)
     w1 = w.reshape(-1).contiguous()
