@@ -641,6 +641,40 @@ __device__ __forceinline__ void st_split(__bf16* p, uint4 v) {  // 8-B aligned 1
   *reinterpret_cast<uint2*>(p + 4) = make_uint2(v.z, v.w);
 }
 
+// Weight-gradient epilogue shared by both main loops: partial[split][co][n] through an LDS fp32 image (two halves
+// of WM/2 rows per wave), float4 row stores.  Starts with a barrier: the main loop's LDS may still be read.
+template <int BM, int BN, int NWR>
+__device__ __forceinline__ void wgrad_epilogue(const WgradArgs& a, f32x4 (&acc)[BM / NWR / 16][BN / 32],
+                                               unsigned char* smem, int split, int co0, int n0) {
+  using Cfg = WgCfg<BM, BN, NWR>;
+  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  constexpr int EP_LD = Cfg::EP_LD, HR = WM / 2;
+  float* ep = reinterpret_cast<float*>(smem) + wv * HR * EP_LD;
+  constexpr int C4 = WN / 4, RSTEP = 64 / C4;
+  const int c4 = lane % C4, rs = lane / C4;
+  const long N = (long)a.Kw * a.Cin;
+  float* out = a.part + (long)split * a.Cout * N;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();  // main loop / previous half done with the LDS
+#pragma unroll
+    for (int i = 0; i < FM / 2; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+          ep[(i * 16 + 4 * (lane >> 4) + qq) * EP_LD + j * 16 + (lane & 15)] = acc[h * (FM / 2) + i][j][qq];
+    __syncthreads();
+#pragma unroll 4
+    for (int r = rs; r < HR; r += RSTEP) {
+      const float4 v = *reinterpret_cast<const float4*>(ep + r * EP_LD + c4 * 4);
+      *reinterpret_cast<float4*>(out + (long)(co0 + wr * WM + h * HR + r) * N + n0 + wc * WN + c4 * 4) = v;
+    }
+  }
+}
+
 template <int BM, int BN, int NWR>
 __global__ __launch_bounds__(128 * NWR, NWR == 2 ? 3 : 1) void conv1d_nlc_wgrad_kernel(WgradArgs a, int TM, int TN,
                                                                                        int splits) {
@@ -749,30 +783,129 @@ __global__ __launch_bounds__(128 * NWR, NWR == 2 ? 3 : 1) void conv1d_nlc_wgrad_
       __syncthreads();
     }
   }
-  // epilogue: partial[split][co][n] through an LDS fp32 image, float4 row stores
-  constexpr int EP_LD = Cfg::EP_LD, HR = WM / 2;
-  float* ep = reinterpret_cast<float*>(smem) + wv * HR * EP_LD;
-  constexpr int C4 = WN / 4, RSTEP = 64 / C4;
-  const int c4 = lane % C4, rs = lane / C4;
-  const long N = (long)a.Kw * a.Cin;
-  float* out = a.part + (long)split * a.Cout * N;
+  wgrad_epilogue<BM, BN, NWR>(a, acc, smem, split, co0, n0);
+}
+
+// LDS-DMA weight-gradient main loop (128x128 tiles, 4 waves): both 64-row operand images go global -> LDS with
+// buffer_load ... lds (no VGPR staging: the register-staged loop spends more LDS cycles on its ds_write_b64
+// stores than on the MFMA operand reads), two stages, one barrier per 64-row chunk.  Images are dense
+// [r][128] bf16 (256-B rows); 16-B chunk c of row r is stored at chunk c ^ swz(r), swz(r) = 2 * ((r & 3) |
+// ((r >> 3) & 1) << 2), so the 8 rows {q, 8+q} x 32 B one 32-lane ds_read_b64_tr_b16 group touches land on 16
+// distinct 16-B slots of the 256-B bank row.  The DMA writes lane-linear, so the XOR is applied to the SOURCE
+// chunk.  Rows past R and out-of-range taps use an out-of-range buffer offset (zeros land).  Resources are
+// rebased at the split's first row / sample: 32-bit offsets cover any batch (the host checks the span).
+__device__ __forceinline__ int wg_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+
+template <int BM, int BN>
+__global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_wgrad_dma_kernel(WgradArgs a, int TM, int TN, int splits) {
+  static_assert(BM == 128 && BN == 128, "the swizzle needs >= 16 chunks per row");
+  constexpr int NWR = 2;
+  using Cfg = WgCfg<BM, BN, NWR>;
+  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
+  constexpr int RA = BM * 2, RB = BN * 2;      // bytes per image row
+  constexpr int A_BYTES = 64 * RA, STAGE = 64 * (RA + RB);
+  constexpr int AP = A_BYTES / 1024 / 4, BP = 64 * RB / 1024 / 4;  // 1-KB DMA pieces per wave per stage
+  constexpr int RPP = 1024 / RA;                                   // rows per piece (4)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int tiles = TM * TN;
+  const int split = wgid / tiles, tile = wgid % tiles;
+  const int co0 = (tile / TN) * BM, n0 = (tile % TN) * BN;
+  const int k = n0 / a.Cin, c0 = n0 % a.Cin;  // the BN columns lie inside one tap
+  const int R = a.B * a.Lout;
+  const int nchunks = (R + 63) / 64;
+  const int ch0 = split * a.chunks_per_split;
+  const int ch1 = min(nchunks, ch0 + a.chunks_per_split);
+  f32x4 acc[FM][FN];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    __syncthreads();  // main loop / previous half done with the LDS
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int i = 0; i < FM / 2; ++i)
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (ch0 < ch1) {  // block-uniform
+    const int r0 = ch0 * 64, b0 = r0 / a.Lout;
+    const long dyrem = (long)(R - r0) * a.Cout * 2, xrem = (long)(a.B - b0) * a.Lin * a.Cin * 2;
+    const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy + (long)r0 * a.Cout, dyrem < 0x7fff0000L ? dyrem : 0x7fff0000L);
+    const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + (long)b0 * a.Lin * a.Cin, xrem < 0x7fff0000L ? xrem : 0x7fff0000L);
+    // this lane's image rows and source chunks (piece p = wv + 4*i covers rows RPP*p .. RPP*p + RPP-1)
+    int arow[AP], asrc[BP > AP ? BP : AP], brow[BP];
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
+    for (int i = 0; i < AP; ++i) {
+      arow[i] = RPP * (wv + 4 * i) + (lane >> 4);
+      asrc[i] = (lane & 15) ^ wg_swz(arow[i]);
+    }
 #pragma unroll
-        for (int qq = 0; qq < 4; ++qq)
-          ep[(i * 16 + 4 * (lane >> 4) + qq) * EP_LD + j * 16 + (lane & 15)] = acc[h * (FM / 2) + i][j][qq];
+    for (int i = 0; i < BP; ++i) brow[i] = RPP * (wv + 4 * i) + (lane >> 4);
+    auto issue = [&](int ch, int st) {
+      unsigned char* As = smem + st * STAGE;
+      const int rel = (ch - ch0) * 64;
+#pragma unroll
+      for (int i = 0; i < AP; ++i) {
+        const int r = rel + arow[i];
+        const unsigned voff = r0 + r < R ? (unsigned)(((long)r * a.Cout + co0 + asrc[i] * 8) * 2) : 0x7ffffff0u;
+        dma16(dyr, voff, As + (wv + 4 * i) * 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < BP; ++i) {
+        const int rg = r0 + rel + brow[i];
+        const int b = fdiv(rg, a.lout), t = rg - b * a.Lout;
+        const int u = t * a.stride + k - a.pad;
+        const int src = (lane & 15) ^ wg_swz(brow[i]);
+        const unsigned voff = (rg < R && u >= 0 && u < a.Lin)
+                                  ? (unsigned)((((long)(b - b0) * a.Lin + u) * a.Cin + c0 + src * 8) * 2)
+                                  : 0x7ffffff0u;
+        dma16(xr, voff, As + A_BYTES + (wv + 4 * i) * 1024);
+      }
+    };
+    const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4, h = lane >> 4;
+    auto tr_at = [&](const unsigned char* img, int RB_, int rr, int col) -> s16x4 {
+      return tr16(reinterpret_cast<const __bf16*>(img + rr * RB_ + ((((col >> 3) ^ wg_swz(rr))) << 4) +
+                                                  ((col & 7) << 1)));
+    };
+    auto mma = [&](int st) {
+      const unsigned char* As = smem + st * STAGE;
+      const unsigned char* Bs = As + A_BYTES;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {  // two 32-deep k-steps over r
+        typedef short s16x8v __attribute__((ext_vector_type(8)));
+        bf16x8 af[FM], bfr[FN];
+        const int rr = ks * 32 + 8 * h + q;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int col = wr * WM + i * 16 + p4;
+          const s16x4 lo = tr_at(As, RA, rr, col), hi = tr_at(As, RA, rr + 4, col);
+          s16x8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          af[i] = __builtin_bit_cast(bf16x8, v);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int col = wc * WN + j * 16 + p4;
+          const s16x4 lo = tr_at(Bs, RB, rr, col), hi = tr_at(Bs, RB, rr + 4, col);
+          s16x8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          bfr[j] = __builtin_bit_cast(bf16x8, v);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    };
+    issue(ch0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-#pragma unroll 4
-    for (int r = rs; r < HR; r += RSTEP) {
-      const float4 v = *reinterpret_cast<const float4*>(ep + r * EP_LD + c4 * 4);
-      *reinterpret_cast<float4*>(out + (long)(co0 + wr * WM + h * HR + r) * N + n0 + wc * WN + c4 * 4) = v;
+    for (int ch = ch0; ch < ch1; ++ch) {
+      const int st = (ch - ch0) & 1;
+      if (ch + 1 < ch1) issue(ch + 1, st ^ 1);  // lands during this chunk's MFMAs
+      mma(st);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
     }
   }
+  wgrad_epilogue<BM, BN, NWR>(a, acc, smem, split, co0, n0);
 }
 
 template <int BM, int BN>
@@ -789,6 +922,34 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t stream) {
   const int TM = a.Cout / BM, TN = a.Kw * a.Cin / BN;
   hipLaunchKernelGGL((conv1d_nlc_wgrad_kernel<BM, BN, NWR>), dim3((unsigned)(TM * TN * splits)), dim3(Cfg::NTHR),
                      Cfg::SMEM, stream, a, TM, TN, splits);
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
+}
+
+// ECG_WGRAD_DMA=0 selects the register-staged weight-gradient loop (read once; default: LDS-DMA for 128x128).
+inline bool wgrad_dma() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ECG_WGRAD_DMA");
+    v = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return v == 1;
+}
+
+template <int BM, int BN>
+int launch_wgrad_dma(const WgradArgs& a, int splits, hipStream_t stream) {
+  using Cfg = WgCfg<BM, BN, 2>;
+  constexpr int STAGES = 2 * 64 * (BM + BN) * 2;
+  constexpr int SMEM = STAGES > Cfg::EP_BYTES ? STAGES : Cfg::EP_BYTES;
+  static bool attr = false;
+  if (!attr) {
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_wgrad_dma_kernel<BM, BN>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
+    attr = true;
+  }
+  const int TM = a.Cout / BM, TN = a.Kw * a.Cin / BN;
+  hipLaunchKernelGGL((conv1d_nlc_wgrad_dma_kernel<BM, BN>), dim3((unsigned)(TM * TN * splits)), dim3(THREADS), SMEM,
+                     stream, a, TM, TN, splits);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
@@ -878,6 +1039,12 @@ ECG_API int ecg_conv1d_nlc_wgrad(const void* dy, const void* x, float* part, int
               stride, pad, cps, make_fastdiv(Lout)};
   const bool bm128 = Cout % 128 == 0, bn128 = Cin % 128 == 0;
   if (wgrad_big(Cout, Cin)) return launch_wgrad<256, 256>(a, splits, stream);
+  if (bm128 && bn128 && wgrad_dma()) {
+    // 32-bit buffer offsets from the split's first row / sample
+    const long rows = (long)cps * 64;
+    if (rows * Cout * 2 < 0x7fff0000L && (rows / Lout + 2) * (long)Lin * Cin * 2 < 0x7fff0000L)
+      return launch_wgrad_dma<128, 128>(a, splits, stream);
+  }
   if (bm128 && bn128) return launch_wgrad<128, 128>(a, splits, stream);
   if (bm128) return launch_wgrad<128, 64>(a, splits, stream);
   if (bn128) return launch_wgrad<64, 128>(a, splits, stream);
