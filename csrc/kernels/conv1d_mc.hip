@@ -796,16 +796,17 @@ __global__ __launch_bounds__(128 * NWR, NWR == 2 ? 3 : 1) void conv1d_nlc_wgrad_
 // rebased at the split's first row / sample: 32-bit offsets cover any batch (the host checks the span).
 __device__ __forceinline__ int wg_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
 
-template <int BM, int BN>
-__global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_wgrad_dma_kernel(WgradArgs a, int TM, int TN, int splits) {
-  static_assert(BM == 128 && BN == 128, "the swizzle needs >= 16 chunks per row");
-  constexpr int NWR = 2;
+template <int BM, int BN, int NWR>
+__global__ __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) void conv1d_nlc_wgrad_dma_kernel(WgradArgs a, int TM, int TN,
+                                                                                           int splits) {
+  static_assert(BM == BN && (BM == 128 || BM == 256), "square tiles with >= 16 chunks per row");
   using Cfg = WgCfg<BM, BN, NWR>;
-  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
-  constexpr int RA = BM * 2, RB = BN * 2;      // bytes per image row
+  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NW = Cfg::NW;
+  constexpr int RA = BM * 2, RB = BN * 2;  // bytes per image row
   constexpr int A_BYTES = 64 * RA, STAGE = 64 * (RA + RB);
-  constexpr int AP = A_BYTES / 1024 / 4, BP = 64 * RB / 1024 / 4;  // 1-KB DMA pieces per wave per stage
-  constexpr int RPP = 1024 / RA;                                   // rows per piece (4)
+  constexpr int AP = A_BYTES / 1024 / NW, BP = 64 * RB / 1024 / NW;  // 1-KB DMA pieces per wave per stage
+  constexpr int RPP = 1024 / RA;                                      // rows per piece (4 or 2)
+  constexpr int SH = RA == 256 ? 4 : 5, SLOT = RA / 16 - 1;           // lane -> (row in piece, 16-B slot)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1, wc = wv & 1;
@@ -834,11 +835,11 @@ __global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_wgrad_dma_kernel(WgradA
     int arow[AP], asrc[BP > AP ? BP : AP], brow[BP];
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
-      arow[i] = RPP * (wv + 4 * i) + (lane >> 4);
-      asrc[i] = (lane & 15) ^ wg_swz(arow[i]);
+      arow[i] = RPP * (wv + NW * i) + (lane >> SH);
+      asrc[i] = (lane & SLOT) ^ wg_swz(arow[i]);
     }
 #pragma unroll
-    for (int i = 0; i < BP; ++i) brow[i] = RPP * (wv + 4 * i) + (lane >> 4);
+    for (int i = 0; i < BP; ++i) brow[i] = RPP * (wv + NW * i) + (lane >> SH);
     auto issue = [&](int ch, int st) {
       unsigned char* As = smem + st * STAGE;
       const int rel = (ch - ch0) * 64;
@@ -846,18 +847,18 @@ __global__ __launch_bounds__(THREADS, 2) void conv1d_nlc_wgrad_dma_kernel(WgradA
       for (int i = 0; i < AP; ++i) {
         const int r = rel + arow[i];
         const unsigned voff = r0 + r < R ? (unsigned)(((long)r * a.Cout + co0 + asrc[i] * 8) * 2) : 0x7ffffff0u;
-        dma16(dyr, voff, As + (wv + 4 * i) * 1024);
+        dma16(dyr, voff, As + (wv + NW * i) * 1024);
       }
 #pragma unroll
       for (int i = 0; i < BP; ++i) {
         const int rg = r0 + rel + brow[i];
         const int b = fdiv(rg, a.lout), t = rg - b * a.Lout;
         const int u = t * a.stride + k - a.pad;
-        const int src = (lane & 15) ^ wg_swz(brow[i]);
+        const int src = (lane & SLOT) ^ wg_swz(brow[i]);
         const unsigned voff = (rg < R && u >= 0 && u < a.Lin)
                                   ? (unsigned)((((long)(b - b0) * a.Lin + u) * a.Cin + c0 + src * 8) * 2)
                                   : 0x7ffffff0u;
-        dma16(xr, voff, As + A_BYTES + (wv + 4 * i) * 1024);
+        dma16(xr, voff, As + A_BYTES + (wv + NW * i) * 1024);
       }
     };
     const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4, h = lane >> 4;
@@ -938,25 +939,27 @@ inline bool wgrad_dma() {
 
 template <int BM, int BN>
 int launch_wgrad_dma(const WgradArgs& a, int splits, hipStream_t stream) {
-  using Cfg = WgCfg<BM, BN, 2>;
+  constexpr int NWR = BM >= 256 ? 4 : 2;
+  using Cfg = WgCfg<BM, BN, NWR>;
   constexpr int STAGES = 2 * 64 * (BM + BN) * 2;
   constexpr int SMEM = STAGES > Cfg::EP_BYTES ? STAGES : Cfg::EP_BYTES;
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
   static bool attr = false;
   if (!attr) {
-    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_wgrad_dma_kernel<BM, BN>,
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_wgrad_dma_kernel<BM, BN, NWR>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
     attr = true;
   }
   const int TM = a.Cout / BM, TN = a.Kw * a.Cin / BN;
-  hipLaunchKernelGGL((conv1d_nlc_wgrad_dma_kernel<BM, BN>), dim3((unsigned)(TM * TN * splits)), dim3(THREADS), SMEM,
-                     stream, a, TM, TN, splits);
+  hipLaunchKernelGGL((conv1d_nlc_wgrad_dma_kernel<BM, BN, NWR>), dim3((unsigned)(TM * TN * splits)), dim3(Cfg::NTHR),
+                     SMEM, stream, a, TM, TN, splits);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
 
-// 256x256 weight-gradient tiles (opt-in, ECG_CONV_BIG >= 2, both channel counts multiples of 256): measured
-// -6 %..+6 % against 128x128 on the ResNet shapes (profiles/r1_resnet/cmb_p4_big*.log) - the register-staged
-// single-buffer loop, not the L2->LDS traffic, bounds this kernel.
+// 256x256 weight-gradient tiles (opt-in, ECG_CONV_BIG >= 2, both channel counts multiples of 256): register-staged
+// -6 %..+6 % against 128x128 (profiles/r1_resnet/cmb_p4_big*.log); with the LDS-DMA loop 1-14 % slower than the
+// 128x128 DMA tiles (profiles/r1_resnet/wgrad_dma_256_*.log).
 inline bool wgrad_big(int Cout, int Cin) { return conv_big() >= 2 && Cout % 256 == 0 && Cin % 256 == 0; }
 
 }  // namespace
@@ -1038,13 +1041,13 @@ ECG_API int ecg_conv1d_nlc_wgrad(const void* dy, const void* x, float* part, int
   WgradArgs a{static_cast<const __bf16*>(dy), static_cast<const __bf16*>(x), part, B, Lin, Cin, Lout, Cout, Kw,
               stride, pad, cps, make_fastdiv(Lout)};
   const bool bm128 = Cout % 128 == 0, bn128 = Cin % 128 == 0;
-  if (wgrad_big(Cout, Cin)) return launch_wgrad<256, 256>(a, splits, stream);
-  if (bm128 && bn128 && wgrad_dma()) {
-    // 32-bit buffer offsets from the split's first row / sample
-    const long rows = (long)cps * 64;
-    if (rows * Cout * 2 < 0x7fff0000L && (rows / Lout + 2) * (long)Lin * Cin * 2 < 0x7fff0000L)
-      return launch_wgrad_dma<128, 128>(a, splits, stream);
-  }
+  // LDS-DMA loops: 32-bit buffer offsets from the split's first row / sample
+  const long rows = (long)cps * 64;
+  const bool dma_ok = wgrad_dma() && rows * Cout * 2 < 0x7fff0000L &&
+                      (rows / Lout + 2) * (long)Lin * Cin * 2 < 0x7fff0000L;
+  if (wgrad_big(Cout, Cin)) return dma_ok ? launch_wgrad_dma<256, 256>(a, splits, stream)
+                                          : launch_wgrad<256, 256>(a, splits, stream);
+  if (bm128 && bn128 && dma_ok) return launch_wgrad_dma<128, 128>(a, splits, stream);
   if (bm128 && bn128) return launch_wgrad<128, 128>(a, splits, stream);
   if (bm128) return launch_wgrad<128, 64>(a, splits, stream);
   if (bn128) return launch_wgrad<64, 128>(a, splits, stream);
