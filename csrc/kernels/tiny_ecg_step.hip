@@ -545,12 +545,15 @@ struct TinySample {
       } else {
         const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
         auto mfma_pair = [&](int pair, f32x4 a) {
-          const int ta = 32 * pair + 8 * h + q;  // time of row q of this lane-quarter's first 4x16 block
-          // A[co][t] (lane: co = l&15, t = 32*pair + 8h + j): transposing reads of the [t][co] mask image
-          const bf16x8 A = cat44(lds_tr16(ms + (ta + 4) * C + p4), lds_tr16(ms + (ta + 4 + 4) * C + p4));
+          // Reduction slot (h, j) holds time 32*pair + 4h + j (j < 4) or 32*pair + 16 + 4h + (j - 4): the two
+          // lane quarters of one 32-lane LDS cycle read 8 consecutive 32-B rows (256 B, conflict-free); with
+          // 8h + j their rows were 256 B apart (2-way conflicts on every transposing read of this phase).
+          const int ta = 32 * pair + 4 * h + q;
+          // A[co][t]: transposing reads of the [t][co] mask image
+          const bf16x8 A = cat44(lds_tr16(ms + (ta + 4) * C + p4), lds_tr16(ms + (ta + 16 + 4) * C + p4));
           // B[t][ci] = h1[t + k - 2][ci]
           const bf16x8 Bm =
-              cat44(lds_tr16(h1s + (ta + k - 2 + 2) * C + p4), lds_tr16(h1s + (ta + k - 2 + 4 + 2) * C + p4));
+              cat44(lds_tr16(h1s + (ta + k - 2 + 2) * C + p4), lds_tr16(h1s + (ta + 16 + k - 2 + 2) * C + p4));
           return __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bm, a, 0, 0, 0);
         };
         // two independent accumulation chains so the next pair's transposing reads overlap this pair's MFMA
@@ -617,11 +620,11 @@ struct TinySample {
             *reinterpret_cast<bf16x4*>(hp) = dv;
           }
           // conv1 wgrad over the pair's 32 steps: A[ci][t] = dh1 (transposing reads of the rows just written by
-          // this wave), B[t][kk] = xcol (columns 8..15 come from the zero row)
-          const int ta = 32 * pair + 8 * h + q;
-          const bf16x8 Ad = cat44(lds_tr16(h1s + (ta + 2) * C + p4), lds_tr16(h1s + (ta + 2 + 4) * C + p4));
+          // this wave), B[t][kk] = xcol (columns 8..15 come from the zero row); reduction slots as in phase 3
+          const int ta = 32 * pair + 4 * h + q;
+          const bf16x8 Ad = cat44(lds_tr16(h1s + (ta + 2) * C + p4), lds_tr16(h1s + (ta + 16 + 2) * C + p4));
           const __bf16* xa = p4 < 8 ? xcol + ta * 8 + p4 : xzero;
-          const __bf16* xb = p4 < 8 ? xcol + (ta + 4) * 8 + p4 : xzero;
+          const __bf16* xb = p4 < 8 ? xcol + (ta + 16) * 8 + p4 : xzero;
           wacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ad, cat44(lds_tr16(xa), lds_tr16(xb)), wacc, 0, 0, 0);
         }
       }
