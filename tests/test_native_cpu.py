@@ -110,3 +110,31 @@ def test_prefetcher_loop_mode_and_shutdown(tmp_path):
         slot, view, _ = pf.next_batch_cpu()
         pf.recycle(slot)
     pf.close()  # joins the producer thread
+
+
+def test_labl_compat_api(tmp_path):
+    """Reference LABL API names (labl_loader(EXPERIMENTAL).py): open_shard yields (mm, base, N, L) that
+    np.frombuffer reads exactly like the reference; the prefetcher keeps its constructor and methods."""
+    import labl_loader
+    data, paths = _shards(tmp_path)
+    reader = labl_loader.LABLShardedReader(paths)
+    with reader.open_shard(paths[2]) as (mm, base, N, L):
+        assert (base, N, L) == (16, 128, 40)
+        w5 = np.frombuffer(mm, dtype=np.float32, count=L, offset=base + 5 * L * 4)
+        assert np.array_equal(w5, data[256 + 5])
+    ring = labl_loader.PinnedRing(3, (8, 1, 40))
+    assert len(ring.slots) == 3 and ring.q_free.qsize() == 3 and ring.q_full.empty()
+    pf = labl_loader.LABLPrefetcher(reader, batch_size=64, num_slots=2, normalize=False, pinned=False)
+    assert (pf.L, pf.B) == (40, 64)
+    pf.start()
+    got = [b[:, 0].clone().numpy() for b, ms in pf]
+    pf.close()
+    assert np.array_equal(np.concatenate(got), data)
+
+
+def test_labl_open_shard_view_outlives_block(tmp_path):
+    import labl_loader
+    data, paths = _shards(tmp_path)
+    with labl_loader.LABLShardedReader(paths).open_shard(paths[0]) as (mm, base, N, L):
+        w = np.frombuffer(mm, dtype=np.float32, count=N * L, offset=base)
+    assert np.array_equal(w.reshape(N, L), data[:N])  # mapping stays until the last view is dropped
