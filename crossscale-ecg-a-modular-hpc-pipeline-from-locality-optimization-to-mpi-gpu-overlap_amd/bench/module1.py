@@ -135,8 +135,14 @@ def measure_step(dl: DataLoader, device, non_blocking: bool, iters: int = 50, co
 
 def bench_labl(shard_paths: Sequence[str], batch_size: int, iters: int, normalize: bool, device,
                compute: str = "torch", num_slots: int = 4) -> Dict:
-    """A4: native LABL prefetcher + copy-stream H2D double buffer (reference bench_labl, :23-94)."""
+    """A4: native LABL prefetcher + copy-stream H2D double buffer (reference bench_labl, :23-94).
+    ``shard_paths`` is a list of shard files or, as in the reference, a glob string."""
     from ..ops.native_io import NativePrefetcher
+    if isinstance(shard_paths, str):
+        import glob as _glob
+        shard_paths = sorted(_glob.glob(shard_paths))
+        if not shard_paths:
+            raise FileNotFoundError("bench_labl: no shards match the glob")
     dev = torch.device(device)
     pf = NativePrefetcher(shard_paths, batch_size, num_slots=num_slots, normalize=normalize,
                           pinned=dev.type == "cuda", loop=True)

@@ -138,3 +138,11 @@ def test_labl_open_shard_view_outlives_block(tmp_path):
     with labl_loader.LABLShardedReader(paths).open_shard(paths[0]) as (mm, base, N, L):
         w = np.frombuffer(mm, dtype=np.float32, count=N * L, offset=base)
     assert np.array_equal(w.reshape(N, L), data[:N])  # mapping stays until the last view is dropped
+
+
+def test_bench_labl_cpu_glob(tmp_path):
+    """A4 benchmark on the CPU device, shards given as the reference's glob string."""
+    from crossscale_ecg.bench.module1 import bench_labl
+    _shards(tmp_path, n=300, L=500, size=128)
+    st = bench_labl(str(tmp_path / "ecg_*.bin"), 32, 3, True, "cpu")
+    assert st["samples_per_s"] > 0 and st["step_ms"] > 0
