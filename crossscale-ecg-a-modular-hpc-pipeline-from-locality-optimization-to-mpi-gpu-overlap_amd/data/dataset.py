@@ -168,9 +168,16 @@ class DeviceIndexSampler:
     ``batch_size`` slices, trailing partial batch dropped.  ``fill(table)`` writes the next
     ``table.shape[0]`` batches into ``table`` (int32 [S, B]) in place, so a captured graph that
     reads ``table`` sees new batches every replay.
+
+    Permutations are generated ``epochs_per_block`` epochs at a time as one batched ``argsort`` of
+    independent 62-bit random keys (a uniform random permutation per row): one sort of [E, N] costs about
+    as many launches as one ``randperm(N)``, so for small shards (N=20,000: ~8 sort/scan kernels per
+    epoch, ~40 us per 50-step round, ~6 % of a 0.64 ms fused round) the per-round cost drops to the one
+    or two table copies.
     """
 
-    def __init__(self, n_windows: int, batch_size: int, device, seed: Optional[int] = None):
+    def __init__(self, n_windows: int, batch_size: int, device, seed: Optional[int] = None,
+                 epochs_per_block: Optional[int] = None):
         if n_windows < batch_size:
             raise RuntimeError(f"Not enough windows ({n_windows}) for a batch of {batch_size}")
         self.N = n_windows
@@ -181,12 +188,24 @@ class DeviceIndexSampler:
         if seed is not None:
             self.gen = torch.Generator(device=self.device)
             self.gen.manual_seed(seed)
+        if epochs_per_block is None:  # ~2M keys per block: small shards batch many epochs, big ones one
+            epochs_per_block = max(1, min(32, (1 << 21) // max(1, n_windows)))
+        self.E = int(epochs_per_block)
         self._perm: Optional[torch.Tensor] = None
-        self._cursor = self.steps_per_epoch  # force a new epoch on first use
+        self._rows = 0
+        self._cursor = 0  # force a new block on first use
 
     def _new_epoch(self):
-        p = torch.randperm(self.N, device=self.device, generator=self.gen)
-        self._perm = p[: self.steps_per_epoch * self.B].to(torch.int32).view(self.steps_per_epoch, self.B)
+        spe, B = self.steps_per_epoch, self.B
+        if self.E == 1:
+            p = torch.randperm(self.N, device=self.device, generator=self.gen).view(1, self.N)
+        else:
+            keys = torch.randint(0, 1 << 62, (self.E, self.N), device=self.device, generator=self.gen,
+                                 dtype=torch.int64)
+            p = keys.argsort(dim=1)
+        # [E, spe*B] -> rows of consecutive epochs, each epoch's batches in order (drop-last per epoch)
+        self._perm = p[:, : spe * B].to(torch.int32).reshape(self.E * spe, B)
+        self._rows = self.E * spe
         self._cursor = 0
 
     def fill(self, table: torch.Tensor) -> torch.Tensor:
@@ -195,9 +214,9 @@ class DeviceIndexSampler:
             raise ValueError(f"index table must be int32 [S, {self.B}], got {table.dtype} {tuple(table.shape)}")
         s = 0
         while s < S:
-            if self._cursor >= self.steps_per_epoch:
+            if self._cursor >= self._rows:
                 self._new_epoch()
-            take = min(S - s, self.steps_per_epoch - self._cursor)
+            take = min(S - s, self._rows - self._cursor)
             table[s:s + take].copy_(self._perm[self._cursor:self._cursor + take], non_blocking=True)
             s += take
             self._cursor += take

@@ -109,3 +109,18 @@ def test_prep_cli(tmp_path):
     assert set(js) == {"dataset", "total_windows", "window_len", "shard_size_windows", "num_shards", "load_time_s",
                        "write_time_s", "total_time_s", "timestamp"}
     assert len(S.list_shards(str(tmp_path / "shards"))) == 4
+
+
+@pytest.mark.parametrize("E", [1, 3, None])
+def test_device_index_sampler_epoch_blocks(E):
+    """Batched multi-epoch permutations: every epoch is a drop-last slice of a permutation of [0, N)."""
+    N, B = 103, 10
+    s = DeviceIndexSampler(N, B, "cpu", seed=1, epochs_per_block=E)
+    spe = N // B
+    tab = torch.empty((spe * 7 + 4, B), dtype=torch.int32)
+    s.fill(tab[:5])
+    s.fill(tab[5:])  # refills span block boundaries
+    for e in range(7):
+        v = tab[e * spe:(e + 1) * spe].reshape(-1).tolist()
+        assert len(set(v)) == spe * B and min(v) >= 0 and max(v) < N
+    assert not torch.equal(tab[:spe], tab[spe:2 * spe])
