@@ -228,7 +228,7 @@ def main(argv=None):
                 "global_batch": B * a.gpus,
                 "seq_len": a.win_len,
                 "parallelism": f"dp{a.gpus}",
-                "sync": f"fedavg every {S} local steps (RCCL all_reduce AVG)",
+                "sync": f"fedavg every {S} local steps ({'RCCL' if ctx.backend in ('nccl', 'none') else ctx.backend} all_reduce AVG)",
                 "per_client_batch": B,
                 "max_windows_per_client": a.max_windows,
                 "backend": a.backend,

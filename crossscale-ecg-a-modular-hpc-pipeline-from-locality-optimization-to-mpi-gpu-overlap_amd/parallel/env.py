@@ -85,8 +85,8 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, pr
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     device = setup_device(local_rank, prefer_gpu)
-    if backend is None:
-        backend = "nccl" if device.type == "cuda" else "gloo"
+    if backend is None:  # ECG_DIST_BACKEND=gloo rehearses several ranks on one shared GPU (RCCL needs 1 GPU/rank)
+        backend = os.environ.get("ECG_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
     ctx = DistContext(rank, world, local_rank, backend if world > 1 else "none", device)
     if world > 1 and dist.is_available() and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
