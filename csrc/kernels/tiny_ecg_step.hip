@@ -895,12 +895,17 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
 }
 
 // Sum the per-sample gradient rows and apply SGD (+momentum, weight decay, nesterov) in place.
-// grid = ceil((P+1)/16) blocks of 256 threads: 16 columns x 16 row groups per block, each thread keeps 16
+// grid = ceil((P+1)/32) blocks of 512 threads: 32 columns x 16 row groups per block, each thread keeps 16
 // independent row loads in flight.  The slab was just written by CUs on every XCD, so this is a
-// latency/fabric-bound read of ~1.5 MB: spreading it over ~90 CUs (not 23) is what makes it fast.
+// latency/fabric-bound read of ~1.5 MB.  Measured (bench.py, us/step, two-launch graph round, TinyECG
+// B=256): 4 cols 13.7, 8 cols 12.5, 16 cols 11.8, 32 cols 11.5, 64 cols 11.7 - 128-byte row segments per
+// wave instruction over 46 CUs beat narrower segments over more CUs (profiles/r1_final/ab_red_cols.txt).
 // Column P carries the per-sample loss (accumulated into loss_acc, never SGD-updated).
-constexpr int RED_COLS = 16;
+// RED_COLS (columns per block) only changes how columns are grouped into blocks, never a column's summation
+// order (fixed by RED_ROWG and the chunking below), so every width gives bitwise-identical results.
+constexpr int kRedColsDefault = 32;
 constexpr int RED_ROWG = 16;
+template <int RED_COLS>
 __global__ __launch_bounds__(RED_COLS * RED_ROWG) void slab_reduce_sgd_kernel(
     const float* __restrict__ slab, int G, int stride, int P,
     float* __restrict__ params, float* __restrict__ mom, float* __restrict__ grad_out,
@@ -1258,9 +1263,27 @@ int reduce_dispatch(const float* slab, int G, int stride, int P, float* params, 
                     hipStream_t stream) {
   if (G <= 0 || P <= 0 || stride < P + 1) return ecg::kBadArg;
   if (apply && (!params || (momentum != 0.f && !mom))) return ecg::kBadArg;
-  const int blocks = (P + 1 + RED_COLS - 1) / RED_COLS;
-  hipLaunchKernelGGL(slab_reduce_sgd_kernel, dim3(blocks), dim3(RED_COLS * RED_ROWG), 0, stream, slab, G, stride, P, params, mom,
-                     grad_out, loss_acc, lr, momentum, wd, nesterov, apply);
+  static const int cols = [] {  // ECG_RED_COLS in {4, 8, 16, 32, 64}: columns per reduction block (A/B knob)
+    const char* e = getenv("ECG_RED_COLS");
+    const int v = e ? atoi(e) : kRedColsDefault;
+    return (v == 4 || v == 8 || v == 16 || v == 32 || v == 64) ? v : kRedColsDefault;
+  }();
+  const int blocks = (P + 1 + cols - 1) / cols;
+  if (cols == 4)
+    hipLaunchKernelGGL(slab_reduce_sgd_kernel<4>, dim3(blocks), dim3(4 * RED_ROWG), 0, stream, slab, G, stride, P,
+                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply);
+  else if (cols == 8)
+    hipLaunchKernelGGL(slab_reduce_sgd_kernel<8>, dim3(blocks), dim3(8 * RED_ROWG), 0, stream, slab, G, stride, P,
+                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply);
+  else if (cols == 64)
+    hipLaunchKernelGGL(slab_reduce_sgd_kernel<64>, dim3(blocks), dim3(64 * RED_ROWG), 0, stream, slab, G, stride, P,
+                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply);
+  else if (cols == 32)
+    hipLaunchKernelGGL(slab_reduce_sgd_kernel<32>, dim3(blocks), dim3(32 * RED_ROWG), 0, stream, slab, G, stride, P,
+                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply);
+  else
+    hipLaunchKernelGGL(slab_reduce_sgd_kernel<16>, dim3(blocks), dim3(16 * RED_ROWG), 0, stream, slab, G, stride, P,
+                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
