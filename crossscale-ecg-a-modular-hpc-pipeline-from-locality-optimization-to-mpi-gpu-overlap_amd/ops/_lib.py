@@ -17,7 +17,7 @@ from typing import Optional
 
 import torch  # noqa: F401  (must be loaded before libamdhip64 is resolved by our libraries)
 
-LIB_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib")
+LIB_DIR = os.environ.get("ECG_LIB_DIR") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib")
 
 _lock = threading.Lock()
 _libs = {}

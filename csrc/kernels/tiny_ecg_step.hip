@@ -754,13 +754,27 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     // phase 0: stage params + x into LDS, zero pads.  (Measured: pre-gathering a round's windows into contiguous
     // buffers inside the round graph, to drop the dependent idx -> row load, costs more than it saves:
     // 12.98 vs 12.52 us/step, profiles/r1_round_kernel/ab_pregather.log.)
+    // The parameter loads are issued first, into registers, so their round trip overlaps the dependent
+    // idx -> window chain instead of following the window's LDS stores.
     int ylab = 0;
+    constexpr int PR = 4;  // parameters per thread held in registers (P <= PR * NT for nc <= 40 at 8 waves)
+    float pv[PR];
+#pragma unroll
+    for (int j = 0; j < PR; ++j) {
+      const int i = tid + j * S.NT;
+      pv[j] = i < S.lay.P ? params[i] : 0.f;
+    }
     {
       const long row = idx ? (long)idx[b] : (long)b;
       if (TRAIN) ylab = Y[row];  // label prefetched with the window (used by the head)
       S.stage_x(X + row * ldx);
     }
-    for (int i = tid; i < S.lay.P; i += S.NT) S.put_param(i, params[i]);
+#pragma unroll
+    for (int j = 0; j < PR; ++j) {
+      const int i = tid + j * S.NT;
+      if (i < S.lay.P) S.put_param(i, pv[j]);
+    }
+    for (int i = tid + PR * S.NT; i < S.lay.P; i += S.NT) S.put_param(i, params[i]);
     S.zero_pads();
     __syncthreads();
     ECG_STAMP(1)
