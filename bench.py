@@ -5,34 +5,39 @@ Config (BASELINE.json / Module_3/TRUE_FL_M3/run_part3_sweep.sh:38-49): TinyECG (
 batch 256 per client, window L=500, <=20,000 windows per client, FedAvg every 50 local steps,
 SGD(lr=1e-2, momentum=0.9), AMP (bf16 here), one FL client per GPU (``--gpus N`` ranks over RCCL).
 
-A "step" = one local SGD step of every client (N x 256 samples).  W warmup steps, then exactly K
-timed steps bracketed by barrier + synchronize; FedAvg all-reduces every ``--local-steps`` steps inside
-the timed region.  Reported value = N * 256 * K / max-over-ranks(elapsed)  (whole-job samples/s).
+A "step" = one local SGD step of every client (N x 256 samples).  The step sequence is cut into FedAvg
+rounds of ``--local-steps`` steps; EVERY round - including a trailing partial one - ends with the FedAvg
+all-reduce (one RCCL ``all_reduce(AVG)`` of the flat weights, reference part3_fedavg_overlap_mpi_gpu.py:
+209-211), so the timed region always contains communication.  W warmup steps (same round plan), then
+every hipGraph the timed plan needs is captured and uploaded, then exactly K timed steps bracketed by
+barrier + synchronize; value = N * B * K / max-over-ranks(elapsed) (whole-job samples/s).
+
+Launch: ``python bench.py --gpus N`` with N > 1 and no launcher environment starts N ranks itself
+(``torch.distributed.run`` as a child process, one rank per GPU); the parent never touches the GPU.
+Under torchrun / mpiexec / srun (RANK+WORLD_SIZE set) it runs as one rank.
+
 Data: synthetic N(0,1) windows generated on device (the reference's synthetic shard distribution,
 Module_1/shard_prep.py:35-37), dummy zero labels (Module_3/shard_dataset.py:70), random-init weights.
 
 Extra fields: ``torch_eager_*`` (same step in eager PyTorch bf16-autocast, the reference's G1 code path,
-measured in the same process) and ``conv1d_*`` (Module-2 kernel vs torch.nn.Conv1d, B=256, K=7).
+measured in the same process) and ``conv1d_*`` (Module-2 kernel vs torch.nn.Conv1d, B=256, K=7; the
+headline ``conv1d_speedup_vs_torch`` uses the reference's single-call ``time_once`` metric,
+Module_2/benchmark_part_2.py:61-67,108).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
-import torch
-
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-import crossscale_ecg  # noqa: E402
-from crossscale_ecg.models.tiny_ecg import TinyECG, num_params  # noqa: E402
-from crossscale_ecg.parallel.env import init_distributed, barrier  # noqa: E402
-from crossscale_ecg.parallel.fedavg import allreduce_mean_  # noqa: E402
-
+ROOT = os.path.dirname(os.path.abspath(__file__))
 METRIC = "ECG samples/sec (node) + conv1d speedup vs torch.Conv1d, tiny 1D-CNN at 1/2/4/8 GPU"
+_LAUNCHER_VARS = ("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "PMIX_SIZE", "SLURM_NTASKS")
 
 
 def parse(argv=None):
@@ -47,26 +52,91 @@ def parse(argv=None):
     ap.add_argument("--max-windows", type=int, default=20000)
     ap.add_argument("--win-len", type=int, default=500)
     ap.add_argument("--backend", choices=["fused", "torch"], default="fused")
+    ap.add_argument("--overlap", choices=["none", "tail"], default="tail",
+                    help="tail: the FedAvg all-reduce of round r runs under round r+1's batch preparation "
+                         "(exact FedAvg, bitwise equal to none)")
+    ap.add_argument("--device", choices=["gpu", "cpu"], default="gpu",
+                    help="cpu: plumbing rehearsal of the launch/sync/JSON contract (gloo, eager torch)")
     ap.add_argument("--no-extras", action="store_true", help="skip torch-eager and conv1d side measurements")
     return ap.parse_args(argv)
 
 
-def timed_fused(trainer, ctx, steps, local_steps, flat):
-    done = 0
-    since_sync = 0
-    while done < steps:
-        n = min(local_steps - since_sync, steps - done)
-        trainer.run_round(n, reset_loss=False)
-        done += n
-        since_sync += n
-        if since_sync == local_steps:
-            allreduce_mean_(flat, ctx)  # FedAvg: one RCCL all-reduce (AVG) of the flat weights
-            since_sync = 0
-    return done
+# ----------------------------------------------------------------------------------- self-launch
+def _under_launcher() -> bool:
+    return any(v in os.environ for v in _LAUNCHER_VARS)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(a, argv) -> int:
+    """Start ``a.gpus`` ranks (one per GPU) as a ``torch.distributed.run`` child; return its exit code.
+
+    Nothing here initialises HIP: ``torch.cuda.device_count()`` only counts devices on this image."""
+    backend = os.environ.get("ECG_DIST_BACKEND", "nccl")
+    if a.device == "gpu" and backend == "nccl":
+        import torch
+        n_dev = torch.cuda.device_count()
+        if n_dev < a.gpus:
+            print(f"bench.py: --gpus {a.gpus} needs {a.gpus} GPUs for RCCL (one rank per GPU), found {n_dev}",
+                  file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
+# ----------------------------------------------------------------------------------- timed loop
+def round_plan(steps: int, local_steps: int):
+    """Round lengths covering ``steps`` local steps: full rounds, then one trailing partial round."""
+    full, rem = divmod(int(steps), int(local_steps))
+    return [local_steps] * full + ([rem] if rem else [])
+
+
+class FedAvgRunner:
+    """Runs a round plan on a trainer: each round = local steps then the FedAvg all-reduce (AVG)."""
+
+    def __init__(self, trainer, flat, ctx, overlap: str):
+        from crossscale_ecg.parallel.fedavg import allreduce_mean_
+        self.trainer, self.flat, self.ctx = trainer, flat, ctx
+        self.allreduce = allreduce_mean_
+        self.overlap = overlap if ctx.distributed else "none"
+        self.syncs = 0
+        self._pending = None
+
+    def run(self, plan):
+        for n in plan:
+            if self._pending is not None:  # tail: next batches prepared while the all-reduce is in flight
+                self.trainer.prepare_round(n, reset_loss=False)
+                self._pending.wait()
+                self._pending = None
+                self.trainer.launch_round(n)
+            else:
+                self.trainer.run_round(n, reset_loss=False)
+            if self.overlap == "tail":
+                self._pending = self.allreduce(self.flat, self.ctx, async_op=True)
+            else:
+                self.allreduce(self.flat, self.ctx)
+            self.syncs += 1
+        self.drain()
+
+    def drain(self):
+        if self._pending is not None:
+            self._pending.wait()
+            self._pending = None
 
 
 def torch_eager_rate(x, y, B, steps, device):
+    import torch
     import torch.nn.functional as F
+    from crossscale_ecg.models.tiny_ecg import TinyECG
     model = TinyECG().to(device)
     opt = torch.optim.SGD(model.parameters(), lr=1e-2, momentum=0.9)
     g = torch.Generator(device=device)
@@ -92,7 +162,11 @@ def torch_eager_rate(x, y, B, steps, device):
     return B * steps / (time.perf_counter() - t0)
 
 
-def conv1d_speedup(device, B=256, L=500, K=7, trials=15, inner=20):
+def conv1d_speedup(device, B=256, L=500, K=7, trials=15, burst=20):
+    """Module-2 comparison at one grid point.  ``once``: the reference's ``time_once`` (3 warm-up calls + ONE
+    synchronised timed call, Module_2/benchmark_part_2.py:61-67), median over 15 trials; ``burst``: mean of
+    ``burst`` back-to-back calls (secondary)."""
+    import torch
     from crossscale_ecg.ops.conv1d import conv1d_valid
     x = torch.randn(B, 1, L, device=device)
     w = torch.randn(K, device=device)
@@ -101,34 +175,68 @@ def conv1d_speedup(device, B=256, L=500, K=7, trials=15, inner=20):
         conv.weight.copy_(w.view(1, 1, K))
     out = torch.empty(B, L - K + 1, device=device)
 
-    def t_call(fn):
+    def once(fn):
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(inner):
+        fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3
+
+    def bursty(fn):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(burst):
             fn()
         torch.cuda.synchronize()
-        return (time.perf_counter() - t0) * 1e3 / inner
+        return (time.perf_counter() - t0) * 1e3 / burst
 
+    tfn = lambda: conv(x)  # noqa: E731
+    hfn = lambda: conv1d_valid(x[:, 0], w, backend="hip", out=out)  # noqa: E731
     with torch.no_grad():
-        tt = [t_call(lambda: conv(x)) for _ in range(trials)]
-        th = [t_call(lambda: conv1d_valid(x[:, 0], w, backend="hip", out=out)) for _ in range(trials)]
-    return statistics.median(tt), statistics.median(th)
+        ok = torch.allclose(hfn(), tfn()[:, 0], atol=1e-4, rtol=1e-4)
+        t_once = [once(tfn) for _ in range(trials)]
+        h_once = [once(hfn) for _ in range(trials)]
+        t_b = [bursty(tfn) for _ in range(trials)]
+        h_b = [bursty(hfn) for _ in range(trials)]
+    med = statistics.median
+    return {"conv1d_torch_ms_median": round(med(t_once), 5), "conv1d_hip_ms_median": round(med(h_once), 5),
+            "conv1d_speedup_vs_torch": round(med(t_once) / med(h_once), 3),
+            "conv1d_burst_torch_ms": round(med(t_b), 5), "conv1d_burst_hip_ms": round(med(h_b), 5),
+            "conv1d_burst_speedup_vs_torch": round(med(t_b) / med(h_b), 3), "conv1d_matches_torch": bool(ok)}
 
 
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = parse(argv)
-    ctx = init_distributed()
+    if a.gpus > 1 and not _under_launcher():
+        return self_launch(a, argv)
+
+    import torch
+    sys.path.insert(0, ROOT)
+    import crossscale_ecg  # noqa: F401
+    from crossscale_ecg.models.tiny_ecg import TinyECG, num_params
+    from crossscale_ecg.parallel.env import init_distributed, barrier, shutdown_distributed
+
+    ctx = init_distributed(prefer_gpu=a.device == "gpu")
     if ctx.world_size != a.gpus:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={ctx.world_size}; launch with torchrun for N>1")
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={ctx.world_size}")
     dev = ctx.device
-    if dev.type != "cuda":
-        raise SystemExit("bench.py needs a GPU")
+    on_gpu = dev.type == "cuda"
+    if a.device == "gpu" and not on_gpu:
+        raise SystemExit("bench.py needs a GPU (use --device cpu for the plumbing rehearsal)")
+    if not on_gpu:
+        a.backend, a.no_extras = "torch", True
     resnet = a.model.startswith("resnet")
     if a.batch_size is None:
         a.batch_size = 1024 if resnet else 256
     B, S = a.batch_size, a.local_steps
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize(dev)
+
     # per-client synthetic shard, resident in HBM
     gen = torch.Generator(device=dev)
     gen.manual_seed(1337 + ctx.rank)
@@ -146,40 +254,35 @@ def main(argv=None):
     if resnet and a.backend == "fused":  # native ResNet step engine (one hipGraph per step)
         from crossscale_ecg.train.resnet_trainer import ResNetEngineTrainer
         trainer = ResNetEngineTrainer(model, x, y, B, S, lr=1e-2, momentum=0.9, seed=4321 + ctx.rank, ctx=ctx)
-        run = lambda k: timed_fused(trainer, ctx, k, S, flat)  # noqa: E731
     elif a.backend == "fused":
         from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
         trainer = FusedTinyTrainer(model, x, y, B, S, lr=1e-2, momentum=0.9, seed=4321 + ctx.rank)
-        run = lambda k: timed_fused(trainer, ctx, k, S, flat)  # noqa: E731
     else:
         from crossscale_ecg.train.local import TorchLocalTrainer
-        trainer = TorchLocalTrainer(model, x, y, B, amp_dtype=torch.bfloat16, seed=4321 + ctx.rank)
+        amp = torch.bfloat16 if on_gpu else None
+        trainer = TorchLocalTrainer(model, x, y, B, amp_dtype=amp, seed=4321 + ctx.rank)
+    runner = FedAvgRunner(trainer, flat, ctx, a.overlap)
 
-        def run(k):
-            done = 0
-            while done < k:
-                n = min(S, k - done)
-                trainer.run_steps(n)
-                done += n
-                if n == S:
-                    allreduce_mean_(flat, ctx)
-            return done
-
-    # warmup (also builds the graphs)
+    timed_plan = round_plan(a.steps, S)
     if a.warmup > 0:
-        run(a.warmup)
-    torch.cuda.synchronize(dev)
+        runner.run(round_plan(a.warmup, S))
+    if hasattr(trainer, "prepare"):  # capture + upload every graph the timed plan replays, outside the timing
+        trainer.prepare(sorted(set(timed_plan)))
+    runner.syncs = 0
+    sync()
     barrier(ctx)
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
-    run(a.steps)
-    torch.cuda.synchronize(dev)
+    runner.run(timed_plan)
+    sync()
     barrier(ctx)
-    torch.cuda.synchronize(dev)
+    sync()
     elapsed = time.perf_counter() - t0
+    world_seen, dist_backend = 1, "none"
     if ctx.distributed:
         import torch.distributed as dist
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        world_seen, dist_backend = dist.get_world_size(), dist.get_backend()
+        t = torch.tensor([elapsed], device=dev if dist_backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     total = a.gpus * B * a.steps
@@ -201,15 +304,13 @@ def main(argv=None):
         except Exception as e:  # pragma: no cover
             extras["torch_eager_error"] = repr(e)[:200]
         try:
-            tm, hm = conv1d_speedup(dev)
-            extras["conv1d_torch_ms_median"] = round(tm, 5)
-            extras["conv1d_hip_ms_median"] = round(hm, 5)
-            extras["conv1d_speedup_vs_torch"] = round(tm / hm, 3)
+            extras.update(conv1d_speedup(dev))
         except Exception as e:  # pragma: no cover
             extras["conv1d_error"] = repr(e)[:200]
 
     if ctx.rank == 0:
         n_par = sum(p.numel() for p in model.parameters())
+        comm = "RCCL" if dist_backend == "nccl" else dist_backend
         rec = {
             "metric": METRIC if not resnet else "ECG samples/sec (node), ResNet1D-34 scaling-stress config (BASELINE config 5)",
             "value": round(value, 1),
@@ -221,25 +322,32 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if on_gpu else "fp32",
             "data": "synthetic",
             "config": {
                 "model": f"TinyECG ({num_params(2)} params)" if not resnet else f"{a.model} ({n_par} params)",
                 "global_batch": B * a.gpus,
                 "seq_len": a.win_len,
                 "parallelism": f"dp{a.gpus}",
-                "sync": f"fedavg every {S} local steps ({'RCCL' if ctx.backend in ('nccl', 'none') else ctx.backend} all_reduce AVG)",
+                "sync": f"fedavg every {S} local steps ({comm} all_reduce AVG, overlap={runner.overlap})",
                 "per_client_batch": B,
                 "max_windows_per_client": a.max_windows,
                 "backend": a.backend,
             },
+            "rccl_world_size": world_seen,
+            "dist_backend": dist_backend,
+            "fedavg_syncs_timed": runner.syncs,
+            "timed_round_plan": timed_plan if len(timed_plan) <= 4 else f"{len(timed_plan)} rounds",
             "final_avg_loss": round(loss, 6) if loss == loss else None,
             **extras,
         }
         print(json.dumps(rec), flush=True)
     if hasattr(trainer, "close"):
         trainer.close()
+    barrier(ctx)
+    shutdown_distributed()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -222,6 +222,23 @@ class DeviceIndexSampler:
             self._cursor += take
         return table
 
+    def state_dict(self) -> dict:
+        """Everything needed to continue the exact batch order (generator state, current block, cursor)."""
+        return {"gen": None if self.gen is None else self.gen.get_state(),
+                "perm": None if self._perm is None else self._perm.detach().cpu(),
+                "rows": self._rows, "cursor": self._cursor, "N": self.N, "B": self.B, "E": self.E}
+
+    def load_state_dict(self, st: dict) -> None:
+        if (int(st["N"]), int(st["B"])) != (self.N, self.B):
+            raise ValueError(f"sampler state is for N={st['N']}, B={st['B']}; this sampler has N={self.N}, B={self.B}")
+        if st.get("gen") is not None:
+            if self.gen is None:
+                self.gen = torch.Generator(device=self.device)
+            self.gen.set_state(st["gen"])
+        self.E = int(st["E"])
+        self._perm = None if st.get("perm") is None else st["perm"].to(self.device)
+        self._rows, self._cursor = int(st["rows"]), int(st["cursor"])
+
     def next_batch(self) -> torch.Tensor:
         t = torch.empty((1, self.B), dtype=torch.int32, device=self.device)
         return self.fill(t)[0]

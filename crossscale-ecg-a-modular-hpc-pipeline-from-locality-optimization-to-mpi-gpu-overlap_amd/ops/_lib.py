@@ -84,6 +84,7 @@ def _bind_kernels(lib: C.CDLL) -> None:
     _sig(lib, "ecg_tiny_set_stamps", [vp])
     _sig(lib, "ecg_round_graph_launch", [vp, vp])
     _sig(lib, "ecg_round_graph_destroy", [vp])
+    _sig(lib, "ecg_round_graph_upload", [vp, vp])
     _sig(lib, "conv1d_batch_hip", [vp, vp, vp, i32, i32, i32, vp])
     _sig(lib, "conv1d_batch_hip_bf16", [vp, vp, vp, i32, i32, i32, vp])
     _sig(lib, "ecg_sgd_flat", [vp, vp, vp, i64, f32, f32, f32, f32, i32, i32, f32, vp, vp])

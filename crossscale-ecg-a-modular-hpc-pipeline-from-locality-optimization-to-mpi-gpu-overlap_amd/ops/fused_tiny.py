@@ -234,15 +234,43 @@ class FusedTinyTrainer:
         if code:
             raise _lib.NativeError(f"persistent TinyECG round gave up: {_lib.ROUND_GIVE_UP.get(code, code)}")
 
-    def run_round(self, n_steps: Optional[int] = None, reset_loss: bool = True) -> None:
-        """Enqueue ``n_steps`` (default ``steps_per_round``) local SGD steps on the current stream (async)."""
+    def prepare(self, sizes) -> None:
+        """Capture and upload the round graphs of every step count in ``sizes`` (no kernel runs), so a later
+        ``run_round(n)`` for those sizes only replays."""
+        if not self.use_graph:
+            return
+        lib = _lib.kernels()
+        for n in sizes:
+            n = int(n)
+            if not 0 < n <= self.S:
+                raise ValueError(f"round size {n} not in [1, {self.S}]")
+            _lib.check(lib.ecg_round_graph_upload(self._graph_for(n), _lib.stream_ptr(self.device)),
+                       "ecg_round_graph_upload")
+        torch.cuda.synchronize(self.device)
+
+    def _check_n(self, n_steps: Optional[int]) -> int:
         n = self.S if n_steps is None else int(n_steps)
         if not 0 < n <= self.S:
             raise ValueError(f"n_steps must be in [1, {self.S}]")
+        return n
+
+    def prepare_round(self, n_steps: Optional[int] = None, reset_loss: bool = True) -> None:
+        """Batch preparation of a round (index-table fill on the current stream); reads no weights, so it can run
+        while the previous round's FedAvg all-reduce is still in flight (``--overlap tail``)."""
+        n = self._check_n(n_steps)
         if reset_loss:
             self.loss_acc.zero_()
             self._loss_steps = 0
         self.sampler.fill(self.idx_table[:n])
+
+    def run_round(self, n_steps: Optional[int] = None, reset_loss: bool = True) -> None:
+        """Enqueue ``n_steps`` (default ``steps_per_round``) local SGD steps on the current stream (async)."""
+        self.prepare_round(n_steps, reset_loss)
+        self.launch_round(n_steps)
+
+    def launch_round(self, n_steps: Optional[int] = None) -> None:
+        """The round's SGD steps on the index table filled by ``prepare_round`` (one graph replay)."""
+        n = self._check_n(n_steps)
         if self.use_graph:
             g = self._graph_for(n)
             _lib.check(_lib.kernels().ecg_round_graph_launch(g, _lib.stream_ptr(self.device)),

@@ -65,10 +65,18 @@ class DistContext:
 _CTX: Optional[DistContext] = None
 
 
-def setup_device(local_rank: int = 0, prefer_gpu: bool = True) -> torch.device:
-    """``cuda:{local_rank}`` when a GPU is present (reference always used cuda:0, one GPU per node)."""
+def setup_device(local_rank: int = 0, prefer_gpu: bool = True, exclusive: bool = False) -> torch.device:
+    """``cuda:{local_rank}`` when a GPU is present (reference always used cuda:0, one GPU per node).
+
+    ``exclusive`` (RCCL ranks): every local rank needs a GPU of its own - more local ranks than GPUs is an
+    error rather than two ranks silently sharing a device (RCCL would fail or hang).  Without it (gloo
+    rehearsals) ranks wrap around the visible GPUs."""
     if prefer_gpu and torch.cuda.is_available():
         n = torch.cuda.device_count()
+        if exclusive and local_rank >= n:
+            raise RuntimeError(f"local rank {local_rank} has no GPU of its own ({n} visible); the nccl (RCCL) "
+                               f"backend needs one GPU per rank - launch at most {n} ranks per node, or set "
+                               f"ECG_DIST_BACKEND=gloo to rehearse several ranks on a shared GPU")
         dev = torch.device("cuda", local_rank % max(1, n))
         torch.cuda.set_device(dev)
         return dev
@@ -84,9 +92,12 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, pr
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    device = setup_device(local_rank, prefer_gpu)
     if backend is None:  # ECG_DIST_BACKEND=gloo rehearses several ranks on one shared GPU (RCCL needs 1 GPU/rank)
-        backend = os.environ.get("ECG_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
+        backend = os.environ.get("ECG_DIST_BACKEND")
+    gpu = prefer_gpu and torch.cuda.is_available()
+    device = setup_device(local_rank, prefer_gpu, exclusive=world > 1 and gpu and backend in (None, "nccl"))
+    if backend is None:
+        backend = "nccl" if device.type == "cuda" else "gloo"
     ctx = DistContext(rank, world, local_rank, backend if world > 1 else "none", device)
     if world > 1 and dist.is_available() and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

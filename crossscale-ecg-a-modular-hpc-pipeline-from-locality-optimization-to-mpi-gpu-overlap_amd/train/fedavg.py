@@ -10,9 +10,12 @@ the results CSV and prints node-aggregate samples/s (sum over clients, wall time
 MI355X execution (vs the reference's host-staged per-tensor MPI calls and per-step sync):
   * G1 local round = ONE native hipGraph replay of ``local_steps`` fused HIP steps (``ops.fused_tiny``);
   * FedAvg = ONE RCCL ``all_reduce(AVG)`` of the flat fp32 weight buffer; broadcast = ONE RCCL broadcast;
-  * ``--overlap delayed``: the all-reduce runs on RCCL's stream under the next round (stale-by-one FedAvg);
-  * ``--overlap tail`` (ResNet engine): the round's last step applies SGD per backward segment and all-reduces
-    each segment's weights while earlier segments still run backward (exact FedAvg, comm overlapped);
+  * collectives run from a dedicated comm stream with hipEvents on both streams (``parallel.overlap``), so each
+    row's ``comm_ms`` is the collectives' own span and ``comm_exposed_ms`` the MEASURED compute-stream stall;
+  * ``--overlap tail`` (exact FedAvg): TinyECG / eager clients issue the all-reduce asynchronously and prepare
+    the next round's batches before the compute stream waits; the ResNet engine applies the last step's SGD per
+    backward segment and all-reduces each segment while earlier segments still run backward;
+  * ``--overlap delayed``: the all-reduce runs under the next round's local steps (stale-by-one FedAvg);
   * ResNet1D G1 runs on the native step engine (``train.resnet_trainer``; one hipGraph replay per step);
   * ``--sync none``: pseudo-federated independent clients; ``--sync ddp``: synchronous gradient DP;
   * ``--drop-prob``: client dropout with sample-weighted averaging; ``--ckpt-every``/``--resume``.
@@ -34,10 +37,11 @@ from ..data.dataset import load_shards_to_gpu
 from ..data.shards import assign_shards_evenly
 from ..models import build_model
 from ..parallel.env import DistContext, barrier
-from ..parallel.fedavg import (Communicator, broadcast_model, fedavg_allreduce, weighted_fedavg_, DelayedFedAvg,
-                               model_flat)
+from ..parallel.fedavg import Communicator, broadcast_model, weighted_fedavg_, model_flat
+from ..parallel.overlap import CommRecord, FedAvgComm, FedAvgRound
 from ..utils import profiling, usable_cpus
-from ..utils.ckpt import ckpt_path, save_checkpoint, load_checkpoint, latest_checkpoint
+from ..utils.ckpt import (ckpt_path, save_checkpoint, load_checkpoint, latest_checkpoint, rank_state_path,
+                          save_rank_state, load_trainer_local_state)
 from ..utils.csvio import RoundStats, append_results, ROUND_COLUMNS
 from ..utils.log import RankLogger
 from .local import TorchLocalTrainer
@@ -131,9 +135,7 @@ def _ddp_fused_round(trainer, ctx: DistContext, n: int):
     if not hasattr(trainer, "_ddp_opt"):
         trainer._ddp_grad = torch.zeros_like(trainer.params)
         trainer._ddp_opt = FlatSGD(trainer.params, trainer._ddp_grad, lr=trainer.lr, momentum=trainer.momentum)
-    trainer.loss_acc.zero_()
-    trainer._loss_steps = n
-    trainer.sampler.fill(trainer.idx_table[:n])
+    trainer._loss_steps = n  # batches already drawn by trainer.prepare_round(n)
     lib = _lib.kernels()
     for s in range(n):
         tiny_step_grads(trainer.params, trainer.x, trainer.y32, trainer.idx_table[s], trainer.B, trainer.nc,
@@ -146,8 +148,33 @@ def _ddp_fused_round(trainer, ctx: DistContext, n: int):
         trainer._ddp_opt.step()
 
 
+def _resume(cfg: FedAvgConfig, cname: str, ctx: DistContext, comm: Communicator, model, trainer, log) -> int:
+    """Rank 0 resolves and loads the latest checkpoint and tells every rank the round to start from; each rank
+    restores its own client state (momentum, sampler, RNG) when its directory has it (utils/ckpt.py)."""
+    path = latest_checkpoint(cfg.ckpt_dir, cname) if ctx.rank == 0 else None
+    rnd = -1
+    if path:
+        st = load_checkpoint(path)
+        model.load_state_dict(st["model"])
+        rnd = int(st["round"])
+    rnd = int(comm.bcast(rnd, root=0))
+    if rnd < 0:
+        return 0
+    own = rank_state_path(cfg.ckpt_dir, rnd, cname, ctx.rank)
+    if os.path.exists(own):
+        load_trainer_local_state(trainer, load_checkpoint(own))
+        log.info(f"[fedavg] rank {ctx.rank}: client state restored from {own}")
+    else:
+        log.info(f"[fedavg] rank {ctx.rank}: no {own}; momentum restarts at zero, sampler from its seed")
+    if ctx.rank == 0:
+        log.info(f"[fedavg] resumed {cname} from {path} at round {rnd + 1}")
+    return rnd + 1
+
+
 def run_fedavg(cfg: FedAvgConfig, ctx: DistContext) -> List[Dict]:
     log = RankLogger(ctx.rank, cfg.jsonl, cfg.quiet)
+    if "{rank}" in (cfg.ckpt_dir or ""):  # node-local checkpoint directories (no shared filesystem)
+        cfg.ckpt_dir = cfg.ckpt_dir.format(rank=ctx.rank)
     comm = Communicator(ctx)
     dev = ctx.device
     torch.set_num_threads(max(1, min(4, usable_cpus())))
@@ -159,78 +186,84 @@ def run_fedavg(cfg: FedAvgConfig, ctx: DistContext) -> List[Dict]:
              f"overlap={cfg.overlap}")
     configs = ["G0", "G1"] if cfg.config == "both" else [cfg.config]
     all_rows: List[Dict] = []
+    fcomm = FedAvgComm(ctx)
     for cname in configs:
         set_basic_seeds(cfg.seed + ctx.rank)
         torch.manual_seed(cfg.seed)  # identical init on every client (the round-0 broadcast makes it exact)
         model = build_model(cfg.model, cfg.num_classes).to(dev)
         backend = pick_backend(cfg, cname, ctx)
-        flat = model.flatten_parameters() if hasattr(model, "flatten_parameters") else None
+        if hasattr(model, "flatten_parameters"):
+            model.flatten_parameters()
         trainer = make_trainer(cfg, cname, model, x, y, ctx, backend)
-        start_round = 0
-        if cfg.resume:
-            p = latest_checkpoint(cfg.ckpt_dir, cname)
-            if p:
-                st = load_checkpoint(p)
-                model.load_state_dict(st["model"])
-                start_round = int(st["round"]) + 1
-                log.info(f"[fedavg] resumed {cname} from {p} at round {start_round}")
-        delayed = DelayedFedAvg(model_flat(model), ctx) if (cfg.overlap == "delayed" and cfg.sync == "fedavg") else None
-        rows = []
+        log.info(f"[fedavg] {cname}: kernel backend {backend}")
+        start_round = _resume(cfg, cname, ctx, comm, model, trainer, log) if cfg.resume else 0
+        fedavg = cfg.sync == "fedavg" and ctx.distributed
+        weighted = fedavg and cfg.drop_prob > 0
+        mode = cfg.overlap if (fedavg and not weighted) else "none"
+        # ResNet engine: the tail step applies SGD per backward segment and all-reduces each segment at once
+        seg_tail = mode == "tail" and hasattr(trainer, "tail_fedavg")
+        fround = FedAvgRound(model_flat(model), fcomm, "none" if seg_tail else mode)
+        recs = []
         for r in range(start_round, cfg.rounds):
             t_round0 = time.perf_counter()
-            # ---- broadcast the global model ------------------------------------------------
-            _sync(dev)
-            t_c0 = time.perf_counter()
-            if cfg.sync == "fedavg" and ctx.distributed and (r == start_round or cfg.bcast_every_round):
+            rec = CommRecord()
+            # ---- broadcast the global model (round 0 / resume / every round for reference parity) ----------
+            # (--overlap tail skips the per-round re-broadcast: it would serialise the overlap away, and the RCCL
+            # AVG already leaves identical weights on every client)
+            if ctx.distributed and cfg.sync in ("fedavg", "ddp") and (
+                    r == start_round or (fedavg and cfg.bcast_every_round and mode != "tail")):
+                fround.finalize()  # an in-flight tail all-reduce must land before the weights are overwritten
                 with profiling.range("bcast"):
-                    broadcast_model(comm, model)
-                _sync(dev)
-            t_c1 = time.perf_counter()
-            # ---- local steps -----------------------------------------------------------------
-            tail = (cfg.overlap == "tail" and cfg.sync == "fedavg" and ctx.distributed
-                    and hasattr(trainer, "tail_fedavg") and cfg.drop_prob == 0)
-            local_steps = cfg.local_steps - 1 if tail else cfg.local_steps
+                    fcomm.blocking(lambda: broadcast_model(comm, model), rec)
+            # ---- local steps (the previous round's tail all-reduce overlaps this round's batch preparation) --
+            n = cfg.local_steps - 1 if seg_tail else cfg.local_steps
+            m_l0 = fcomm.mark()
+            stalls0 = len(fround._rec.stalls) if fround._rec is not None else 0
+            prev_rec = fround._rec
             with profiling.range("local_round"):
+                fround.begin_round(prep=lambda: trainer.prepare_round(n))
                 if cfg.sync == "ddp" and backend == "fused" and ctx.distributed:
-                    _ddp_fused_round(trainer, ctx, local_steps)
+                    _ddp_fused_round(trainer, ctx, n)
                 else:
-                    trainer.run_round(local_steps)
-                _sync(dev)
-            t_l1 = time.perf_counter()
-            n_samples = cfg.batch_size * local_steps
-            # ---- FedAvg ----------------------------------------------------------------------
-            _sync(dev)
-            t_c2 = time.perf_counter()
-            if cfg.sync == "fedavg" and ctx.distributed:
+                    trainer.launch_round(n)
+                if seg_tail:  # the round's last step, its segment all-reduces overlapping its own backward
+                    trainer.tail_fedavg(fcomm, rec)
+            m_l1 = fcomm.mark()
+            # the stall on the previous round's collective happened inside [m_l0, m_l1]: not local work
+            inner = prev_rec.stalls[stalls0:] if prev_rec is not None else []
+            inner = inner + (rec.stalls if seg_tail else [])
+            # ---- FedAvg ----------------------------------------------------------------------------------
+            if fedavg:
                 with profiling.range("fedavg"):
-                    if cfg.drop_prob > 0:
+                    if weighted:
                         rng = random.Random(cfg.seed * 1000003 + r * 8191 + ctx.rank)
-                        w = 0.0 if rng.random() < cfg.drop_prob else float(n_samples)
-                        weighted_fedavg_(model_flat(model), w, ctx)
-                    elif delayed is not None:
-                        delayed.boundary()
-                    elif tail:  # last local step + per-segment all-reduce overlapped with its backward
-                        trainer.tail_fedavg()
-                    else:
-                        fedavg_allreduce(comm, model)
-                _sync(dev)
-            t_c3 = time.perf_counter()
+                        w = 0.0 if rng.random() < cfg.drop_prob else float(cfg.batch_size * cfg.local_steps)
+                        fcomm.blocking(lambda: weighted_fedavg_(model_flat(model), w, ctx), rec)
+                    elif not seg_tail:
+                        fround.end_round(rec)
+            due = bool(cfg.ckpt_every) and (r + 1) % cfg.ckpt_every == 0
+            if due:
+                fround.finalize()  # checkpoints hold averaged weights (drains an in-flight all-reduce)
             avg_loss = trainer.avg_loss()
-            local_ms = (t_l1 - t_c1) * 1e3
-            comm_ms = ((t_c1 - t_c0) + (t_c3 - t_c2)) * 1e3
+            if due:
+                if ctx.rank == 0:
+                    mom = getattr(trainer, "mom", None)
+                    save_checkpoint(ckpt_path(cfg.ckpt_dir, r, cname), r, model, mom, cname, asdict(cfg))
+                save_rank_state(cfg.ckpt_dir, r, cname, ctx.rank, trainer)
+            recs.append((r, rec, m_l0, m_l1, inner, avg_loss, (time.perf_counter() - t_round0) * 1e3))
+        fround.finalize()
+        _sync(dev)
+        rows = []
+        for r, rec, m_l0, m_l1, inner, avg_loss, wall_ms in recs:
+            local_ms = m_l0.ms_to(m_l1) - sum(a.ms_to(b) for a, b in inner)
             row = RoundStats(config=cname, world_size=ctx.world_size, rank=ctx.rank, round_idx=r,
                              batch_size=cfg.batch_size, local_steps=cfg.local_steps, local_train_ms=local_ms,
-                             comm_ms=comm_ms, samples_per_s=n_samples / (local_ms / 1e3), avg_loss=avg_loss,
-                             comm_exposed_ms=comm_ms, round_wall_ms=(time.perf_counter() - t_round0) * 1e3,
-                             backend=backend, overlap=cfg.overlap if cfg.sync == "fedavg" else cfg.sync)
+                             comm_ms=rec.comm_ms(), samples_per_s=cfg.batch_size * cfg.local_steps / (local_ms / 1e3),
+                             avg_loss=avg_loss, comm_exposed_ms=rec.exposed_ms(), round_wall_ms=wall_ms,
+                             backend=backend, overlap=(cfg.overlap if not weighted else "none")
+                             if cfg.sync == "fedavg" else cfg.sync)
             rows.append(asdict(row))
             log.event("round", **asdict(row))
-            if cfg.ckpt_every and ctx.rank == 0 and (r + 1) % cfg.ckpt_every == 0:
-                mom = getattr(trainer, "mom", None)
-                save_checkpoint(ckpt_path(cfg.ckpt_dir, r, cname), r, model, mom, cname, asdict(cfg))
-        if delayed is not None:
-            delayed.finalize()
-            _sync(dev)
         if hasattr(trainer, "close"):
             trainer.close()
         gathered = comm.gather(rows, root=0)

@@ -63,6 +63,15 @@ class TorchLocalTrainer:
 
     run_round = run_steps
 
+    def prepare_round(self, n: int, reset_loss: bool = True) -> None:
+        """Eager steps draw their batch inside ``step``; only the loss window is reset here."""
+        if reset_loss:
+            self.loss_acc.zero_()
+            self._loss_steps = 0
+
+    def launch_round(self, n: int) -> None:
+        self.run_steps(n, reset_loss=False)
+
     def avg_loss(self) -> float:
         return float(self.loss_acc.item()) / max(1, self._loss_steps)
 

@@ -133,21 +133,28 @@ def run_overlap_gpu(model, batch_iter: Iterator, device, steps: int, rank: int, 
 
 
 def run_fused_gpu(model, x_gpu, y_gpu, device, steps: int, rank: int, batch_size: int, lr: float = 1e-2,
-                  seed: Optional[int] = None) -> BenchStats:
-    """G1 on the fused HIP step: all ``steps`` replayed from one native hipGraph, one sync at the end."""
+                  seed: Optional[int] = None, precision: str = "bf16") -> BenchStats:
+    """The fused HIP step (``precision`` bf16: G1, fp32: the native G0): all ``steps`` replayed from one native
+    hipGraph, one sync at the end.  The graph for exactly ``steps`` steps is captured and uploaded - and its
+    kernels warmed by a short untimed round whose updates are then rolled back - before the timing starts."""
     from ..ops.fused_tiny import FusedTinyTrainer
-    tr = FusedTinyTrainer(model, x_gpu, y_gpu, batch_size, steps, lr=lr, momentum=0.9, seed=seed)
-    tr.run_round(min(steps, 2))  # build + warm the graph outside the timing, like the reference's first batch
+    tr = FusedTinyTrainer(model, x_gpu, y_gpu, batch_size, steps, lr=lr, momentum=0.9, seed=seed,
+                          precision=precision)
+    w0 = tr.params.clone()
+    tr.prepare([steps])
+    tr.run_round(min(steps, 2))
     _sync(device)
+    tr.params.copy_(w0)
     tr.reset_momentum()
+    _sync(device)
     t0 = time.perf_counter()
     tr.run_round(steps)
     _sync(device)
     ms = (time.perf_counter() - t0) * 1e3
     tr.close()
     avg = ms / steps
-    return BenchStats("G1_fused_hip_graph", _world_size(), rank, batch_size, steps, 0.0, 0.0, avg, avg,
-                      batch_size / (avg / 1e3))
+    name = "G1_fused_hip_graph" if precision == "bf16" else "G0_fused_hip_fp32"
+    return BenchStats(name, _world_size(), rank, batch_size, steps, 0.0, 0.0, avg, avg, batch_size / (avg / 1e3))
 
 
 def run_stream_overlap(model, dl, device, steps: int, rank: int, batch_size: int, lr: float = 1e-2,

@@ -63,7 +63,8 @@ class ResNetEngineTrainer:
             self.engine.apply_update()
         self.steps_done += 1
 
-    def run_round(self, n: Optional[int] = None, reset_loss: bool = True) -> None:
+    def prepare_round(self, n: Optional[int] = None, reset_loss: bool = True) -> None:
+        """Draw the round's batches into the index table (no weights read: may overlap an all-reduce)."""
         n = self.S if n is None else n
         if n > self.S:
             raise ValueError(f"round of {n} steps > steps_per_round={self.S}")
@@ -72,34 +73,45 @@ class ResNetEngineTrainer:
         # the whole round's batches are drawn up front (a round ended by ``tail_fedavg`` uses the last row)
         self.sampler.fill(self.table)
         self.engine.reset_counter()
+
+    def launch_round(self, n: Optional[int] = None) -> None:
+        n = self.S if n is None else n
         for _ in range(n):
             self._step()
 
+    def run_round(self, n: Optional[int] = None, reset_loss: bool = True) -> None:
+        self.prepare_round(n, reset_loss)
+        self.launch_round(n)
+
     run_steps = run_round
 
-    def tail_fedavg(self) -> None:
+    def tail_fedavg(self, comm=None, rec=None) -> None:
         """Run one more local step whose update is applied and all-reduced segment by segment (exact FedAvg of
-        the post-step weights, communication overlapped with the remaining backward)."""
+        the post-step weights, communication overlapped with the remaining backward).
+
+        ``comm``/``rec`` (``parallel.overlap.FedAvgComm`` / ``CommRecord``): issue the collectives from the
+        timed comm stream so the round records the collectives' span and the compute stream's actual stall."""
         eng = self.engine
         if self.ctx is None or not self.ctx.distributed:
             self._step()
             return
+        if comm is None:
+            from ..parallel.overlap import CommRecord, FedAvgComm
+            comm, rec = FedAvgComm(self.ctx), CommRecord()
         first = eng._segments[0][0]
         eng._exec("fwd", 0, first)
-        works = []
+        pend = []
         for i, (b, e, lo, hi) in enumerate(eng._segments):
             eng._exec(f"seg{i}", b, e)
             eng.sgd_range(lo, hi)
-            works.append(allreduce_mean_(eng.flat[lo:hi], self.ctx, async_op=True))
+            pend.append(comm.issue(eng.flat[lo:hi], rec))
         eng._loss_steps += 1
         eng._steps_since_sync += 1
         # BN running statistics (not touched by SGD) are averaged too, like the flat all-reduce of ``none``
         buf = eng.flat[eng.space.param_numel:]
         if buf.numel():
-            works.append(allreduce_mean_(buf, self.ctx, async_op=True))
-        for w in works:
-            if w is not None:
-                w.wait()
+            pend.append(comm.issue(buf, rec))
+        comm.wait(pend, rec)
         self.steps_done += 1
 
     def avg_loss(self) -> float:

@@ -6,7 +6,7 @@ Launch one process per MI355X (RCCL over xGMI):
     torchrun --standalone --nproc-per-node 8 part3_fedavg_overlap_mpi_gpu.py --data-root data/shards \
         --batch-size 256 --rounds 5 --local-steps 50 --config both --max-windows 20000
 ``mpiexec -n 8`` / ``srun`` also work (launcher env shim).  On a CPU box the same command runs with gloo.
-New flags: --kernel-backend {auto,fused,torch} --amp-dtype {bf16,fp16,none} --overlap {none,delayed}
+New flags: --kernel-backend {auto,fused,torch} --amp-dtype {bf16,fp16,none} --overlap {none,tail,delayed}
 --sync {fedavg,none,ddp} --no-bcast-every-round --ckpt-every N --resume --drop-prob p
 --synthetic-windows N --labels {zeros,parity} --config-file cfg.yaml
 """

@@ -6,7 +6,8 @@ Module_3/part3_mpi_gpu_train.py).
         --data-root data/shards
     mpiexec -n 2 python part3_mpi_gpu_train.py ...     (launcher env shim, no mpi4py needed)
 
-Runs G0 (fp32 baseline), G1 (AMP + side-stream lookahead) and, on a GPU, G1 on the fused HIP step; with
+Runs G0 (fp32 baseline), G1 (AMP + side-stream lookahead) and, on a GPU, G0 and G1 on the fused HIP step
+(``G0_fused_hip_fp32``: exact fp32 MFMA; ``G1_fused_hip_graph``: bf16); with
 ``--loader stream`` also the pinned-DataLoader + H2D-stream double-buffer configuration.  Rank 0 appends
 BenchStats rows to ``results/part3_mpi_cuda_results.csv`` and prints per-config means over ranks.
 """
@@ -71,9 +72,10 @@ def main(argv=None):
                                                cfg.steps, ctx.rank, cfg.batch_size, amp_dtype=amp,
                                                log_every=log_every)))
             if cfg.kernel_backend in ("auto", "fused"):
-                torch.manual_seed(cfg.seed)
-                rows.append(asdict(run_fused_gpu(TinyECG().to(dev), x_gpu, y_gpu, dev, cfg.steps, ctx.rank,
-                                                 cfg.batch_size, seed=cfg.seed + ctx.rank)))
+                for prec in ("fp32", "bf16"):  # native G0 (exact fp32 MFMA) and native G1 (bf16)
+                    torch.manual_seed(cfg.seed)
+                    rows.append(asdict(run_fused_gpu(TinyECG().to(dev), x_gpu, y_gpu, dev, cfg.steps, ctx.rank,
+                                                     cfg.batch_size, seed=cfg.seed + ctx.rank, precision=prec)))
             if cfg.loader == "stream" and local_shards:
                 dl, _ = make_dataloader(local_shards, cfg.batch_size, cfg.max_windows, num_workers=2,
                                         pin_memory=True)

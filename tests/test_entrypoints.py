@@ -70,7 +70,8 @@ def test_checkpoint_and_resume(tmp_path):
             "--batch-size", "32", "--local-steps", "2", "--config", "G1", "--ckpt-every", "1", "--ckpt-dir", str(ck),
             "--results-csv", str(tmp_path / "r.csv"), "--quiet"]
     _run(args + ["--rounds", "2"], cwd=str(tmp_path))
-    assert sorted(os.listdir(ck)) == ["fedavg_G1_round00000.pt", "fedavg_G1_round00001.pt"]
+    assert sorted(os.listdir(ck)) == ["fedavg_G1_round00000.pt", "fedavg_G1_round00000.rank0.pt",
+                                      "fedavg_G1_round00001.pt", "fedavg_G1_round00001.rank0.pt"]
     _run(args + ["--rounds", "4", "--resume"], cwd=str(tmp_path))
     rows = list(csv.DictReader(open(tmp_path / "r.csv")))
     assert [int(r["round_idx"]) for r in rows] == [0, 1, 2, 3]
@@ -106,3 +107,60 @@ def test_module_benches_cpu(tmp_path):
                                            "A3_contig_pinned_nb", "A4_LABL"]
     _run([sys.executable, os.path.join(ROOT, "plot_results.py"), "--results-dir", str(tmp_path)], cwd=str(tmp_path))
     assert os.path.exists(tmp_path / "throughput_vs_batch.png")
+
+
+def _fedavg_world2(d, extra, rounds, csv_name):
+    return _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                 "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+                 os.path.join(ROOT, "part3_fedavg_overlap_mpi_gpu.py"), "--synthetic-windows", "300",
+                 "--rounds", str(rounds), "--local-steps", "3", "--batch-size", "32", "--config", "G1",
+                 "--results-csv", str(d / csv_name), "--quiet", *extra], cwd=str(d))
+
+
+def _final_weights(ck_dir, rnd):
+    import torch
+    from crossscale_ecg.utils.ckpt import load_checkpoint
+    st = load_checkpoint(os.path.join(ck_dir, f"fedavg_G1_round{rnd:05d}.pt"))
+    return torch.cat([v.flatten() for v in st["model"].values()])
+
+
+def test_tail_overlap_equals_none_and_measures_exposure(tmp_path):
+    """--overlap tail (async all-reduce under the next round's batch preparation) is exact FedAvg: bitwise the
+    same weights as --overlap none; comm_ms and comm_exposed_ms are separately measured columns."""
+    import torch
+    import crossscale_ecg  # noqa: F401
+    for mode in ("none", "tail"):
+        _fedavg_world2(tmp_path, ["--overlap", mode, "--no-bcast-every-round", "--ckpt-every", "3",
+                                  "--ckpt-dir", str(tmp_path / f"ck_{mode}")], 3, f"{mode}.csv")
+    assert torch.equal(_final_weights(tmp_path / "ck_none", 2), _final_weights(tmp_path / "ck_tail", 2))
+    rows = list(csv.DictReader(open(tmp_path / "tail.csv")))
+    assert {r["overlap"] for r in rows} == {"tail"}
+    for r in rows:
+        comm, exposed = float(r["comm_ms"]), float(r["comm_exposed_ms"])
+        assert comm >= 0 and exposed >= 0
+    assert any(float(r["comm_ms"]) != float(r["comm_exposed_ms"]) for r in rows)
+
+
+def test_resume_only_rank0_has_checkpoint(tmp_path):
+    """Node-local checkpoint dirs: rank 0 resolves the round and broadcasts it; a rank whose directory is empty
+    resumes at the same round (momentum from zero) instead of desynchronising the collectives."""
+    import shutil
+    ck = str(tmp_path / "ck{rank}")
+    _fedavg_world2(tmp_path, ["--ckpt-every", "1", "--ckpt-dir", ck], 2, "a.csv")
+    assert os.path.exists(tmp_path / "ck0" / "fedavg_G1_round00001.pt")
+    assert os.path.exists(tmp_path / "ck1" / "fedavg_G1_round00001.rank1.pt")
+    shutil.rmtree(tmp_path / "ck1")
+    _fedavg_world2(tmp_path, ["--ckpt-every", "1", "--ckpt-dir", ck, "--resume"], 4, "a.csv")
+    rows = list(csv.DictReader(open(tmp_path / "a.csv")))
+    assert sorted((int(r["rank"]), int(r["round_idx"])) for r in rows) == [(k, i) for k in (0, 1) for i in range(4)]
+
+
+def test_resume_continues_the_interrupted_run(tmp_path):
+    """Checkpoint + resume (weights, per-rank momentum, sampler position, RNG) reproduces the uninterrupted run
+    bit for bit."""
+    import torch
+    import crossscale_ecg  # noqa: F401
+    _fedavg_world2(tmp_path, ["--ckpt-every", "1", "--ckpt-dir", str(tmp_path / "full")], 4, "f.csv")
+    _fedavg_world2(tmp_path, ["--ckpt-every", "1", "--ckpt-dir", str(tmp_path / "part")], 2, "p.csv")
+    _fedavg_world2(tmp_path, ["--ckpt-every", "1", "--ckpt-dir", str(tmp_path / "part"), "--resume"], 4, "p.csv")
+    assert torch.equal(_final_weights(tmp_path / "full", 3), _final_weights(tmp_path / "part", 3))
