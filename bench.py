@@ -10,7 +10,9 @@ rounds of ``--local-steps`` steps; EVERY round - including a trailing partial on
 all-reduce (one RCCL ``all_reduce(AVG)`` of the flat weights, reference part3_fedavg_overlap_mpi_gpu.py:
 209-211), so the timed region always contains communication.  W warmup steps (same round plan), then
 every hipGraph the timed plan needs is captured and uploaded, then exactly K timed steps bracketed by
-barrier + synchronize; value = N * B * K / max-over-ranks(elapsed) (whole-job samples/s).
+barrier + synchronize; value = N * B * K / max-over-ranks(elapsed) (whole-job samples/s).  Each round's
+batch indices are drawn while the previous round computes (the first timed round's behind the last warmup
+round) and copied into the step table by the round graph's first node.
 
 Launch: ``python bench.py --gpus N`` with N > 1 and no launcher environment starts N ranks itself
 (``torch.distributed.run`` as a child process, one rank per GPU); the parent never touches the GPU.
@@ -111,15 +113,15 @@ class FedAvgRunner:
         self.syncs = 0
         self._pending = None
 
-    def run(self, plan):
-        for n in plan:
-            if self._pending is not None:  # tail: next batches prepared while the all-reduce is in flight
-                self.trainer.prepare_round(n, reset_loss=False)
+    def run(self, plan, then=None):
+        """``then``: size of the round that will follow ``plan`` (its batches are staged behind the last round)."""
+        for i, n in enumerate(plan):
+            next_n = plan[i + 1] if i + 1 < len(plan) else then
+            self.trainer.prepare_round(n, reset_loss=False)  # no-op when the previous round staged it
+            if self._pending is not None:  # tail: the next batches were prepared while the all-reduce ran
                 self._pending.wait()
                 self._pending = None
-                self.trainer.launch_round(n)
-            else:
-                self.trainer.run_round(n, reset_loss=False)
+            self.trainer.launch_round(n, next_n)
             if self.overlap == "tail":
                 self._pending = self.allreduce(self.flat, self.ctx, async_op=True)
             else:
@@ -265,7 +267,7 @@ def main(argv=None):
 
     timed_plan = round_plan(a.steps, S)
     if a.warmup > 0:
-        runner.run(round_plan(a.warmup, S))
+        runner.run(round_plan(a.warmup, S), then=timed_plan[0])
     if hasattr(trainer, "prepare"):  # capture + upload every graph the timed plan replays, outside the timing
         trainer.prepare(sorted(set(timed_plan)))
     runner.syncs = 0

@@ -5,13 +5,15 @@ Reference: Module_2/benchmark_part_2.py (grid B in {64,128,256,512} x K in {3,5,
 Module_2/train_cpu_openmp.py (thread scaling at K=32).
 
 Two comparisons are produced:
-  * ``part2_hip_results.csv``    - HIP ``conv1d_batch_hip`` vs ``torch.nn.Conv1d`` on the MI355X (MIOpen).
-    Three timings per cell: ``*_call_ms`` = the reference's single call + device sync (host wall clock,
-    dominated by launch + sync latency), ``*_ms`` = back-to-back calls between syncs (host per-call cost,
-    the number the headline speedup uses), ``*_ev_ms`` = hipEvent device time per call.  Every cell is
-    also checked against an fp64 reference (``max_abs_err``), which the reference never did.
+  * ``part2_hip_results.csv``    - HIP conv1d vs ``torch.nn.Conv1d`` on the MI355X (MIOpen).  Three timings per
+    cell.  HEADLINE ``speedup_med`` = the reference's metric: ``time_once`` (3 warm-up calls + ONE timed call,
+    host wall clock until the result is ready; the HIP side is the blocking ``conv1d_batch_hip_sync`` call,
+    the torch side ``conv(x)`` + ``torch.cuda.synchronize()``), median of 15 trials.  Secondary:
+    ``speedup_burst`` (50 back-to-back calls between syncs, host per-call cost) and ``speedup_ev`` (hipEvent
+    device time per call).  Every cell is checked against an fp64 reference (``max_abs_err``).
   * ``part2_openmp_results.csv`` - the C++ OpenMP/AVX kernel (reference C ABI) vs CPU ``nn.Conv1d`` on the
-    host CPU: the reference's exact like-for-like experiment.
+    host CPU: the reference's exact like-for-like experiment, best-vs-best over a thread sweep (each side at
+    the thread count where its median is lowest; ``nthreads`` / ``torch_threads`` record the winners).
 """
 from __future__ import annotations
 
@@ -95,6 +97,9 @@ def bench_pair_gpu(bs: int, K: int, rng: np.random.Generator, trials: int = TRIA
     def hip_step():
         conv1d_valid(xt, wt, backend="hip", out=out)
 
+    def hip_call():  # single-call path: returns when the output is complete
+        conv1d_valid(xt, wt, backend="hip", out=out, blocking=True)
+
     hip_step()
     sync()
     ref = conv1d_valid_reference(x_np, w_np)
@@ -102,7 +107,7 @@ def bench_pair_gpu(bs: int, K: int, rng: np.random.Generator, trials: int = TRIA
     t_call, h_call, t_b, h_b, t_e, h_e = [], [], [], [], [], []
     raw = []
     for _ in range(trials):
-        tc, hc = time_once(torch_step, sync=sync), time_once(hip_step, sync=sync)
+        tc, hc = time_once(torch_step, sync=sync), time_once(hip_call, sync=sync)
         t_call.append(tc)
         h_call.append(hc)
         raw.append((tc, hc))
@@ -111,18 +116,50 @@ def bench_pair_gpu(bs: int, K: int, rng: np.random.Generator, trials: int = TRIA
         t_e.append(time_events(torch_step, inner))
         h_e.append(time_events(hip_step, inner))
     row = {"batch_size": bs, "kernel_size": K, "backend": "hip"}
-    row.update(_agg("torch_call_ms", t_call))
-    row.update(_agg("hip_call_ms", h_call))
-    row.update(_agg("torch_ms", t_b))
-    row.update(_agg("hip_ms", h_b))
+    row.update(_agg("torch_ms", t_call))  # reference metric (time_once)
+    row.update(_agg("hip_ms", h_call))
+    row.update(_agg("torch_burst_ms", t_b))
+    row.update(_agg("hip_burst_ms", h_b))
     row["torch_ev_ms"] = float(stats.median(t_e))
     row["hip_ev_ms"] = float(stats.median(h_e))
     row["torch_sps"] = bs / (row["torch_ms_median"] / 1e3)
     row["hip_sps"] = bs / (row["hip_ms_median"] / 1e3)
     row["speedup_med"] = row["torch_ms_median"] / row["hip_ms_median"]
-    row["speedup_call_med"] = row["torch_call_ms_median"] / row["hip_call_ms_median"]
+    row["speedup_burst"] = row["torch_burst_ms_median"] / row["hip_burst_ms_median"]
     row["speedup_ev"] = row["torch_ev_ms"] / row["hip_ev_ms"]
     row["max_abs_err"] = err
+    return row, raw
+
+
+def thread_sweep(max_threads: int):
+    t, out = 1, []
+    while t <= max_threads:
+        out.append(t)
+        t *= 2
+    if out[-1] != max_threads:
+        out.append(max_threads)
+    return out
+
+
+def bench_pair_cpu_best(bs: int, K: int, rng: np.random.Generator, max_threads: int, trials: int = TRIALS):
+    """Best-vs-best on the host: each side at the thread count (1, 2, 4, ... max) with its lowest median."""
+    best_t = best_o = None
+    state = rng.bit_generator.state
+    for th in thread_sweep(max_threads):
+        rng.bit_generator.state = state  # identical data for every thread count
+        torch.set_num_threads(th)
+        row, raw = bench_pair_cpu(bs, K, rng, th, trials)
+        if best_t is None or row["torch_ms_median"] < best_t[0]["torch_ms_median"]:
+            best_t = (row, raw, th)
+        if best_o is None or row["omp_ms_median"] < best_o[0]["omp_ms_median"]:
+            best_o = (row, raw, th)
+    row = {"batch_size": bs, "kernel_size": K, "nthreads": best_o[2], "torch_threads": best_t[2]}
+    for k in ("torch_ms_median", "torch_ms_mean", "torch_ms_std", "torch_ms_p95", "torch_sps"):
+        row[k] = best_t[0][k]
+    for k in ("omp_ms_median", "omp_ms_mean", "omp_ms_std", "omp_ms_p95", "omp_sps", "max_abs_err"):
+        row[k] = best_o[0][k]
+    row["speedup_med"] = row["torch_ms_median"] / row["omp_ms_median"]
+    raw = [(a, b) for (a, _), (_, b) in zip(best_t[1], best_o[1])]
     return row, raw
 
 
@@ -159,10 +196,10 @@ def bench_pair_cpu(bs: int, K: int, rng: np.random.Generator, nthreads: int, tri
     return row, list(zip(tm, om))
 
 
-HIP_COLUMNS = ["batch_size", "kernel_size", "backend", "torch_call_ms_median", "hip_call_ms_median",
-               "torch_ms_median", "torch_ms_mean", "torch_ms_std", "torch_ms_p95", "hip_ms_median", "hip_ms_mean",
-               "hip_ms_std", "hip_ms_p95", "torch_ev_ms", "hip_ev_ms", "torch_sps", "hip_sps", "speedup_med",
-               "speedup_call_med", "speedup_ev", "max_abs_err"]
+HIP_COLUMNS = ["batch_size", "kernel_size", "backend", "torch_ms_median", "torch_ms_mean", "torch_ms_std",
+               "torch_ms_p95", "hip_ms_median", "hip_ms_mean", "hip_ms_std", "hip_ms_p95", "torch_sps", "hip_sps",
+               "speedup_med", "torch_burst_ms_median", "hip_burst_ms_median", "speedup_burst", "torch_ev_ms",
+               "hip_ev_ms", "speedup_ev", "max_abs_err"]
 
 
 def run_part2(results_dir: str = "results", gpu: bool = True, cpu: bool = True, trials: int = TRIALS,
@@ -181,9 +218,9 @@ def run_part2(results_dir: str = "results", gpu: bool = True, cpu: bool = True, 
                 raw += [{"batch_size": bs, "kernel_size": K, "trial": i, "torch_ms": a, "omp_ms": b}
                         for i, (a, b) in enumerate(r)]
                 if verbose:
-                    print(f"[HIP] B={bs} K={K}: torch {row['torch_ms_median'] * 1e3:.1f} us  hip "
+                    print(f"[HIP] B={bs} K={K}: single call torch {row['torch_ms_median'] * 1e3:.1f} us  hip "
                           f"{row['hip_ms_median'] * 1e3:.1f} us  speedup {row['speedup_med']:.2f}x "
-                          f"(single-call {row['speedup_call_med']:.2f}x, device {row['speedup_ev']:.2f}x) "
+                          f"(burst {row['speedup_burst']:.2f}x, device {row['speedup_ev']:.2f}x) "
                           f"err {row['max_abs_err']:.1e}", flush=True)
         safe_write_csv(rows, os.path.join(results_dir, "part2_hip_results.csv"), HIP_COLUMNS)
         safe_write_csv(raw, os.path.join(results_dir, "part2_hip_results_raw.csv"), PART2_RAW_COLUMNS)
@@ -194,14 +231,16 @@ def run_part2(results_dir: str = "results", gpu: bool = True, cpu: bool = True, 
         rows, raw = [], []
         for bs in batch_sizes:
             for K in kernel_sizes:
-                row, r = bench_pair_cpu(bs, K, rng, nthreads, trials)
+                row, r = bench_pair_cpu_best(bs, K, rng, nthreads, trials)
                 rows.append(row)
                 raw += [{"batch_size": bs, "kernel_size": K, "trial": i, "torch_ms": a, "omp_ms": b}
                         for i, (a, b) in enumerate(r)]
                 if verbose:
-                    print(f"[CPU] B={bs} K={K}: torch {row['torch_ms_median']:.3f} ms  omp "
-                          f"{row['omp_ms_median']:.3f} ms  speedup {row['speedup_med']:.2f}x", flush=True)
-        safe_write_csv(rows, os.path.join(results_dir, "part2_openmp_results.csv"), PART2_COLUMNS + ["max_abs_err"])
+                    print(f"[CPU] B={bs} K={K}: torch {row['torch_ms_median']:.3f} ms ({row['torch_threads']} thr)  "
+                          f"omp {row['omp_ms_median']:.3f} ms ({row['nthreads']} thr)  speedup "
+                          f"{row['speedup_med']:.2f}x", flush=True)
+        safe_write_csv(rows, os.path.join(results_dir, "part2_openmp_results.csv"),
+                       PART2_COLUMNS + ["torch_threads", "max_abs_err"])
         safe_write_csv(raw, os.path.join(results_dir, "part2_openmp_results_raw.csv"), PART2_RAW_COLUMNS)
         out["cpu"] = rows
     return out

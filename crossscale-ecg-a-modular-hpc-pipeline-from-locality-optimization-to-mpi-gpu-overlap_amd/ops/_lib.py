@@ -70,14 +70,14 @@ def _bind_kernels(lib: C.CDLL) -> None:
     _sig(lib, "ecg_tiny_train_step", [vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, vp, f32, f32, f32, i32,
                                       vp, vp, i32, vp])
     _sig(lib, "ecg_round_graph_create", [C.POINTER(vp), vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, i32, vp,
-                                         f32, f32, f32, i32, vp, vp, i32])
+                                         f32, f32, f32, i32, vp, vp, i32, vp])
     _sig(lib, "ecg_tiny_step_grads_twice", [vp, i32, i64, vp, vp, vp, i32, vp, i32, i32, f32, i32, vp])
     _sig(lib, "ecg_tiny_round_ws_bytes", [i32, i32], i64)
     _sig(lib, "ecg_tiny_round_fits", [i32, i32, i32, i32])
     _sig(lib, "ecg_tiny_train_round", [vp, i32, i64, vp, vp, vp, vp, i32, i32, i32, vp, f32, f32, f32, i32, vp, i64,
                                        vp, i32, vp, vp])
     _sig(lib, "ecg_round_graph_create_persistent", [C.POINTER(vp), vp, i32, i64, vp, vp, vp, vp, i32, i32, i32, vp,
-                                                    f32, f32, f32, i32, vp, i64, vp, i32])
+                                                    f32, f32, f32, i32, vp, i64, vp, i32, vp])
     _sig(lib, "ecg_tiny_force_waves", [i32])
     _sig(lib, "ecg_tiny_ctl_ints", [])
     _sig(lib, "ecg_tiny_gslab_rows", [])
@@ -86,6 +86,12 @@ def _bind_kernels(lib: C.CDLL) -> None:
     _sig(lib, "ecg_round_graph_destroy", [vp])
     _sig(lib, "ecg_round_graph_upload", [vp, vp])
     _sig(lib, "conv1d_batch_hip", [vp, vp, vp, i32, i32, i32, vp])
+    _sig(lib, "conv1d_batch_hip_sync", [vp, vp, vp, i32, i32, i32, vp])
+    _sig(lib, "conv1d_valid_dgrad_hip", [vp, vp, vp, i32, i32, i32, vp])
+    _sig(lib, "conv1d_valid_dgrad_hip_bf16", [vp, vp, vp, i32, i32, i32, vp])
+    _sig(lib, "conv1d_valid_wgrad_ws_floats", [i32, i32, i32], i64)
+    _sig(lib, "conv1d_valid_wgrad_hip", [vp, vp, vp, vp, i64, i32, i32, i32, vp])
+    _sig(lib, "conv1d_valid_wgrad_hip_bf16", [vp, vp, vp, vp, i64, i32, i32, i32, vp])
     _sig(lib, "conv1d_batch_hip_bf16", [vp, vp, vp, i32, i32, i32, vp])
     _sig(lib, "ecg_sgd_flat", [vp, vp, vp, i64, f32, f32, f32, f32, i32, i32, f32, vp, vp])
     _sig(lib, "ecg_gather_rows_f32", [vp, i64, i32, vp, i32, vp, i64, i32, f32, vp])

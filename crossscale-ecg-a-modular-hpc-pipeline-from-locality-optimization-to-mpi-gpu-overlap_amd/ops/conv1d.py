@@ -1,6 +1,9 @@
-"""Single-channel valid conv1d (the Module-2 op) on three backends.
+"""Single-channel valid conv1d (the Module-2 op) on three backends, plus its HIP backward.
 
-* ``hip``   - ``conv1d_batch_hip`` (csrc/kernels/conv1d_valid.hip), fp32 or bf16, async on the torch stream.
+* ``hip``   - ``conv1d_batch_hip`` (csrc/kernels/conv1d_valid.hip), fp32 or bf16, async on the torch stream;
+              ``blocking=True`` uses ``conv1d_batch_hip_sync`` (returns when the output is complete, like the
+              reference's CPU kernel) - the single-call path the Module-2 ``time_once`` metric measures.
+              ``conv1d_valid_fn`` is the differentiable version (HIP dgrad + deterministic two-pass wgrad).
 * ``cpu``   - ``conv1d_batch_omp_simd`` (csrc/cpu/conv1d_cpu.cpp), the reference C ABI
               (Module_2/conv1d_openmp_simd.c:21-28) with OpenMP + AVX2/AVX-512.
 * ``torch`` - ``F.conv1d`` (MIOpen on the GPU / oneDNN on the CPU) — the baseline the paper compares to
@@ -31,11 +34,12 @@ def _as_2d(x: torch.Tensor) -> torch.Tensor:
     return x.contiguous()
 
 
-_HIP_FNS = {}  # dtype -> bound C function (after the first call)
+_HIP_FNS = {}  # dtype (or "sync") -> bound C function (after the first call)
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 
-def _conv1d_hip_fast(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None) -> torch.Tensor | None:
+def _conv1d_hip_fast(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None,
+                     blocking: bool = False) -> torch.Tensor | None:
     """Per-call fast path of the hip backend (the Module-2 benchmark times single calls, so Python overhead is
     part of the measured number, as the torch side's dispatch is part of its): no intermediate tensors, one
     raw-stream query.  Returns None when the operands need the general path (conversions, copies, checks)."""
@@ -45,8 +49,9 @@ def _conv1d_hip_fast(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None)
         return None
     if not _HIP_FNS:
         lib = _lib.kernels()  # raises if the HIP library is missing: no silent fallback on a GPU tensor
-        _HIP_FNS.update({torch.float32: lib.conv1d_batch_hip, torch.bfloat16: lib.conv1d_batch_hip_bf16})
-    fn = _HIP_FNS.get(x.dtype)
+        _HIP_FNS.update({torch.float32: lib.conv1d_batch_hip, torch.bfloat16: lib.conv1d_batch_hip_bf16,
+                         "sync": lib.conv1d_batch_hip_sync})
+    fn = _HIP_FNS.get("sync" if blocking and x.dtype == torch.float32 else x.dtype)
     if fn is None:
         return None
     B, L, K = x.shape[0], x.shape[-1], w.numel()
@@ -60,14 +65,18 @@ def _conv1d_hip_fast(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None)
     st = fn(x.data_ptr(), w.data_ptr(), out.data_ptr(), B, L, K, _raw_stream(x.device.index))
     if st:
         _lib.check(st, "conv1d_batch_hip")
+    if blocking and x.dtype != torch.float32:
+        torch.cuda.current_stream(x.device).synchronize()
     return out if out.dim() == d else out.view((B, 1, outL) if d == 3 else (B, outL))
 
 
 def conv1d_valid(x: torch.Tensor, w: torch.Tensor, backend: str = "auto", out: torch.Tensor | None = None,
-                 nthreads: int | None = None) -> torch.Tensor:
-    """y[b, i] = sum_k x[b, i+k] w[k] for x [B, L] (or [B,1,L]), w [K] -> y [B, L-K+1] (same rank as x)."""
+                 nthreads: int | None = None, blocking: bool = False) -> torch.Tensor:
+    """y[b, i] = sum_k x[b, i+k] w[k] for x [B, L] (or [B,1,L]), w [K] -> y [B, L-K+1] (same rank as x).
+
+    ``blocking`` (hip): return only when the output is complete (one native launch + stream wait)."""
     if backend == "hip" or (backend == "auto" and x.is_cuda):
-        y = _conv1d_hip_fast(x, w, out)
+        y = _conv1d_hip_fast(x, w, out, blocking)
         if y is not None:
             return y
     keep3 = x.dim() == 3
@@ -99,6 +108,8 @@ def conv1d_valid(x: torch.Tensor, w: torch.Tensor, backend: str = "auto", out: t
         else:
             raise ValueError(f"unsupported dtype {x2.dtype}")
         _lib.check(st, "conv1d_batch_hip")
+        if blocking:
+            torch.cuda.current_stream(x2.device).synchronize()
         return out.unsqueeze(1) if keep3 else out
     if backend == "cpu":
         if x2.is_cuda or x2.dtype != torch.float32:
@@ -106,6 +117,55 @@ def conv1d_valid(x: torch.Tensor, w: torch.Tensor, backend: str = "auto", out: t
         y = torch.from_numpy(run_omp_conv(x2.numpy(), w1.float().numpy(), nthreads))
         return y.unsqueeze(1) if keep3 else y
     raise ValueError(f"unknown backend {backend!r}")
+
+
+def conv1d_valid_backward(x: torch.Tensor, w: torch.Tensor, dy: torch.Tensor, need_dx: bool = True,
+                          need_dw: bool = True):
+    """HIP backward of ``conv1d_valid``: (dx [B, L] in x's dtype, dw [K] fp32) from dy [B, L-K+1]."""
+    x2, dy2 = _as_2d(x), _as_2d(dy).to(x.dtype).contiguous()
+    w1 = w.reshape(-1).to(device=x2.device, dtype=torch.float32).contiguous()
+    B, L = x2.shape
+    K = w1.numel()
+    if dy2.shape != (B, L - K + 1):
+        raise ValueError(f"dy must be [{B}, {L - K + 1}], got {tuple(dy2.shape)}")
+    bf = x2.dtype == torch.bfloat16
+    if x2.dtype not in (torch.float32, torch.bfloat16) or not x2.is_cuda:
+        raise ValueError("conv1d_valid_backward needs a CUDA fp32/bf16 tensor")
+    lib = _lib.kernels()
+    stream = _lib.stream_ptr(x2.device)
+    dx = dw = None
+    if need_dx:
+        dx = torch.empty_like(x2)
+        fn = lib.conv1d_valid_dgrad_hip_bf16 if bf else lib.conv1d_valid_dgrad_hip
+        _lib.check(fn(dy2.data_ptr(), w1.data_ptr(), dx.data_ptr(), B, L, K, stream), "conv1d_valid_dgrad_hip")
+    if need_dw:
+        n = int(lib.conv1d_valid_wgrad_ws_floats(B, L, K))
+        ws = torch.empty(n, dtype=torch.float32, device=x2.device)
+        dw = torch.empty(K, dtype=torch.float32, device=x2.device)
+        fn = lib.conv1d_valid_wgrad_hip_bf16 if bf else lib.conv1d_valid_wgrad_hip
+        _lib.check(fn(x2.data_ptr(), dy2.data_ptr(), dw.data_ptr(), ws.data_ptr(), n, B, L, K, stream),
+                   "conv1d_valid_wgrad_hip")
+    return dx, dw
+
+
+class _Conv1dValidFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return conv1d_valid(x, w.detach().reshape(-1).float(), backend="hip")
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx, dw = conv1d_valid_backward(x, w, dy, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        if dx is not None and x.dim() == 3:
+            dx = dx.unsqueeze(1)
+        return dx, (dw.view_as(w).to(w.dtype) if dw is not None else None)
+
+
+def conv1d_valid_fn(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """Differentiable single-channel valid conv1d on the HIP kernels (forward, dgrad, wgrad)."""
+    return _Conv1dValidFn.apply(x, w)
 
 
 def run_omp_conv(x_np: np.ndarray, w_np: np.ndarray, nthreads: int | None = None,

@@ -143,6 +143,10 @@ class FusedTinyTrainer:
         self.slab = torch.empty((self.B, self.stride), dtype=torch.float32, device=self.device)
         self.loss_acc = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.idx_table = torch.zeros((self.S, self.B), dtype=torch.int32, device=self.device)
+        # batches of the NEXT round are drawn into idx_stage while the current round computes; each round graph
+        # starts with a device copy idx_stage -> idx_table (csrc capture_round)
+        self.idx_stage = torch.zeros((self.S, self.B), dtype=torch.int32, device=self.device)
+        self._staged: Optional[int] = None  # rows staged for the next round (None: nothing staged)
         self.sampler = DeviceIndexSampler(self.x.shape[0], self.B, self.device, seed=seed)
         self.use_graph = use_graph
         self._graphs = {}  # n_steps -> native hipGraphExec handle
@@ -182,13 +186,14 @@ class FusedTinyTrainer:
                 C.byref(g), self.x.data_ptr(), self.x.shape[1], self.x.stride(0), self.idx_table.data_ptr(),
                 self.y32.data_ptr(), self.params.data_ptr(), self.mom.data_ptr(), self.nc, self.B, n,
                 self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd, int(self.nesterov), self.ws.data_ptr(),
-                self.ws.numel(), self.status.data_ptr(), self.prec)
+                self.ws.numel(), self.status.data_ptr(), self.prec, self.idx_stage.data_ptr())
         else:
             st = lib.ecg_round_graph_create(C.byref(g), self.x.data_ptr(), self.x.shape[1], self.x.stride(0),
                                             self.idx_table.data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
                                             self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
                                             n, self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd,
-                                            int(self.nesterov), *self._fuse_ptrs(), self.prec)
+                                            int(self.nesterov), *self._fuse_ptrs(), self.prec,
+                                            self.idx_stage.data_ptr())
         _lib.check(st, "ecg_round_graph_create")
         self._graphs[n] = g
         return g
@@ -235,17 +240,21 @@ class FusedTinyTrainer:
             raise _lib.NativeError(f"persistent TinyECG round gave up: {_lib.ROUND_GIVE_UP.get(code, code)}")
 
     def prepare(self, sizes) -> None:
-        """Capture and upload the round graphs of every step count in ``sizes`` (no kernel runs), so a later
-        ``run_round(n)`` for those sizes only replays."""
+        """Capture, upload and warm every round graph whose step count is in ``sizes``, so a later round of that
+        size only replays.  The warm-up replay is rolled back (weights, momentum, loss, staged batches are
+        restored): it leaves the training state exactly as it found it."""
         if not self.use_graph:
             return
         lib = _lib.kernels()
+        sizes = [self._check_n(n) for n in sizes]
+        snap = [t.clone() for t in (self.params, self.mom, self.loss_acc, self.idx_stage, self.status)]
+        stream = _lib.stream_ptr(self.device)
         for n in sizes:
-            n = int(n)
-            if not 0 < n <= self.S:
-                raise ValueError(f"round size {n} not in [1, {self.S}]")
-            _lib.check(lib.ecg_round_graph_upload(self._graph_for(n), _lib.stream_ptr(self.device)),
-                       "ecg_round_graph_upload")
+            g = self._graph_for(n)
+            _lib.check(lib.ecg_round_graph_upload(g, stream), "ecg_round_graph_upload")
+            _lib.check(lib.ecg_round_graph_launch(g, stream), "ecg_round_graph_launch")
+        for t, v in zip((self.params, self.mom, self.loss_acc, self.idx_stage, self.status), snap):
+            t.copy_(v)
         torch.cuda.synchronize(self.device)
 
     def _check_n(self, n_steps: Optional[int]) -> int:
@@ -254,34 +263,52 @@ class FusedTinyTrainer:
             raise ValueError(f"n_steps must be in [1, {self.S}]")
         return n
 
+    def stage(self, n_steps: Optional[int] = None) -> None:
+        """Draw the next round's ``n_steps`` batches into the staging table (enqueued on the current stream: it
+        runs after the rounds already enqueued, which read the staging table at their start)."""
+        n = self._check_n(n_steps)
+        self.sampler.fill(self.idx_stage[:n])
+        self._staged = n
+
     def prepare_round(self, n_steps: Optional[int] = None, reset_loss: bool = True) -> None:
-        """Batch preparation of a round (index-table fill on the current stream); reads no weights, so it can run
-        while the previous round's FedAvg all-reduce is still in flight (``--overlap tail``)."""
+        """Batch preparation of a round (unless ``launch_round(..., next_n=n)`` already staged it); reads no
+        weights, so it can run while the previous round's FedAvg all-reduce is in flight (``--overlap tail``)."""
         n = self._check_n(n_steps)
         if reset_loss:
             self.loss_acc.zero_()
             self._loss_steps = 0
-        self.sampler.fill(self.idx_table[:n])
+        if self._staged != n:
+            if self._staged is not None:
+                raise RuntimeError(f"{self._staged} rows are staged for the next round, not {n}")
+            self.stage(n)
 
-    def run_round(self, n_steps: Optional[int] = None, reset_loss: bool = True) -> None:
-        """Enqueue ``n_steps`` (default ``steps_per_round``) local SGD steps on the current stream (async)."""
+    def run_round(self, n_steps: Optional[int] = None, reset_loss: bool = True, next_n: Optional[int] = None) -> None:
+        """Enqueue ``n_steps`` (default ``steps_per_round``) local SGD steps on the current stream (async);
+        ``next_n``: also stage the following round's batches behind this round."""
         self.prepare_round(n_steps, reset_loss)
-        self.launch_round(n_steps)
+        self.launch_round(n_steps, next_n)
 
-    def launch_round(self, n_steps: Optional[int] = None) -> None:
-        """The round's SGD steps on the index table filled by ``prepare_round`` (one graph replay)."""
+    def launch_round(self, n_steps: Optional[int] = None, next_n: Optional[int] = None) -> None:
+        """The round's SGD steps on the staged batches (one graph replay), then optionally stage the next round."""
         n = self._check_n(n_steps)
+        if self._staged != n:
+            raise RuntimeError("launch_round without prepare_round: no batches staged for this round")
+        self._staged = None
         if self.use_graph:
             g = self._graph_for(n)
             _lib.check(_lib.kernels().ecg_round_graph_launch(g, _lib.stream_ptr(self.device)),
                        "ecg_round_graph_launch")
-        elif self.persistent:
-            self._eager_round(n)
         else:
-            for s in range(n):
-                self._eager_step(s)
+            self.idx_table[:n].copy_(self.idx_stage[:n])
+            if self.persistent:
+                self._eager_round(n)
+            else:
+                for s in range(n):
+                    self._eager_step(s)
         self.steps_done += n
         self._loss_steps = getattr(self, "_loss_steps", 0) + n
+        if next_n is not None:
+            self.stage(next_n)
 
     def avg_loss(self) -> float:
         """Mean per-step loss since the last reset (synchronises)."""

@@ -135,7 +135,9 @@ def _ddp_fused_round(trainer, ctx: DistContext, n: int):
     if not hasattr(trainer, "_ddp_opt"):
         trainer._ddp_grad = torch.zeros_like(trainer.params)
         trainer._ddp_opt = FlatSGD(trainer.params, trainer._ddp_grad, lr=trainer.lr, momentum=trainer.momentum)
-    trainer._loss_steps = n  # batches already drawn by trainer.prepare_round(n)
+    trainer._loss_steps = n  # batches already drawn by trainer.prepare_round(n) into the staging table
+    trainer.idx_table[:n].copy_(trainer.idx_stage[:n])
+    trainer._staged = None
     lib = _lib.kernels()
     for s in range(n):
         tiny_step_grads(trainer.params, trainer.x, trainer.y32, trainer.idx_table[s], trainer.B, trainer.nc,

@@ -69,7 +69,7 @@ class TorchLocalTrainer:
             self.loss_acc.zero_()
             self._loss_steps = 0
 
-    def launch_round(self, n: int) -> None:
+    def launch_round(self, n: int, next_n=None) -> None:
         self.run_steps(n, reset_loss=False)
 
     def avg_loss(self) -> float:

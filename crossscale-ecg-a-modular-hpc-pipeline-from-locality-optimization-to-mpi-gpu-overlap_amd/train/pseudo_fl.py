@@ -136,16 +136,11 @@ def run_fused_gpu(model, x_gpu, y_gpu, device, steps: int, rank: int, batch_size
                   seed: Optional[int] = None, precision: str = "bf16") -> BenchStats:
     """The fused HIP step (``precision`` bf16: G1, fp32: the native G0): all ``steps`` replayed from one native
     hipGraph, one sync at the end.  The graph for exactly ``steps`` steps is captured and uploaded - and its
-    kernels warmed by a short untimed round whose updates are then rolled back - before the timing starts."""
+    kernels warmed by one replay that ``prepare`` rolls back - before the timing starts."""
     from ..ops.fused_tiny import FusedTinyTrainer
     tr = FusedTinyTrainer(model, x_gpu, y_gpu, batch_size, steps, lr=lr, momentum=0.9, seed=seed,
                           precision=precision)
-    w0 = tr.params.clone()
     tr.prepare([steps])
-    tr.run_round(min(steps, 2))
-    _sync(device)
-    tr.params.copy_(w0)
-    tr.reset_momentum()
     _sync(device)
     t0 = time.perf_counter()
     tr.run_round(steps)

@@ -74,7 +74,7 @@ class ResNetEngineTrainer:
         self.sampler.fill(self.table)
         self.engine.reset_counter()
 
-    def launch_round(self, n: Optional[int] = None) -> None:
+    def launch_round(self, n: Optional[int] = None, next_n: Optional[int] = None) -> None:
         n = self.S if n is None else n
         for _ in range(n):
             self._step()

@@ -1,15 +1,21 @@
-// Single-channel "valid" conv1d (cross-correlation) for gfx950 - the Module-2 kernel.
+// Single-channel "valid" conv1d (cross-correlation) for gfx950 - the Module-2 kernel, forward and backward.
 //
-//   y[b, i] = sum_{k<K} x[b, i + k] * w[k],   x:[B, L], w:[K], y:[B, L-K+1]
+//   forward  y[b, i]  = sum_{k<K} x[b, i + k] * w[k]                 x:[B, L], w:[K], y:[B, outL], outL = L-K+1
+//   dgrad    dx[b, j] = sum_{k<K} dy[b, j - k] * w[k]   (0 <= j-k < outL)
+//   wgrad    dw[k]    = sum_{b, i} x[b, i + k] * dy[b, i]
 //
 // Same math and C ABI shape as the reference CPU kernel conv1d_batch_omp_simd
-// (Module_2/conv1d_openmp_simd.c:21-61, OpenMP over batch + AVX2 over taps).  MI355X design:
-// one 256-thread workgroup per window; the window (+ tail) is staged into LDS with 16-byte global
-// loads, the K taps live in registers (compile-time K for the benchmarked 3/5/7 and a runtime
-// loop otherwise), and output positions are spread over lanes so every LDS read and global store is
-// unit-stride across the wave (conflict-free, fully coalesced).  The op is latency/launch bound
-// (B=512, L=500 is 1 MB in / 1 MB out), so the design goal is a single short launch with no
-// workspace, no solver lookup and no host sync - what beats MIOpen's general convolution path here.
+// (Module_2/conv1d_openmp_simd.c:21-61: OpenMP over the batch, AVX2 over taps).  The op moves ~2 KB per window
+// and is launch/latency bound (B=512, L=500 is 1 MB in, 1 MB out), so the MI355X design minimises the dependent
+// chain of a launch rather than arithmetic:
+//   * one thread per QUAD of outputs (4 consecutive positions of one window), flat grid over (window, quad):
+//     B=256, L=500 is 124 quads x 256 windows = 124 workgroups of 256 threads, well under one wave per SIMD;
+//   * the quad's input span x[4q .. 4q+3+K-1] comes straight from global memory into registers as 16-byte
+//     vectors (ceil((K+3)/4) loads, all issued before the first FMA; neighbouring lanes share cache lines, so
+//     the halo costs L1/L2 hits, not HBM bytes) - no LDS staging, no barrier, one memory round trip;
+//   * the K taps are scalar loads kept in SGPRs (compile-time K for 3/5/7/9/11/15/32, a runtime loop
+//     otherwise); 4K FMAs per thread; 16-byte stores when the output rows are 16-byte aligned.
+//   * wgrad: per-workgroup partial sums [G][K] (fixed order) + a one-workgroup second pass - deterministic.
 #include "../include/ecg_common.h"
 
 namespace {
@@ -17,86 +23,266 @@ namespace {
 constexpr int kThreads = 256;
 
 template <typename T>
-__device__ __forceinline__ float ld(const T* p) { return (float)(*p); }
+struct Vec4;
+template <>
+struct Vec4<float> {
+  typedef float4 type;
+  __device__ static inline void unpack(const float4& v, float* o) {
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  }
+};
+template <>
+struct Vec4<__bf16> {
+  typedef bf16x4 type;
+  __device__ static inline void unpack(const bf16x4& v, float* o) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = (float)v[j];
+  }
+};
 
+__device__ __forceinline__ void store1(float* p, float v) { *p = v; }
+__device__ __forceinline__ void store1(__bf16* p, float v) { *p = (__bf16)v; }
+
+// Loads 4 * NV consecutive elements of a row starting at ``pos`` (zero at and beyond ``len``) into ``o``.
+// ``vec``: the row base is 16-byte (fp32) / 8-byte (bf16) aligned and len % 4 == 0, so a 4-vector is either
+// entirely inside the row or entirely past its end.
+template <int NV, typename T>
+__device__ __forceinline__ void load_span(const T* __restrict__ row, int pos, int len, bool vec, float* o) {
+  if (vec) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      if (pos + 4 * v < len) {
+        const typename Vec4<T>::type q = reinterpret_cast<const typename Vec4<T>::type*>(row + pos)[v];
+        Vec4<T>::unpack(q, o + 4 * v);
+      } else {
+        o[4 * v] = o[4 * v + 1] = o[4 * v + 2] = o[4 * v + 3] = 0.f;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4 * NV; ++e) o[e] = (pos + e < len) ? (float)row[pos + e] : 0.f;
+  }
+}
+
+template <typename TY>
+__device__ __forceinline__ void store_quad(TY* __restrict__ yrow, int pos, int len, bool vec, const float* acc) {
+  if (vec && pos + 3 < len) {
+    if constexpr (sizeof(TY) == 4) {
+      *reinterpret_cast<float4*>(yrow + pos) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    } else {
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (__bf16)acc[j];
+      *reinterpret_cast<bf16x4*>(yrow + pos) = o;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (pos + j < len) store1(yrow + pos + j, acc[j]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------- forward
 template <int KC, typename TX, typename TY>
-__global__ __launch_bounds__(kThreads) void conv1d_valid_kernel(const TX* __restrict__ x, const float* __restrict__ w,
-                                                                 TY* __restrict__ y, int L, int K, int outL,
-                                                                 int rows_per_block, int B) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* xs = reinterpret_cast<float*>(smem);
-  const int Kr = KC > 0 ? KC : K;
-  float wr[KC > 0 ? KC : 1];
+__global__ __launch_bounds__(kThreads) void conv1d_valid_fwd_kernel(const TX* __restrict__ x,
+                                                                     const float* __restrict__ w,
+                                                                     TY* __restrict__ y, int B, int L, int K,
+                                                                     int outL, int nquads, int xvec, int yvec) {
+  const long gq = (long)blockIdx.x * kThreads + threadIdx.x;
+  if (gq >= (long)B * nquads) return;
+  const int b = (int)(gq / nquads), q = (int)(gq - (long)b * nquads);
+  const int i0 = 4 * q;
+  const TX* xrow = x + (long)b * L;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
   if constexpr (KC > 0) {
+    constexpr int NV = (KC + 3 + 3) / 4;
+    float xv[4 * NV];
+    load_span<NV>(xrow, i0, L, xvec != 0, xv);
+    float wr[KC];
 #pragma unroll
     for (int k = 0; k < KC; ++k) wr[k] = w[k];
-  }
-  const int Lpad = (L + 3) & ~3;
-  for (int rr = 0; rr < rows_per_block; ++rr) {
-    const int b = blockIdx.x * rows_per_block + rr;
-    if (b >= B) break;
-    const TX* xrow = x + (long)b * L;
-    // stage x row into LDS (vectorised when the row is 16-B aligned)
-    if constexpr (sizeof(TX) == 4) {
-      if ((((uintptr_t)xrow) & 15) == 0) {
-        const int n4 = L >> 2;
-        for (int i = threadIdx.x; i < n4; i += kThreads)
-          reinterpret_cast<float4*>(xs)[i] = reinterpret_cast<const float4*>(xrow)[i];
-        for (int i = (n4 << 2) + threadIdx.x; i < L; i += kThreads) xs[i] = xrow[i];
-      } else {
-        for (int i = threadIdx.x; i < L; i += kThreads) xs[i] = xrow[i];
-      }
-    } else {
-      for (int i = threadIdx.x; i < L; i += kThreads) xs[i] = ld(xrow + i);
-    }
-    for (int i = L + threadIdx.x; i < Lpad + 64; i += kThreads) xs[i] = 0.f;
-    __syncthreads();
-    TY* yrow = y + (long)b * outL;
-    for (int i = threadIdx.x; i < outL; i += kThreads) {
-      float acc = 0.f;
-      if constexpr (KC > 0) {
 #pragma unroll
-        for (int k = 0; k < KC; ++k) acc = fmaf(xs[i + k], wr[k], acc);
-      } else {
-        for (int k = 0; k < Kr; ++k) acc = fmaf(xs[i + k], w[k], acc);
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = fmaf(xv[j + k], wr[k], acc[j]);
+  } else {
+    for (int k = 0; k < K; ++k) {
+      const float wk = w[k];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int e = i0 + j + k;
+        acc[j] = fmaf(e < L ? (float)xrow[e] : 0.f, wk, acc[j]);
       }
-      yrow[i] = (TY)acc;
+    }
+  }
+  store_quad(y + (long)b * outL, i0, outL, yvec != 0, acc);
+}
+
+// --------------------------------------------------------------------------------------------- data grad
+// dx[j] for j in [4q, 4q+4): needs dy[j-K+1 .. j] -> the span dy[4q-K+1 .. 4q+3] (zero outside [0, outL)).
+template <int KC, typename T>
+__global__ __launch_bounds__(kThreads) void conv1d_valid_dgrad_kernel(const T* __restrict__ dy,
+                                                                       const float* __restrict__ w,
+                                                                       T* __restrict__ dx, int B, int L, int K,
+                                                                       int outL, int nquads, int xvec) {
+  const long gq = (long)blockIdx.x * kThreads + threadIdx.x;
+  if (gq >= (long)B * nquads) return;
+  const int b = (int)(gq / nquads), q = (int)(gq - (long)b * nquads);
+  const int j0 = 4 * q;
+  const T* dyrow = dy + (long)b * outL;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (KC > 0) {
+    // span element s <-> dy index j0 - KC + 1 + s, s in [0, KC + 3)
+    const int base = j0 - KC + 1;
+    float dv[KC + 3];
+#pragma unroll
+    for (int s = 0; s < KC + 3; ++s) {
+      const int e = base + s;
+      dv[s] = (e >= 0 && e < outL) ? (float)dyrow[e] : 0.f;
+    }
+    float wr[KC];
+#pragma unroll
+    for (int k = 0; k < KC; ++k) wr[k] = w[k];
+    // dx[j0 + jj] = sum_k dy[j0 + jj - k] w[k] = sum_k dv[jj - k + KC - 1] w[k]
+#pragma unroll
+    for (int k = 0; k < KC; ++k)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) acc[jj] = fmaf(dv[jj - k + KC - 1], wr[k], acc[jj]);
+  } else {
+    for (int k = 0; k < K; ++k) {
+      const float wk = w[k];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int e = j0 + jj - k;
+        acc[jj] = fmaf((e >= 0 && e < outL) ? (float)dyrow[e] : 0.f, wk, acc[jj]);
+      }
+    }
+  }
+  store_quad(dx + (long)b * L, j0, L, xvec != 0, acc);
+}
+
+// ------------------------------------------------------------------------------------------- weight grad
+// Pass 1: workgroup g sums x[b, i+k] * dy[b, i] over its (window, quad) range for every tap k < K (K <= 64),
+// reducing lanes -> waves -> workgroup in a fixed order; partial[g][k].  Pass 2: one workgroup sums the G rows.
+constexpr int kMaxWgradK = 64;
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void conv1d_valid_wgrad_partial_kernel(const T* __restrict__ x,
+                                                                               const T* __restrict__ dy,
+                                                                               float* __restrict__ partial, int B,
+                                                                               int L, int K, int outL, int nquads) {
+  __shared__ float red[kThreads / 64][kMaxWgradK];
+  const long gq = (long)blockIdx.x * kThreads + threadIdx.x;
+  const bool live = gq < (long)B * nquads;
+  const int b = live ? (int)(gq / nquads) : 0, q = live ? (int)(gq - (long)b * nquads) : 0;
+  const int i0 = 4 * q;
+  const T* xrow = x + (long)b * L;
+  const T* dyrow = dy + (long)b * outL;
+  float d[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) d[j] = (live && i0 + j < outL) ? (float)dyrow[i0 + j] : 0.f;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int k = 0; k < K; ++k) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int e = i0 + j + k;
+      s = fmaf((live && e < L) ? (float)xrow[e] : 0.f, d[j], s);
+    }
+    s = ecg::wave_sum(s);
+    if (lane == 0) red[wv][k] = s;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += kThreads) {
+    float s = 0.f;
+#pragma unroll
+    for (int v = 0; v < kThreads / 64; ++v) s += red[v][k];
+    partial[(long)blockIdx.x * K + k] = s;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void conv1d_valid_wgrad_final_kernel(const float* __restrict__ partial,
+                                                                             float* __restrict__ dw, int G, int K) {
+  __shared__ float red[kThreads / 64];
+  for (int k = 0; k < K; ++k) {
+    float s = 0.f;
+    for (int g = threadIdx.x; g < G; g += kThreads) s += partial[(long)g * K + k];
+    s = ecg::wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+#pragma unroll
+      for (int v = 0; v < kThreads / 64; ++v) t += red[v];
+      dw[k] = t;
     }
     __syncthreads();
   }
 }
 
+template <typename T>
+inline bool vec_ok(const T* p, int len) {
+  return (((uintptr_t)p) % (4 * sizeof(T))) == 0 && (len % 4) == 0;
+}
+
+#define ECG_K_SWITCH(K, LAUNCH) \
+  switch (K) {                  \
+    case 3: LAUNCH(3); break;   \
+    case 5: LAUNCH(5); break;   \
+    case 7: LAUNCH(7); break;   \
+    case 9: LAUNCH(9); break;   \
+    case 11: LAUNCH(11); break; \
+    case 15: LAUNCH(15); break; \
+    case 32: LAUNCH(32); break; \
+    default: LAUNCH(0);         \
+  }
+
 template <typename TX, typename TY>
-int launch(const TX* x, const float* w, TY* y, int B, int L, int K, hipStream_t stream) {
+int launch_fwd(const TX* x, const float* w, TY* y, int B, int L, int K, hipStream_t stream) {
   if (B <= 0 || L <= 0 || K <= 0 || K > L) return ecg::kBadArg;
   const int outL = L - K + 1;
-  const size_t smem = (size_t)(((L + 3) & ~3) + 64) * sizeof(float);
-  if (smem > 160 * 1024) return ecg::kTooLarge;
-  // one window per block; big batches pack two rows per block to halve the block count
-  const int rpb = B >= 2048 ? 2 : 1;
-  dim3 grid((B + rpb - 1) / rpb), block(kThreads);
-  switch (K) {
-#define ECG_CASE(KK)                                                                                           \
-  case KK:                                                                                                     \
-    if (smem > 64 * 1024)                                                                                      \
-      ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_valid_kernel<KK, TX, TY>,                         \
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));               \
-    hipLaunchKernelGGL((conv1d_valid_kernel<KK, TX, TY>), grid, block, smem, stream, x, w, y, L, K, outL, rpb, B); \
-    break;
-    ECG_CASE(3)
-    ECG_CASE(5)
-    ECG_CASE(7)
-    ECG_CASE(9)
-    ECG_CASE(11)
-    ECG_CASE(15)
-    ECG_CASE(32)
-#undef ECG_CASE
-    default:
-      if (smem > 64 * 1024)
-        ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_valid_kernel<0, TX, TY>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
-      hipLaunchKernelGGL((conv1d_valid_kernel<0, TX, TY>), grid, block, smem, stream, x, w, y, L, K, outL, rpb, B);
-  }
+  const int nquads = (outL + 3) / 4;
+  const long threads = (long)B * nquads;
+  const dim3 grid((unsigned)((threads + kThreads - 1) / kThreads)), block(kThreads);
+  const int xv = vec_ok(x, L), yv = vec_ok(y, outL);
+#define ECG_FWD(KK)                                                                                          \
+  hipLaunchKernelGGL((conv1d_valid_fwd_kernel<KK, TX, TY>), grid, block, 0, stream, x, w, y, B, L, K, outL, \
+                     nquads, xv, yv)
+  ECG_K_SWITCH(K, ECG_FWD)
+#undef ECG_FWD
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
+}
+
+template <typename T>
+int launch_dgrad(const T* dy, const float* w, T* dx, int B, int L, int K, hipStream_t stream) {
+  if (B <= 0 || L <= 0 || K <= 0 || K > L) return ecg::kBadArg;
+  const int outL = L - K + 1;
+  const int nquads = (L + 3) / 4;
+  const long threads = (long)B * nquads;
+  const dim3 grid((unsigned)((threads + kThreads - 1) / kThreads)), block(kThreads);
+  const int xv = vec_ok(dx, L);
+#define ECG_DG(KK)                                                                                              \
+  hipLaunchKernelGGL((conv1d_valid_dgrad_kernel<KK, T>), grid, block, 0, stream, dy, w, dx, B, L, K, outL, nquads, \
+                     xv)
+  ECG_K_SWITCH(K, ECG_DG)
+#undef ECG_DG
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
+}
+
+template <typename T>
+int launch_wgrad(const T* x, const T* dy, float* dw, float* ws, long ws_floats, int B, int L, int K,
+                 hipStream_t stream) {
+  if (B <= 0 || L <= 0 || K <= 0 || K > L || K > kMaxWgradK) return ecg::kBadArg;
+  const int outL = L - K + 1;
+  const int nquads = (outL + 3) / 4;
+  const long threads = (long)B * nquads;
+  const int G = (int)((threads + kThreads - 1) / kThreads);
+  if ((long)G * K > ws_floats) return ecg::kBadArg;
+  hipLaunchKernelGGL((conv1d_valid_wgrad_partial_kernel<T>), dim3(G), dim3(kThreads), 0, stream, x, dy, ws, B, L, K,
+                     outL, nquads);
+  hipLaunchKernelGGL(conv1d_valid_wgrad_final_kernel, dim3(1), dim3(kThreads), 0, stream, ws, dw, G, K);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
@@ -106,11 +292,47 @@ int launch(const TX* x, const float* w, TY* y, int B, int L, int K, hipStream_t 
 // C-ABI twin of the reference's conv1d_batch_omp_simd(x, w, y, batch, L, K, nthreads):
 // the thread count is replaced by the HIP stream the kernel is enqueued on (async, no sync).
 ECG_API int conv1d_batch_hip(const float* x, const float* w, float* y, int batch, int L, int K, hipStream_t stream) {
-  return launch<float, float>(x, w, y, batch, L, K, stream);
+  return launch_fwd<float, float>(x, w, y, batch, L, K, stream);
+}
+
+// Blocking twin (the reference's CPU kernel returns when its output is complete): launch, then wait for the
+// stream.  One native call covers the whole "result ready" path the Module-2 single-call metric times.
+ECG_API int conv1d_batch_hip_sync(const float* x, const float* w, float* y, int batch, int L, int K,
+                                  hipStream_t stream) {
+  const int st = launch_fwd<float, float>(x, w, y, batch, L, K, stream);
+  if (st) return st;
+  ECG_HIP_CHECK(hipStreamSynchronize(stream));
+  return ecg::kOk;
 }
 
 // bf16 activations in/out, fp32 taps and accumulation.
 ECG_API int conv1d_batch_hip_bf16(const __bf16* x, const float* w, __bf16* y, int batch, int L, int K,
                                   hipStream_t stream) {
-  return launch<__bf16, __bf16>(x, w, y, batch, L, K, stream);
+  return launch_fwd<__bf16, __bf16>(x, w, y, batch, L, K, stream);
+}
+
+// Backward: dx [B, L] from dy [B, L-K+1] (fp32 or bf16 with fp32 accumulation).
+ECG_API int conv1d_valid_dgrad_hip(const float* dy, const float* w, float* dx, int batch, int L, int K,
+                                   hipStream_t stream) {
+  return launch_dgrad<float>(dy, w, dx, batch, L, K, stream);
+}
+ECG_API int conv1d_valid_dgrad_hip_bf16(const __bf16* dy, const float* w, __bf16* dx, int batch, int L, int K,
+                                        hipStream_t stream) {
+  return launch_dgrad<__bf16>(dy, w, dx, batch, L, K, stream);
+}
+
+// Floats of workspace the weight gradient needs (one partial row of K per workgroup).
+ECG_API long conv1d_valid_wgrad_ws_floats(int batch, int L, int K) {
+  const long nquads = (L - K + 1 + 3) / 4;
+  return ((long)batch * nquads + kThreads - 1) / kThreads * (long)K;
+}
+
+// dw [K] (fp32) from x [B, L] and dy [B, L-K+1]; deterministic two-pass reduction through ``ws``.
+ECG_API int conv1d_valid_wgrad_hip(const float* x, const float* dy, float* dw, float* ws, long ws_floats, int batch,
+                                   int L, int K, hipStream_t stream) {
+  return launch_wgrad<float>(x, dy, dw, ws, ws_floats, batch, L, K, stream);
+}
+ECG_API int conv1d_valid_wgrad_hip_bf16(const __bf16* x, const __bf16* dy, float* dw, float* ws, long ws_floats,
+                                        int batch, int L, int K, hipStream_t stream) {
+  return launch_wgrad<__bf16>(x, dy, dw, ws, ws_floats, batch, L, K, stream);
 }

@@ -1489,7 +1489,7 @@ ECG_API int ecg_tiny_train_round(const float* X, int L, long ldx, const int* idx
 static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws, long ws_bytes, int prec,
                          const float* X, int L, long ldx, const int* idx_table, const int* Y, float* params,
                          float* mom, int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr,
-                         float momentum, float wd, int nesterov, int* ctl, float* gslab) {
+                         float momentum, float wd, int nesterov, int* ctl, float* gslab, const int* idx_stage) {
   hipStream_t cap;
   ECG_HIP_CHECK(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
   RoundGraph* rg = new RoundGraph();
@@ -1501,7 +1501,13 @@ static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws
     return ecg::kHipError;
   }
   int st = 0;
-  if (pa) {
+  // Staged batches: the round's index rows were enqueued into idx_stage one round ahead (while the previous round
+  // computed); the graph's first node moves them into the table every replay reads.
+  if (idx_stage && hipMemcpyAsync(const_cast<int*>(idx_table), idx_stage, (size_t)steps * B * sizeof(int),
+                                  hipMemcpyDeviceToDevice, cap) != hipSuccess)
+    st = ecg::kHipError;
+  if (st) {
+  } else if (pa) {
     st = round_dispatch(*pa, ws, ws_bytes, prec, cap);
   } else {
     for (int s = 0; s < steps && st == 0; ++s)
@@ -1527,27 +1533,29 @@ static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws
 
 // Capture ``steps`` consecutive fused steps (batch s reads idx_table + s*B) into one hipGraph.
 // All pointers are baked into the graph: callers keep the buffers alive and refill idx_table in place.
+// ``idx_stage`` (optional): the graph first copies idx_stage[0 : steps*B] into idx_table.
 ECG_API int ecg_round_graph_create(void** handle, const float* X, int L, long ldx, const int* idx_table,
                                    const int* Y, float* params, float* mom, int nc, float* slab, int slab_stride,
                                    int B, int steps, float* loss_acc, float lr, float momentum, float wd,
-                                   int nesterov, int* ctl, float* gslab, int prec) {
+                                   int nesterov, int* ctl, float* gslab, int prec, const int* idx_stage) {
   if (!handle || steps <= 0) return ecg::kBadArg;
   int st = check_step_args(L, nc, B, slab_stride, 0, prec == 1);
   if (st) return st;
   return capture_round(handle, steps, nullptr, nullptr, 0, prec, X, L, ldx, idx_table, Y, params, mom, nc, slab,
-                       slab_stride, B, loss_acc, lr, momentum, wd, nesterov, ctl, gslab);
+                       slab_stride, B, loss_acc, lr, momentum, wd, nesterov, ctl, gslab, idx_stage);
 }
 
 // The persistent round (workspace memset + one launch) captured as a hipGraph, replayed once per round.
 ECG_API int ecg_round_graph_create_persistent(void** handle, const float* X, int L, long ldx, const int* idx_table,
                                               const int* Y, float* params, float* mom, int nc, int B, int steps,
                                               float* loss_acc, float lr, float momentum, float wd, int nesterov,
-                                              void* ws, long ws_bytes, int* status, int prec) {
+                                              void* ws, long ws_bytes, int* status, int prec,
+                                              const int* idx_stage) {
   if (!handle || steps <= 0) return ecg::kBadArg;
   const RoundArgs a = make_round_args(X, L, ldx, idx_table, Y, params, mom, nc, B, steps, loss_acc, lr, momentum, wd,
                                       nesterov, ws, status, nullptr);
   return capture_round(handle, steps, &a, ws, ws_bytes, prec, X, L, ldx, idx_table, Y, params, mom, nc, nullptr, 0,
-                       B, loss_acc, lr, momentum, wd, nesterov, nullptr, nullptr);
+                       B, loss_acc, lr, momentum, wd, nesterov, nullptr, nullptr, idx_stage);
 }
 
 ECG_API int ecg_round_graph_launch(void* handle, hipStream_t stream) {

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Where does the fixed (per timed region) overhead of a short bench.py run go?
+
+Times, in one process after warm-up, the FedAvg round plan of K steps for several K (5 repetitions each) and
+the pieces of a round in isolation: the index-table fill, a graph replay of n steps, a bare synchronize.
+"""
+from __future__ import annotations
+
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+import crossscale_ecg  # noqa: E402,F401
+from crossscale_ecg.models.tiny_ecg import TinyECG  # noqa: E402
+from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(1337)
+    x = torch.randn(20000, 500, generator=g, device=dev)
+    y = torch.zeros(20000, dtype=torch.long, device=dev)
+    torch.manual_seed(1234)
+    m = TinyECG().to(dev)
+    tr = FusedTinyTrainer(m, x, y, 256, 50, seed=4321)
+    tr.prepare([1, 5, 20, 50])
+    for _ in range(4):
+        tr.run_round(50)
+    torch.cuda.synchronize()
+
+    def timed(fn, reps=7):
+        out = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            out.append((time.perf_counter() - t0) * 1e6)
+        return statistics.median(out), min(out)
+
+    def plan(k):
+        def f():
+            done = 0
+            while done < k:
+                n = min(50, k - done)
+                tr.run_round(n, reset_loss=False)
+                done += n
+        return f
+
+    print("bare synchronize: median %.1f us  min %.1f us" % timed(lambda: None))
+    print("index fill (20 rows): median %.1f us  min %.1f us" % timed(lambda: tr.sampler.fill(tr.idx_table[:20])))
+    for n in (1, 5, 20, 50):
+        med, mn = timed(lambda: tr.launch_round(n))
+        print(f"graph replay n={n:3d} (no fill): median {med:8.1f} us  min {mn:8.1f} us  -> {med / n:6.2f} us/step")
+    for k in (20, 50, 100, 500):
+        med, mn = timed(plan(k))
+        print(f"plan K={k:4d}: median {med:8.1f} us  min {mn:8.1f} us  -> {med / k:6.2f} us/step (min {mn / k:6.2f})")
+    tr.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -2,7 +2,7 @@
 # One GPU-box session: tests, smoke, bench, rocprof.  Every GPU step has its own time limit; a crash,
 # abort or timeout (exit >= 124 or signal) stops the session, an ordinary test failure (exit 1) does not.
 # Usage (from the repo root on the box): bash scripts/gpu_session.sh [steps...]
-#   steps: tests smoke bench prof  (default: all)
+#   steps: tests smoke bench bench20 diag_g1 modules prof  (default: tests smoke bench prof)
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out
@@ -27,9 +27,17 @@ run() {  # run <name> <timeout_s> <cmd...>
 python csrc/build.py > "$OUT/build.log" 2>&1 || { cat "$OUT/build.log"; exit 2; }
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 500 --warmup 100 ;;
+    bench20) run bench20 300 python bench.py --steps 20 --warmup 5
+             run bench20b 300 python bench.py --steps 20 --warmup 5 --no-extras
+             run bench500 300 python bench.py --steps 500 --warmup 100 --no-extras ;;
+    diag_g1) run diag_g1 600 python scripts/diag_g1_overlap.py "$OUT/diag_g1" ;;
+    diag_call) run diag_overhead 300 python scripts/diag_bench_overhead.py
+               run diag_conv1d_call 300 python scripts/diag_conv1d_call.py ;;
+    module2) mkdir -p gpurun_out/results
+             run module2 600 python benchmark_part_2.py --results-dir gpurun_out/results --batch-scaling ;;
     modules)
       R=gpurun_out/results
       mkdir -p $R

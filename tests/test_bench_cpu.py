@@ -1,0 +1,39 @@
+"""bench.py launch/sync/JSON contract rehearsed on CPU: ``--gpus 2`` self-launches two gloo ranks (the parent
+never initialises a GPU), every round - including the trailing partial one - ends with the FedAvg all-reduce."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, env_extra=None):
+    env = dict(os.environ, ECG_DIST_BACKEND="gloo", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+               OMP_NUM_THREADS="1", **(env_extra or {}))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--max-windows", "600",
+                        "--batch-size", "16", *args], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    return json.loads(lines[0])
+
+
+def test_bench_self_launch_world2_partial_round_syncs():
+    rec = _bench("--gpus", "2", "--steps", "7", "--warmup", "3", "--local-steps", "5")
+    assert rec["n_gpus"] == 2 and rec["rccl_world_size"] == 2 and rec["dist_backend"] == "gloo"
+    assert rec["timed_round_plan"] == [5, 2] and rec["fedavg_syncs_timed"] == 2
+    assert rec["config"]["global_batch"] == 32 and rec["config"]["parallelism"] == "dp2"
+    assert rec["value"] == rec["n_gpus"] * 16 * 7 / (rec["ms_per_step"] * 7 / 1e3) or \
+        abs(rec["value"] - 32 / (rec["ms_per_step"] / 1e3)) < 1e-3 * rec["value"]
+
+
+def test_bench_overlap_none_world2():
+    rec = _bench("--gpus", "2", "--steps", "4", "--warmup", "0", "--local-steps", "2", "--overlap", "none")
+    assert rec["fedavg_syncs_timed"] == 2 and "overlap=none" in rec["config"]["sync"]
+
+
+def test_bench_single_rank():
+    rec = _bench("--steps", "3", "--warmup", "1", "--local-steps", "2")
+    assert rec["n_gpus"] == 1 and rec["rccl_world_size"] == 1 and rec["fedavg_syncs_timed"] == 2

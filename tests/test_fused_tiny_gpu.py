@@ -243,3 +243,26 @@ def test_persistent_round_is_opt_in_and_checked():
     tr.run_round()
     assert tr.avg_loss() == tr.avg_loss()
     tr.close()
+
+
+def test_prepare_rollback_and_staged_rounds_bitwise():
+    """``prepare`` (capture + upload + one warm replay) leaves no trace in the training state, and staging the next
+    round's batches behind the current round (``next_n``) gives bit-identical training to staging at launch."""
+    from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
+    plan = [5, 5, 3, 5, 2]
+    outs = []
+    for mode in ("plain", "prepared_staged"):
+        dev, x, y, model, _ = _setup(B=64, N=1024)
+        tr = FusedTinyTrainer(model, x, y, 64, 5, seed=21)
+        if mode == "plain":
+            for n in plan:
+                tr.run_round(n, reset_loss=False)
+        else:
+            tr.prepare(sorted(set(plan)))
+            for i, n in enumerate(plan):
+                tr.run_round(n, reset_loss=False, next_n=plan[i + 1] if i + 1 < len(plan) else None)
+        torch.cuda.synchronize()
+        outs.append((tr.params.clone(), tr.mom.clone(), tr.avg_loss(), tr.idx_table.clone()))
+        tr.close()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2] and torch.equal(outs[0][3][:2], outs[1][3][:2])

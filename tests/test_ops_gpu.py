@@ -37,6 +37,45 @@ def test_conv1d_valid_bf16_and_3d_and_odd_alignment():
     assert (yb.float() - refb).abs().max().item() < 2e-2 * refb.abs().max().item()
 
 
+@pytest.mark.parametrize("B,L,K", [(64, 500, 3), (256, 500, 7), (33, 333, 5), (8, 500, 32), (17, 101, 12)])
+def test_conv1d_valid_backward_matches_autograd(B, L, K):
+    """HIP dgrad + deterministic wgrad vs torch autograd of F.conv1d in fp64."""
+    from crossscale_ecg.ops.conv1d import conv1d_valid_fn
+    x = torch.randn(B, L, device=DEV, requires_grad=True)
+    w = torch.randn(K, device=DEV, requires_grad=True)
+    dy = torch.randn(B, L - K + 1, device=DEV)
+    y = conv1d_valid_fn(x, w)
+    y.backward(dy)
+    xd, wd = x.detach().double().requires_grad_(), w.detach().double().requires_grad_()
+    yr = F.conv1d(xd.unsqueeze(1), wd.view(1, 1, K))[:, 0]
+    yr.backward(dy.double())
+    assert torch.allclose(y.double(), yr, atol=1e-4, rtol=1e-5)
+    assert torch.allclose(x.grad.double(), xd.grad, atol=1e-4, rtol=1e-5), (x.grad.double() - xd.grad).abs().max()
+    assert torch.allclose(w.grad.double(), wd.grad, rtol=1e-4, atol=1e-3), (w.grad.double() - wd.grad).abs().max()
+    # deterministic: the same inputs give the same bits
+    from crossscale_ecg.ops.conv1d import conv1d_valid_backward
+    a = conv1d_valid_backward(x.detach(), w.detach(), dy)
+    b = conv1d_valid_backward(x.detach(), w.detach(), dy)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+
+
+def test_conv1d_valid_backward_bf16_and_blocking():
+    from crossscale_ecg.ops.conv1d import conv1d_valid, conv1d_valid_backward
+    x = torch.randn(128, 500, device=DEV).bfloat16()
+    w = torch.randn(7, device=DEV)
+    dy = torch.randn(128, 494, device=DEV).bfloat16()
+    dx, dw = conv1d_valid_backward(x, w, dy)
+    xd = x.double().requires_grad_()
+    wd = w.double().requires_grad_()
+    F.conv1d(xd.unsqueeze(1), wd.view(1, 1, 7))[:, 0].backward(dy.double())
+    assert (dx.double() - xd.grad).abs().max().item() < 2e-2 * xd.grad.abs().max().item()
+    assert (dw.double() - wd.grad).abs().max().item() < 1e-3 * wd.grad.abs().max().item()
+    xf = torch.randn(256, 500, device=DEV)
+    out = torch.empty(256, 494, device=DEV)
+    y = conv1d_valid(xf, w, backend="hip", out=out, blocking=True)
+    assert torch.allclose(y, F.conv1d(xf.unsqueeze(1), w.view(1, 1, 7))[:, 0], atol=1e-5, rtol=1e-5)
+
+
 @pytest.mark.parametrize("momentum,dampening,wd,nesterov", [(0.9, 0.0, 0.0, False), (0.0, 0.0, 1e-4, False),
                                                              (0.9, 0.1, 1e-3, False), (0.9, 0.0, 0.0, True)])
 def test_flat_sgd_matches_torch(momentum, dampening, wd, nesterov):

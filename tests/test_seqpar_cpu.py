@@ -36,7 +36,9 @@ def _worker(rank, world, port, q):
         loss = torch.nn.functional.cross_entropy(logits, y)
         loss.backward()
         allreduce_seq_grads_(m)
-        q.put((rank, "ok", (logits.detach(), {n: p.grad.clone() for n, p in m.named_parameters()})))
+        # numpy copies travel by value (a tensor would travel as a shared-memory handle that dies with this process)
+        q.put((rank, "ok", (logits.detach().numpy().copy(),
+                            {n: p.grad.detach().numpy().copy() for n, p in m.named_parameters()})))
     except Exception:  # pragma: no cover
         import traceback
         q.put((rank, "err", traceback.format_exc()))
@@ -79,6 +81,8 @@ def test_seq_parallel_matches_full_record(world):
     for p in ps:
         p.join(timeout=60)
     for rank, (logits, grads) in out.items():
+        logits = torch.from_numpy(logits)
+        grads = {n: torch.from_numpy(g) for n, g in grads.items()}
         assert torch.allclose(logits, ref_logits.detach(), atol=1e-5), rank
         for n, g in grads.items():
             assert torch.allclose(g, ref_grads[n], atol=1e-5, rtol=1e-4), (rank, n, (g - ref_grads[n]).abs().max())
