@@ -30,6 +30,8 @@ import torch
 import torch.nn.functional as F
 from torch.utils.data import DataLoader, RandomSampler, SequentialSampler
 
+from ..utils.timing import warm_until_stable
+
 from ..data.dataset import ShardDataset
 from ..data.shards import ensure_synthetic_shards, list_shards
 from ..models.tiny_ecg import TinyECG
@@ -102,10 +104,11 @@ def measure_step(dl: DataLoader, device, non_blocking: bool, iters: int = 50, co
             it = iter(dl)
             return next(it)
 
-    for _ in range(5):
+    def warm():
         xc, yc = nxt()
         step(xc.to(dev, non_blocking=non_blocking), yc.to(dev, non_blocking=non_blocking))
-    _sync(dev)
+
+    warm_until_stable(warm, dev)  # >= 5 steps (reference), until no first-use compile remains
     data_ms = h2d_ms = comp_ms = 0.0
     total = 0
     it = iter(dl)
@@ -176,7 +179,11 @@ def bench_labl(shard_paths: Sequence[str], batch_size: int, iters: int, normaliz
         return n, wait
 
     try:
-        for i in range(5):  # warm-up
+        wi = [0]
+
+        def warm():  # warm-up step (>= 5, until stable)
+            i = wi[0]
+            wi[0] += 1
             n, _ = stage(i)
             if main is not None:
                 main.wait_event(ready[i % 2])
@@ -184,6 +191,8 @@ def bench_labl(shard_paths: Sequence[str], batch_size: int, iters: int, normaliz
             if main is not None:
                 consumed[i % 2] = torch.cuda.Event()
                 consumed[i % 2].record(main)
+
+        warm_until_stable(warm, dev)
         _sync(dev)
         data_ms = h2d_ms = comp_ms = 0.0
         total = 0

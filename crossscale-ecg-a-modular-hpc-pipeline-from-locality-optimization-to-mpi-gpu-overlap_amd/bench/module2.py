@@ -7,8 +7,9 @@ Module_2/train_cpu_openmp.py (thread scaling at K=32).
 Two comparisons are produced:
   * ``part2_hip_results.csv``    - HIP conv1d vs ``torch.nn.Conv1d`` on the MI355X (MIOpen).  Three timings per
     cell.  HEADLINE ``speedup_med`` = the reference's metric: ``time_once`` (3 warm-up calls + ONE timed call,
-    host wall clock until the result is ready; the HIP side is the blocking ``conv1d_batch_hip_sync`` call,
-    the torch side ``conv(x)`` + ``torch.cuda.synchronize()``), median of 15 trials.  Secondary:
+    host wall clock until the result is ready, then ``torch.cuda.synchronize()`` on both sides; the HIP side is
+    the bound blocking op ``HipConv1dValid`` - launch + host spin on the stream - the torch side the module call
+    ``conv(x)``), median of 15 trials.  Secondary:
     ``speedup_burst`` (50 back-to-back calls between syncs, host per-call cost) and ``speedup_ev`` (hipEvent
     device time per call).  Every cell is checked against an fp64 reference (``max_abs_err``).
   * ``part2_openmp_results.csv`` - the C++ OpenMP/AVX kernel (reference C ABI) vs CPU ``nn.Conv1d`` on the
@@ -25,7 +26,7 @@ from typing import Callable, Dict, List, Tuple
 import numpy as np
 import torch
 
-from ..ops.conv1d import conv1d_valid, run_omp_conv, conv1d_valid_reference
+from ..ops.conv1d import HipConv1dValid, conv1d_valid, run_omp_conv, conv1d_valid_reference
 from ..utils import usable_cpus
 from ..utils.csvio import PART2_COLUMNS, PART2_RAW_COLUMNS, PART2_SCALING_COLUMNS, safe_write_csv
 
@@ -97,8 +98,10 @@ def bench_pair_gpu(bs: int, K: int, rng: np.random.Generator, trials: int = TRIA
     def hip_step():
         conv1d_valid(xt, wt, backend="hip", out=out)
 
+    op = HipConv1dValid(wt, blocking=True)  # the bound op, as nn.Conv1d holds its weight
+
     def hip_call():  # single-call path: returns when the output is complete
-        conv1d_valid(xt, wt, backend="hip", out=out, blocking=True)
+        op(xt, out)
 
     hip_step()
     sync()

@@ -87,6 +87,7 @@ def _bind_kernels(lib: C.CDLL) -> None:
     _sig(lib, "ecg_round_graph_upload", [vp, vp])
     _sig(lib, "conv1d_batch_hip", [vp, vp, vp, i32, i32, i32, vp])
     _sig(lib, "conv1d_batch_hip_sync", [vp, vp, vp, i32, i32, i32, vp])
+    _sig(lib, "conv1d_batch_hip_spin", [vp, vp, vp, i32, i32, i32, vp])
     _sig(lib, "conv1d_valid_dgrad_hip", [vp, vp, vp, i32, i32, i32, vp])
     _sig(lib, "conv1d_valid_dgrad_hip_bf16", [vp, vp, vp, i32, i32, i32, vp])
     _sig(lib, "conv1d_valid_wgrad_ws_floats", [i32, i32, i32], i64)
@@ -137,6 +138,8 @@ def io_lib() -> C.CDLL:
         _sig(lib, "ecg_prefetch_destroy", [vp])
         _sig(lib, "ecg_prefetch_error", [vp], C.c_char_p)
         _sig(lib, "ecg_upload_shards", [C.POINTER(C.c_char_p), i32, C.c_int64, C.c_int64, vp, C.c_int64, vp, i64p])
+        _sig(lib, "ecg_upload_shards_mt", [C.POINTER(C.c_char_p), i32, C.c_int64, C.c_int64, vp, C.c_int64, i32, vp,
+                                           i64p])
         lib._ecg_bound = True
     return lib
 

@@ -70,6 +70,41 @@ def _conv1d_hip_fast(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None,
     return out if out.dim() == d else out.view((B, 1, outL) if d == 3 else (B, outL))
 
 
+class HipConv1dValid:
+    """A bound single-channel valid conv1d on the HIP kernel - the op-object counterpart of ``nn.Conv1d(1, 1, K)``
+    (taps held by the object, like the module holds its weight).  ``y = op(x, out)`` for x [B, L] / [B, 1, L]
+    fp32 on the taps' device, out [B, L-K+1].  ``blocking``: return when y is complete, the host spinning on
+    the stream (the reference CPU kernel's call semantics, Module_2/conv1d_openmp_simd.c:21-61); else async on
+    the current stream.  Per call it only re-checks the shapes and takes the data pointers."""
+
+    def __init__(self, w: torch.Tensor, blocking: bool = True):
+        if not w.is_cuda:
+            raise ValueError("HipConv1dValid needs the taps on a GPU")
+        self.w = w.detach().reshape(-1).to(torch.float32).contiguous()
+        self.K = self.w.numel()
+        lib = _lib.kernels()
+        self._fn = lib.conv1d_batch_hip_spin if blocking else lib.conv1d_batch_hip
+        self._wp = self.w.data_ptr()
+        self._dev = self.w.device.index
+        self._shapes = None
+
+    def __call__(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        shapes = (x.shape, out.shape, x.dtype, out.dtype)
+        if shapes != self._shapes:
+            B, L = x.shape[0], x.shape[-1]
+            if (x.dtype != torch.float32 or out.dtype != torch.float32 or not x.is_contiguous()
+                    or not out.is_contiguous() or x.numel() != B * L or out.numel() != B * (L - self.K + 1)
+                    or x.device != self.w.device or out.device != self.w.device):
+                raise ValueError("HipConv1dValid: x must be contiguous fp32 [B, L] and out [B, L-K+1] on the "
+                                 "taps' device")
+            self._shapes, self._BL = shapes, (B, L)
+        B, L = self._BL
+        st = self._fn(x.data_ptr(), self._wp, out.data_ptr(), B, L, self.K, _raw_stream(self._dev))
+        if st:
+            _lib.check(st, "conv1d_batch_hip")
+        return out
+
+
 def conv1d_valid(x: torch.Tensor, w: torch.Tensor, backend: str = "auto", out: torch.Tensor | None = None,
                  nthreads: int | None = None, blocking: bool = False) -> torch.Tensor:
     """y[b, i] = sum_k x[b, i+k] w[k] for x [B, L] (or [B,1,L]), w [K] -> y [B, L-K+1] (same rank as x).

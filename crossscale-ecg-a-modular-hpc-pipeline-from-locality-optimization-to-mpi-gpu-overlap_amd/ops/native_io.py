@@ -127,15 +127,21 @@ class NativePrefetcher:
             pass
 
 
-def upload_shards(paths: Sequence[str], device, n_rows: int, L: int, chunk_rows: int = 65536) -> torch.Tensor:
-    """Upload the first ``n_rows`` windows of ``paths`` into a new device tensor [n_rows, L]."""
+def upload_shards(paths: Sequence[str], device, n_rows: int, L: int, chunk_rows: int = 32768,
+                  threads: Optional[int] = None) -> torch.Tensor:
+    """Upload the first ``n_rows`` windows of ``paths`` into a new device tensor [n_rows, L].
+
+    ``threads`` host threads copy each chunk from the mmap'd shards into one of three pinned staging buffers
+    while the previous chunk's DMA runs (default: the process's usable CPUs, at most 8)."""
+    from ..utils import usable_cpus
     dev = torch.device(device)
     x = torch.empty((n_rows, L), dtype=torch.float32, device=dev)
     arr = _paths_array(list(paths))
     rows = C.c_int64()
     stream = torch.cuda.current_stream(dev)
-    _lib.check(_lib.io_lib().ecg_upload_shards(arr, len(paths), n_rows, L, x.data_ptr(), chunk_rows,
-                                               stream.cuda_stream, C.byref(rows)), "ecg_upload_shards")
+    th = int(threads) if threads else max(1, min(8, usable_cpus()))
+    _lib.check(_lib.io_lib().ecg_upload_shards_mt(arr, len(paths), n_rows, L, x.data_ptr(), chunk_rows, th,
+                                                  stream.cuda_stream, C.byref(rows)), "ecg_upload_shards")
     if rows.value != n_rows:
         raise RuntimeError(f"uploaded {rows.value} rows, expected {n_rows}")
     return x

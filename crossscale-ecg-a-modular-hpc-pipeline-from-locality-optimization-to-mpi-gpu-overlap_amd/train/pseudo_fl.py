@@ -18,6 +18,7 @@ import torch
 import torch.nn.functional as F
 
 from ..utils.csvio import BenchStats
+from ..utils.timing import warm_until_stable
 
 
 def _sync(device):
@@ -37,11 +38,12 @@ def run_baseline_gpu(model, batch_iter: Iterator, device, steps: int, rank: int,
     model = model.to(device)
     opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=0.9)
     model.train()
-    for _ in range(warmup):  # untimed: MIOpen solver search / allocator warm-up (not in the reference)
+    def warm():  # untimed: MIOpen solver search / first-use kernel compiles (not in the reference)
         x, y = next(batch_iter)
         F.cross_entropy(model(x), y).backward()
         opt.zero_grad(set_to_none=True)
-    _sync(device)
+
+    warm_until_stable(warm, device, min_steps=warmup)
     data_ms = compute_ms = step_ms = 0.0
     n_samples = n_steps = 0
     while n_steps < steps:
@@ -80,13 +82,14 @@ def run_overlap_gpu(model, batch_iter: Iterator, device, steps: int, rank: int, 
     side = torch.cuda.Stream(device)
     main = torch.cuda.current_stream(device)
     model.train()
-    for _ in range(warmup):  # untimed warm-up (MIOpen bf16 solver search)
+    def warm():  # untimed warm-up (MIOpen bf16 solver search / first-use compiles)
         x, y = next(batch_iter)
         with torch.autocast("cuda", dtype=amp_dtype):
             loss = F.cross_entropy(model(x), y)
         loss.backward()
         opt.zero_grad(set_to_none=True)
-    _sync(device)
+
+    warm_until_stable(warm, device, min_steps=warmup)
     data_ms = compute_ms = step_ms = 0.0
     n_samples = n_steps = 0
     t_d0 = time.perf_counter()

@@ -19,6 +19,27 @@ def sync(device: Optional[torch.device]) -> None:
         torch.cuda.synchronize(device)
 
 
+def warm_until_stable(step, device=None, min_steps: int = 5, max_steps: int = 200, window: int = 5,
+                      tol: float = 1.5) -> int:
+    """Untimed warm-up: run ``step()`` (synchronised) at least ``min_steps`` times and until the last ``window``
+    step times are all within ``tol`` x their minimum, at most ``max_steps``.  Returns the steps run.
+
+    A fixed 5-step warm-up (the reference's, bench_locality.py:29-38) is not enough on a fresh MI355X box: MIOpen
+    compiles some solvers' kernels at first use, and a compile that lands in the timed loop inflates the mean
+    step time by its whole duration (round 1: A4 at B=256 and G1_overlap_amp read 3-20x slower)."""
+    times = []
+    for i in range(max_steps):
+        t0 = time.perf_counter()
+        step()
+        sync(device)
+        times.append(time.perf_counter() - t0)
+        if i + 1 >= max(min_steps, window):
+            last = times[-window:]
+            if max(last) <= tol * min(last):
+                return i + 1
+    return max_steps
+
+
 class WallTimer:
     def __init__(self, device=None):
         self.device = device

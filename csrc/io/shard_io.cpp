@@ -380,19 +380,43 @@ ECG_API const char* ecg_prefetch_error(void* handle) {
 }
 
 // ------------------------------------------------------------------ bulk upload (GPU-resident shards)
-// Streams up to max_rows windows of the given shards into dst [max_rows, L] through two pinned staging
-// buffers of chunk_rows windows, overlapping the memcpy of chunk i+1 with the DMA of chunk i. Returns
-// rows uploaded in *rows_out.  Synchronises ``stream`` before returning (the staging buffers are freed).
-ECG_API int ecg_upload_shards(const char** paths, int npaths, int64_t max_rows, int64_t L, float* dst,
-                              int64_t chunk_rows, hipStream_t stream, int64_t* rows_out) {
+// Streams up to max_rows windows of the given shards into dst [max_rows, L] through kStages pinned staging
+// buffers of chunk_rows windows.  Per chunk, ``threads`` host threads copy disjoint slices of the mmap'd shard
+// into the free staging buffer (one thread cannot move page-cache bytes at the PCIe/DMA rate), then one
+// hipMemcpyAsync moves it to HBM while the next chunk is being copied: host copy and DMA overlap, and a
+// staging buffer is reused only after the event behind its DMA completed.  Returns rows uploaded in *rows_out.
+// Synchronises ``stream`` before returning (the staging buffers are freed).  Sized for multi-GB per-GPU shards
+// on 288 GB of HBM (Module_3/shard_dataset.py:103-115 does one pageable, effectively synchronous copy).
+constexpr int kStages = 3;
+
+void parallel_copy(float* dst, const float* src, size_t bytes, int threads) {
+  if (threads <= 1 || bytes < ((size_t)4 << 20)) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  std::vector<std::thread> pool;
+  const size_t per = (bytes / threads + 4095) & ~(size_t)4095;
+  for (int t = 0; t < threads; ++t) {
+    const size_t lo = std::min(bytes, (size_t)t * per), hi = std::min(bytes, lo + per);
+    if (lo >= hi) break;
+    pool.emplace_back([=] {
+      std::memcpy(reinterpret_cast<char*>(dst) + lo, reinterpret_cast<const char*>(src) + lo, hi - lo);
+    });
+  }
+  for (auto& th : pool) th.join();
+}
+
+ECG_API int ecg_upload_shards_mt(const char** paths, int npaths, int64_t max_rows, int64_t L, float* dst,
+                                 int64_t chunk_rows, int threads, hipStream_t stream, int64_t* rows_out) {
   if (!paths || npaths <= 0 || !dst || L <= 0 || chunk_rows <= 0) return kBadArg;
+  if (threads <= 0) threads = 1;
   const size_t chunk_bytes = (size_t)chunk_rows * L * sizeof(float);
-  float* stage[2] = {nullptr, nullptr};
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  bool pending[2] = {false, false};
+  float* stage[kStages] = {};
+  hipEvent_t ev[kStages] = {};
+  bool pending[kStages] = {};
   int st = kOk;
   int64_t row = 0;
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < kStages; ++i) {
     if (hipHostMalloc((void**)&stage[i], chunk_bytes, hipHostMallocDefault) != hipSuccess ||
         hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) {
       st = kHipError;
@@ -407,6 +431,7 @@ ECG_API int ecg_upload_shards(const char** paths, int npaths, int64_t max_rows, 
       st = kIoError;
       break;
     }
+    madvise(m.base, m.size, MADV_WILLNEED);
     int64_t off = 0;
     while (off < m.N && row < max_rows) {
       const int64_t take = std::min<int64_t>(std::min<int64_t>(chunk_rows, m.N - off), max_rows - row);
@@ -414,25 +439,30 @@ ECG_API int ecg_upload_shards(const char** paths, int npaths, int64_t max_rows, 
         (void)hipEventSynchronize(ev[s]);
         pending[s] = false;
       }
-      std::memcpy(stage[s], m.data() + off * L, (size_t)take * L * sizeof(float));
-      if (hipMemcpyAsync(dst + row * L, stage[s], (size_t)take * L * sizeof(float), hipMemcpyHostToDevice, stream) !=
-              hipSuccess ||
+      const size_t bytes = (size_t)take * L * sizeof(float);
+      parallel_copy(stage[s], m.data() + off * L, bytes, threads);
+      if (hipMemcpyAsync(dst + row * L, stage[s], bytes, hipMemcpyHostToDevice, stream) != hipSuccess ||
           hipEventRecord(ev[s], stream) != hipSuccess) {
         st = kHipError;
         break;
       }
       pending[s] = true;
-      s ^= 1;
+      s = (s + 1) % kStages;
       row += take;
       off += take;
     }
     close_map(&m);
   }
   (void)hipStreamSynchronize(stream);
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < kStages; ++i) {
     if (ev[i]) (void)hipEventDestroy(ev[i]);
     if (stage[i]) (void)hipHostFree(stage[i]);
   }
   if (rows_out) *rows_out = row;
   return st;
+}
+
+ECG_API int ecg_upload_shards(const char** paths, int npaths, int64_t max_rows, int64_t L, float* dst,
+                              int64_t chunk_rows, hipStream_t stream, int64_t* rows_out) {
+  return ecg_upload_shards_mt(paths, npaths, max_rows, L, dst, chunk_rows, 1, stream, rows_out);
 }

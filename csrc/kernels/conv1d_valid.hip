@@ -305,6 +305,18 @@ ECG_API int conv1d_batch_hip_sync(const float* x, const float* w, float* y, int 
   return ecg::kOk;
 }
 
+// Same, but the host polls the stream instead of sleeping in hipStreamSynchronize (no wake-up latency; the
+// calling thread spins for the few microseconds the kernel runs).
+ECG_API int conv1d_batch_hip_spin(const float* x, const float* w, float* y, int batch, int L, int K,
+                                  hipStream_t stream) {
+  const int st = launch_fwd<float, float>(x, w, y, batch, L, K, stream);
+  if (st) return st;
+  hipError_t e;
+  while ((e = hipStreamQuery(stream)) == hipErrorNotReady) {
+  }
+  return e == hipSuccess ? ecg::kOk : ecg::kHipError;
+}
+
 // bf16 activations in/out, fp32 taps and accumulation.
 ECG_API int conv1d_batch_hip_bf16(const __bf16* x, const float* w, __bf16* y, int batch, int L, int K,
                                   hipStream_t stream) {

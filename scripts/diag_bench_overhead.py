@@ -46,18 +46,16 @@ def main():
 
     def plan(k):
         def f():
-            done = 0
-            while done < k:
-                n = min(50, k - done)
-                tr.run_round(n, reset_loss=False)
-                done += n
+            sizes = [50] * (k // 50) + ([k % 50] if k % 50 else [])
+            for i, n in enumerate(sizes):  # staged like bench.py: next round's batches behind this round
+                tr.run_round(n, reset_loss=False, next_n=sizes[i + 1] if i + 1 < len(sizes) else None)
         return f
 
     print("bare synchronize: median %.1f us  min %.1f us" % timed(lambda: None))
-    print("index fill (20 rows): median %.1f us  min %.1f us" % timed(lambda: tr.sampler.fill(tr.idx_table[:20])))
+    print("index fill (20 rows): median %.1f us  min %.1f us" % timed(lambda: tr.sampler.fill(tr.idx_stage[:20])))
     for n in (1, 5, 20, 50):
-        med, mn = timed(lambda: tr.launch_round(n))
-        print(f"graph replay n={n:3d} (no fill): median {med:8.1f} us  min {mn:8.1f} us  -> {med / n:6.2f} us/step")
+        med, mn = timed(lambda: (tr.prepare_round(n, reset_loss=False), tr.launch_round(n)))
+        print(f"round n={n:3d} (fill + replay): median {med:8.1f} us  min {mn:8.1f} us  -> {med / n:6.2f} us/step")
     for k in (20, 50, 100, 500):
         med, mn = timed(plan(k))
         print(f"plan K={k:4d}: median {med:8.1f} us  min {mn:8.1f} us  -> {med / k:6.2f} us/step (min {mn / k:6.2f})")

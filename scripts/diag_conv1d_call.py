@@ -52,6 +52,13 @@ def main():
                                                         sync=False)))
         rows.append(("raw ctypes launch + sync", once(lambda: fn(xp, wp, op, B, L, K, raw(0)))))
         rows.append(("raw ctypes launch, no sync", once(lambda: fn(xp, wp, op, B, L, K, raw(0)), sync=False)))
+        from crossscale_ecg.ops.conv1d import HipConv1dValid
+        bop = HipConv1dValid(w, blocking=True)
+        x2 = x[:, 0].contiguous()
+        rows.append(("HipConv1dValid (bound, spin) + sync", once(lambda: bop(x2, out))))
+        rows.append(("HipConv1dValid (bound, spin), no sync", once(lambda: bop(x2, out), sync=False)))
+        rows.append(("spin C call, no sync", once(lambda: lib.conv1d_batch_hip_spin(xp, wp, op, B, L, K, raw(0)),
+                                                  sync=False)))
         if hasattr(lib, "conv1d_batch_hip_sync"):
             rows.append(("blocking C call (launch+hipStreamSynchronize)",
                          once(lambda: lib.conv1d_batch_hip_sync(xp, wp, op, B, L, K, raw(0)), sync=False)))

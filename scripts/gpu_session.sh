@@ -36,6 +36,7 @@ for s in $STEPS; do
     diag_g1) run diag_g1 600 python scripts/diag_g1_overlap.py "$OUT/diag_g1" ;;
     diag_call) run diag_overhead 300 python scripts/diag_bench_overhead.py
                run diag_conv1d_call 300 python scripts/diag_conv1d_call.py ;;
+    hbm) run hbm 600 python -m crossscale_ecg.bench.hbm --gb 16 --dir /tmp/ecg_hbm_shards --cleanup ;;
     module2) mkdir -p gpurun_out/results
              run module2 600 python benchmark_part_2.py --results-dir gpurun_out/results --batch-scaling ;;
     modules)
