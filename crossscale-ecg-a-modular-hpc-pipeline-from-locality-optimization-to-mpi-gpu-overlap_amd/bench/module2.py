@@ -7,9 +7,9 @@ Module_2/train_cpu_openmp.py (thread scaling at K=32).
 Two comparisons are produced:
   * ``part2_hip_results.csv``    - HIP conv1d vs ``torch.nn.Conv1d`` on the MI355X (MIOpen).  Three timings per
     cell.  HEADLINE ``speedup_med`` = the reference's metric: ``time_once`` (3 warm-up calls + ONE timed call,
-    host wall clock until the result is ready, then ``torch.cuda.synchronize()`` on both sides; the HIP side is
-    the bound blocking op ``HipConv1dValid`` - launch + host spin on the stream - the torch side the module call
-    ``conv(x)``), median of 15 trials.  Secondary:
+    host wall clock until the result is ready: the HIP side is the bound blocking op ``HipConv1dValid`` - launch
+    + stream wait in one native call - the torch side the module call ``conv(x)`` + ``torch.cuda.synchronize()``),
+    median of 15 trials.  Secondary:
     ``speedup_burst`` (50 back-to-back calls between syncs, host per-call cost) and ``speedup_ev`` (hipEvent
     device time per call).  Every cell is checked against an fp64 reference (``max_abs_err``).
   * ``part2_openmp_results.csv`` - the C++ OpenMP/AVX kernel (reference C ABI) vs CPU ``nn.Conv1d`` on the
@@ -110,7 +110,9 @@ def bench_pair_gpu(bs: int, K: int, rng: np.random.Generator, trials: int = TRIA
     t_call, h_call, t_b, h_b, t_e, h_e = [], [], [], [], [], []
     raw = []
     for _ in range(trials):
-        tc, hc = time_once(torch_step, sync=sync), time_once(hip_call, sync=sync)
+        # the blocking op returns with its output complete: no extra synchronize (it would only add its own
+        # ~3 us call cost); the async torch module needs one to reach the same point
+        tc, hc = time_once(torch_step, sync=sync), time_once(hip_call)
         t_call.append(tc)
         h_call.append(hc)
         raw.append((tc, hc))

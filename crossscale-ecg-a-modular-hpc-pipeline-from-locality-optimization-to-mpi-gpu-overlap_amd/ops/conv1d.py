@@ -73,9 +73,11 @@ def _conv1d_hip_fast(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None,
 class HipConv1dValid:
     """A bound single-channel valid conv1d on the HIP kernel - the op-object counterpart of ``nn.Conv1d(1, 1, K)``
     (taps held by the object, like the module holds its weight).  ``y = op(x, out)`` for x [B, L] / [B, 1, L]
-    fp32 on the taps' device, out [B, L-K+1].  ``blocking``: return when y is complete, the host spinning on
-    the stream (the reference CPU kernel's call semantics, Module_2/conv1d_openmp_simd.c:21-61); else async on
-    the current stream.  Per call it only re-checks the shapes and takes the data pointers."""
+    fp32 on the taps' device, out [B, L-K+1].  ``blocking``: return when y is complete (launch +
+    hipStreamSynchronize in one native call: the reference CPU kernel's call semantics,
+    Module_2/conv1d_openmp_simd.c:21-61; measured faster than polling hipStreamQuery, profiles/r2/
+    conv1d_single_call_breakdown.txt); else async on the current stream.  Per call it only re-checks the shapes
+    and takes the data pointers."""
 
     def __init__(self, w: torch.Tensor, blocking: bool = True):
         if not w.is_cuda:
@@ -83,7 +85,7 @@ class HipConv1dValid:
         self.w = w.detach().reshape(-1).to(torch.float32).contiguous()
         self.K = self.w.numel()
         lib = _lib.kernels()
-        self._fn = lib.conv1d_batch_hip_spin if blocking else lib.conv1d_batch_hip
+        self._fn = lib.conv1d_batch_hip_sync if blocking else lib.conv1d_batch_hip
         self._wp = self.w.data_ptr()
         self._dev = self.w.device.index
         self._shapes = None

@@ -36,6 +36,7 @@ for s in $STEPS; do
     diag_g1) run diag_g1 600 python scripts/diag_g1_overlap.py "$OUT/diag_g1" ;;
     diag_call) run diag_overhead 300 python scripts/diag_bench_overhead.py
                run diag_conv1d_call 300 python scripts/diag_conv1d_call.py ;;
+    diag_resnet) run diag_resnet 600 python scripts/diag_resnet_numerics.py ;;
     hbm) run hbm 600 python -m crossscale_ecg.bench.hbm --gb 16 --dir /tmp/ecg_hbm_shards --cleanup ;;
     module2) mkdir -p gpurun_out/results
              run module2 600 python benchmark_part_2.py --results-dir gpurun_out/results --batch-scaling ;;
@@ -52,6 +53,14 @@ for s in $STEPS; do
       run fedavg1 600 python part3_fedavg_overlap_mpi_gpu.py --synthetic-windows 20000 --rounds 5 \
         --local-steps 50 --config both --results-csv $R/fedavg_results_w1.csv
       run plots 300 python plot_results.py --results-dir $R
+      ;;
+    pmc)
+      export TMPDIR=/tmp
+      timeout -k 10 60 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
+      P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"
+      P2="SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD"
+      run pmc1 120 rocprofv3 --pmc $P1 --kernel-trace --output-format csv -d "$OUT/pmc1" -o tiny -- python3 scripts/pmc_tiny_step.py
+      run pmc2 120 rocprofv3 --pmc $P2 --kernel-trace --output-format csv -d "$OUT/pmc2" -o tiny -- python3 scripts/pmc_tiny_step.py
       ;;
     prof)
       export TMPDIR=/tmp
