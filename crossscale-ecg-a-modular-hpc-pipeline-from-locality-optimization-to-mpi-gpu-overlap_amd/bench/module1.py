@@ -77,7 +77,7 @@ class _Compute:
             st = _lib.kernels().ecg_tiny_train_step(x2.data_ptr(), x2.shape[1], x2.stride(0), None, y32.data_ptr(),
                                                     self.flat.data_ptr(), self.mom.data_ptr(), 2,
                                                     self.slab.data_ptr(), self.slab.shape[1], x2.shape[0],
-                                                    self.loss.data_ptr(), 1e-2, 0.0, 0.0, 0, None, None, 0,
+                                                    self.loss.data_ptr(), 1e-2, 0.0, 0.0, 0, None, None, 0, None,
                                                     _lib.stream_ptr(self.dev))
             _lib.check(st, "ecg_tiny_train_step")
             return

@@ -64,14 +64,16 @@ def _sig(lib, name, argtypes, restype=i32):
 def _bind_kernels(lib: C.CDLL) -> None:
     _sig(lib, "ecg_tiny_param_count", [i32])
     _sig(lib, "ecg_tiny_smem_bytes", [i32, i32])
-    _sig(lib, "ecg_tiny_step_grads", [vp, i32, i64, vp, vp, vp, i32, vp, i32, i32, f32, i32, vp])
-    _sig(lib, "ecg_tiny_forward", [vp, i32, i64, vp, vp, i32, vp, i32, i32, vp])
-    _sig(lib, "ecg_slab_reduce_sgd", [vp, i32, i32, i32, vp, vp, vp, vp, f32, f32, f32, i32, i32, vp])
+    _sig(lib, "ecg_tiny_step_grads", [vp, i32, i64, vp, vp, vp, i32, vp, i32, i32, f32, i32, vp, vp])
+    _sig(lib, "ecg_tiny_forward", [vp, i32, i64, vp, vp, i32, vp, i32, i32, vp, vp])
+    _sig(lib, "ecg_tiny_wprep_bytes", [])
+    _sig(lib, "ecg_tiny_prep", [vp, vp, vp])
+    _sig(lib, "ecg_slab_reduce_sgd", [vp, i32, i32, i32, vp, vp, vp, vp, f32, f32, f32, i32, i32, vp, vp])
     _sig(lib, "ecg_tiny_train_step", [vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, vp, f32, f32, f32, i32,
-                                      vp, vp, i32, vp])
+                                      vp, vp, i32, vp, vp])
     _sig(lib, "ecg_round_graph_create", [C.POINTER(vp), vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, i32, vp,
-                                         f32, f32, f32, i32, vp, vp, i32, vp])
-    _sig(lib, "ecg_tiny_step_grads_twice", [vp, i32, i64, vp, vp, vp, i32, vp, i32, i32, f32, i32, vp])
+                                         f32, f32, f32, i32, vp, vp, i32, vp, vp])
+    _sig(lib, "ecg_tiny_step_grads_twice", [vp, i32, i64, vp, vp, vp, i32, vp, i32, i32, f32, i32, vp, vp])
     _sig(lib, "ecg_tiny_round_ws_bytes", [i32, i32], i64)
     _sig(lib, "ecg_tiny_round_fits", [i32, i32, i32, i32])
     _sig(lib, "ecg_tiny_train_round", [vp, i32, i64, vp, vp, vp, vp, i32, i32, i32, vp, f32, f32, f32, i32, vp, i64,

@@ -21,6 +21,7 @@ accumulated on the device and read once per round (the reference syncs + ``loss.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Optional
 
 import torch
@@ -37,6 +38,24 @@ def prec_id(precision: str) -> int:
     if precision not in PRECISION:
         raise ValueError(f"precision must be one of {list(PRECISION)}, got {precision!r}")
     return PRECISION[precision]
+
+
+def prefrag_default() -> bool:
+    """Prepared fragments (PF) on by default; ECG_TINY_PREFRAG=0 builds the conv operands in LDS every step
+    (A/B knob: both paths are bitwise identical, csrc/kernels/tiny_ecg_step.hip WP_* comment)."""
+    return os.environ.get("ECG_TINY_PREFRAG", "1") != "0"
+
+
+def new_wprep(device) -> torch.Tensor:
+    """Device buffer for the prepared-fragment image (bf16 conv operands of the flat weights, MFMA lane order)."""
+    return torch.empty(_lib.kernels().ecg_tiny_wprep_bytes(), dtype=torch.uint8, device=device)
+
+
+def _wprep_ptr(precision: str, prefrag: Optional[bool], device, wprep: Optional[torch.Tensor] = None):
+    if precision != "bf16" or not (prefrag_default() if prefrag is None else prefrag):
+        return None, None
+    w = new_wprep(device) if wprep is None else wprep
+    return w.data_ptr(), w
 
 
 def slab_stride(num_classes: int) -> int:
@@ -67,8 +86,9 @@ def labels_int32(y: torch.Tensor, num_classes: int) -> torch.Tensor:
 
 
 def tiny_forward(flat_params: torch.Tensor, x: torch.Tensor, idx: Optional[torch.Tensor], batch: int,
-                 num_classes: int = 2, precision: str = "bf16") -> torch.Tensor:
-    """Logits [batch, C] of TinyECG for windows ``x[idx[b]]`` (or ``x[b]`` when idx is None)."""
+                 num_classes: int = 2, precision: str = "bf16", prefrag: Optional[bool] = None) -> torch.Tensor:
+    """Logits [batch, C] of TinyECG for windows ``x[idx[b]]`` (or ``x[b]`` when idx is None).  ``prefrag``: build
+    the prepared-fragment image first and run the PF kernel (default: ``prefrag_default()``)."""
     _check_dataset(x, None, num_classes)
     if idx is not None:
         _check_idx(idx, batch, x.shape[0], x.device)
@@ -76,16 +96,19 @@ def tiny_forward(flat_params: torch.Tensor, x: torch.Tensor, idx: Optional[torch
         raise ValueError("batch larger than dataset")
     out = torch.empty((batch, num_classes), dtype=torch.float32, device=x.device)
     lib = _lib.kernels()
+    wp, _keep = _wprep_ptr(precision, prefrag, x.device)
     st = lib.ecg_tiny_forward(x.data_ptr(), x.shape[1], x.stride(0), _lib.ptr(idx), flat_params.data_ptr(),
-                              num_classes, out.data_ptr(), batch, prec_id(precision), _lib.stream_ptr(x.device))
+                              num_classes, out.data_ptr(), batch, prec_id(precision), wp, _lib.stream_ptr(x.device))
     _lib.check(st, "ecg_tiny_forward")
     return out
 
 
 def tiny_step_grads(flat_params: torch.Tensor, x: torch.Tensor, y32: torch.Tensor, idx: Optional[torch.Tensor],
                     batch: int, num_classes: int = 2, slab: Optional[torch.Tensor] = None,
-                    precision: str = "bf16") -> torch.Tensor:
-    """Per-sample gradient slab [batch, stride] (loss in column P) of one fused step (no update)."""
+                    precision: str = "bf16", prefrag: Optional[bool] = None,
+                    wprep: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Per-sample gradient slab [batch, stride] (loss in column P) of one fused step (no update).  ``prefrag``:
+    rebuild the prepared-fragment image (``wprep``, or a temporary) from the weights and run the PF kernel."""
     _check_dataset(x, y32, num_classes)
     if idx is not None:
         _check_idx(idx, batch, x.shape[0], x.device)
@@ -93,9 +116,10 @@ def tiny_step_grads(flat_params: torch.Tensor, x: torch.Tensor, y32: torch.Tenso
     if slab is None:
         slab = torch.empty((batch, stride), dtype=torch.float32, device=x.device)
     lib = _lib.kernels()
+    wp, _keep = _wprep_ptr(precision, prefrag, x.device, wprep)
     st = lib.ecg_tiny_step_grads(x.data_ptr(), x.shape[1], x.stride(0), _lib.ptr(idx), y32.data_ptr(),
                                  flat_params.data_ptr(), num_classes, slab.data_ptr(), stride, batch,
-                                 1.0 / batch, prec_id(precision), _lib.stream_ptr(x.device))
+                                 1.0 / batch, prec_id(precision), wp, _lib.stream_ptr(x.device))
     _lib.check(st, "ecg_tiny_step_grads")
     return slab
 
@@ -107,7 +131,7 @@ def reduce_slab(slab: torch.Tensor, num_classes: int = 2):
     loss = torch.zeros(1, dtype=torch.float32, device=slab.device)
     lib = _lib.kernels()
     st = lib.ecg_slab_reduce_sgd(slab.data_ptr(), slab.shape[0], slab.shape[1], P, None, None, grad.data_ptr(),
-                                 loss.data_ptr(), 0.0, 0.0, 0.0, 0, 0, _lib.stream_ptr(slab.device))
+                                 loss.data_ptr(), 0.0, 0.0, 0.0, 0, 0, None, _lib.stream_ptr(slab.device))
     _lib.check(st, "ecg_slab_reduce_sgd")
     return grad, loss
 
@@ -122,7 +146,8 @@ class FusedTinyTrainer:
     def __init__(self, model: TinyECG, x_gpu: torch.Tensor, y_gpu: torch.Tensor, batch_size: int,
                  steps_per_round: int, lr: float = 1e-2, momentum: float = 0.9, weight_decay: float = 0.0,
                  nesterov: bool = False, seed: Optional[int] = None, use_graph: bool = True,
-                 single_launch: bool = False, precision: str = "bf16", persistent: Optional[bool] = None):
+                 single_launch: bool = False, precision: str = "bf16", persistent: Optional[bool] = None,
+                 prefrag: Optional[bool] = None):
         self.device = x_gpu.device
         self.precision = precision
         self.prec = prec_id(precision)
@@ -168,6 +193,11 @@ class FusedTinyTrainer:
         if persistent and not fits:
             raise ValueError(f"persistent round needs all {self.B} workgroups resident at once (B <= #CUs)")
         self.persistent = bool(persistent) and fits and not self.single_launch
+        # prepared fragments (two-launch bf16 steps): the round graph's first node rebuilds the image from the
+        # round's starting weights, every step's SGD keeps it current
+        pf = prefrag_default() if prefrag is None else bool(prefrag)
+        self.prefrag = pf and precision == "bf16" and not self.single_launch and not self.persistent
+        self.wprep = new_wprep(self.device) if self.prefrag else None
         self.status = torch.zeros(4, dtype=torch.int32, device=self.device)  # sticky give-up code
         self.ws = None
         if self.persistent:
@@ -193,7 +223,7 @@ class FusedTinyTrainer:
                                             self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
                                             n, self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd,
                                             int(self.nesterov), *self._fuse_ptrs(), self.prec,
-                                            self.idx_stage.data_ptr())
+                                            self.idx_stage.data_ptr(), _lib.ptr(self.wprep))
         _lib.check(st, "ecg_round_graph_create")
         self._graphs[n] = g
         return g
@@ -220,7 +250,8 @@ class FusedTinyTrainer:
                                      self.idx_table[s].data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
                                      self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
                                      self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd, int(self.nesterov),
-                                     *self._fuse_ptrs(), self.prec, _lib.stream_ptr(self.device))
+                                     *self._fuse_ptrs(), self.prec, _lib.ptr(self.wprep),
+                                     _lib.stream_ptr(self.device))
         _lib.check(st, "ecg_tiny_train_step")
 
     def _eager_round(self, n: int, stamps: Optional[torch.Tensor] = None):

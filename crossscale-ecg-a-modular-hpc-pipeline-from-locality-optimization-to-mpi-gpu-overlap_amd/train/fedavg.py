@@ -141,10 +141,11 @@ def _ddp_fused_round(trainer, ctx: DistContext, n: int):
     lib = _lib.kernels()
     for s in range(n):
         tiny_step_grads(trainer.params, trainer.x, trainer.y32, trainer.idx_table[s], trainer.B, trainer.nc,
-                        trainer.slab, precision=trainer.precision)
+                        trainer.slab, precision=trainer.precision, prefrag=getattr(trainer, "prefrag", None),
+                        wprep=getattr(trainer, "wprep", None))
         st = lib.ecg_slab_reduce_sgd(trainer.slab.data_ptr(), trainer.B, trainer.stride, trainer.P, None, None,
                                      trainer._ddp_grad.data_ptr(), trainer.loss_acc.data_ptr(), 0.0, 0.0, 0.0, 0, 0,
-                                     _lib.stream_ptr(trainer.device))
+                                     None, _lib.stream_ptr(trainer.device))
         _lib.check(st, "ecg_slab_reduce_sgd")
         allreduce_mean_(trainer._ddp_grad, ctx)
         trainer._ddp_opt.step()

@@ -98,6 +98,65 @@ __device__ __forceinline__ float ld_wt(__amdgpu_buffer_rsrc_t r, int idx) {
 // fp32 path: v_mfma_f32_16x16x4_f32 (exact f32 products, K = 80 = 20 k-steps of 4, no padding)
 constexpr int F32_KSTEPS = C * K2 / 4;
 
+// ---- prepared fragments (PF, bf16 path): the conv operands of the flat fp32 parameters in MFMA lane order,
+// kept in a small global image instead of being rebuilt in every workgroup's LDS every step.
+//   WP_FRAGF  bf16 [3][64][8]  conv2 forward operand   (element (r, co), r = 16k + ci, as put_param's fragF)
+//   WP_FRAGD  bf16 [3][64][8]  conv2 dgrad operand     (element (r, ci), r = 16k + co)
+//   WP_AW1    bf16 [16][8]     conv1 A operand row c: {w1[c][0..6], b1[c]}
+//   WP_B2     fp32 [16]        conv2 bias (byte offset WP_B2_BYTE)
+// tiny_prep_kernel writes the whole image from the flat parameters (the first node of every round graph: a
+// FedAvg all-reduce / broadcast / checkpoint load may have rewritten the weights between rounds), and
+// slab_reduce_sgd_kernel's SGD epilogue rewrites each updated parameter's slots, so inside a round the image
+// always equals what put_param would have built from ``params``: bitwise the same MFMA operands.  Every step
+// workgroup then loads its operands straight into VGPRs (7 x 16 B per lane, L2-hot: all 32 workgroups of an
+// XCD read the same 6.4 KB): no per-step scatter into LDS (1,280 x 2 two-byte stores + conversions per sample)
+// and no LDS round trip for the fragments in conv1 / conv2 / dgrad.
+constexpr int WP_FRAGF = 0;
+constexpr int WP_FRAGD = 3 * 64 * 8;
+constexpr int WP_AW1 = 2 * 3 * 64 * 8;
+constexpr int WP_B2_BYTE = (WP_AW1 + C * 8) * 2;  // 6400
+constexpr int WP_BYTES = WP_B2_BYTE + C * 4;     // 6464
+constexpr int kParamsW2End = C * K1 + C + C * C * K2;  // == make_layout(nc).b2 for every nc (1408)
+
+// Write flat parameter i's slots of the image (parameters past b2 - the head - have none).
+__device__ __forceinline__ void wprep_put(unsigned char* wp, int i, float v) {
+  __bf16* wb = reinterpret_cast<__bf16*>(wp);
+  if (i < C * K1) {
+    wb[WP_AW1 + (i / K1) * 8 + i % K1] = ecg::to_bf16(v);
+  } else if (i < C * K1 + C) {
+    wb[WP_AW1 + (i - C * K1) * 8 + 7] = ecg::to_bf16(v);
+  } else if (i < kParamsW2End) {
+    const int e = i - (C * K1 + C);
+    const int co = e / (C * K2), ci = (e / K2) % C, k = e % K2;
+    const int rf = 16 * k + ci, rd = 16 * k + co;
+    const __bf16 bv = ecg::to_bf16(v);
+    wb[WP_FRAGF + ((rf >> 5) * 64 + 16 * ((rf & 31) >> 3) + co) * 8 + (rf & 7)] = bv;
+    wb[WP_FRAGD + ((rd >> 5) * 64 + 16 * ((rd & 31) >> 3) + ci) * 8 + (rd & 7)] = bv;
+  } else if (i < kParamsW2End + C) {
+    reinterpret_cast<float*>(wp + WP_B2_BYTE)[i - kParamsW2End] = v;
+  }
+}
+
+// Block 0: the whole prepared-fragment image from ``params`` (K padding rows r in [80, 96) zero).  Blocks 1..:
+// optional int32 copy idx_src -> idx_dst (n ints; the round graph's staged batch rows), 4 KB per block.
+__global__ __launch_bounds__(256) void tiny_prep_kernel(const float* __restrict__ params,
+                                                        unsigned char* __restrict__ wp,
+                                                        const int* __restrict__ idx_src, int* __restrict__ idx_dst,
+                                                        long n_idx) {
+  const int tid = threadIdx.x;
+  if (blockIdx.x == 0) {
+    for (int i = tid; i < kParamsW2End + C; i += 256) wprep_put(wp, i, params[i]);
+    __bf16* wb = reinterpret_cast<__bf16*>(wp);
+    for (int e = tid; e < 2 * 32 * 8; e += 256) {
+      const int which = e >> 8, l = 32 + ((e >> 3) & 31), j = e & 7;
+      wb[(which ? WP_FRAGD : WP_FRAGF) + (2 * 64 + l) * 8 + j] = ecg::to_bf16(0.f);
+    }
+    return;
+  }
+  const long base = (long)(blockIdx.x - 1) * 1024;
+  for (long i = base + tid; i < n_idx && i < base + 1024; i += 256) idx_dst[i] = idx_src[i];
+}
+
 __host__ __device__ inline Smem make_smem(int L, int waves, int nc = MAX_CLASSES, bool f32 = false) {
   Smem s;
   s.Lp = (L + 31) / 32 * 32;
@@ -161,8 +220,9 @@ __device__ __forceinline__ float row16_sum(float v) {
 //   conv2 dgrad dh1^T[ci][t] = (g W2)[ci][(k,co)] x m[(k,co)][t], times relu'(h1), written over h1
 //   conv1 wgrad dW1ext[ci][kk] = dh1^T[ci][t] x xcol[t][kk]   (both operands by transposing reads; kk = 7 -> db1)
 // The fp32 path keeps conv1 / conv1-wgrad on VALU (exact f32) and the time-major MFMA orientation.
-template <int WAVES, bool F32>
+template <int WAVES, bool F32, bool PF = false>
 struct TinySample {
+  static_assert(!(PF && F32), "prepared fragments are bf16 operands");
   using AT = std::conditional_t<F32, float, __bf16>;  // activation / MFMA operand type
   static constexpr int NT = WAVES * 64;
   Smem sm;
@@ -180,6 +240,27 @@ struct TinySample {
   float* fragD32;          // fp32 path: [20][64] dgrad B operand
   float* red;
   uint32_t mask1 = 0u;     // relu'(h1) bits of this lane's conv1 outputs (phase 1 -> phase 4)
+  // PF: this lane's conv operands in registers, loaded from the global image (phase 0 / end of phase 2)
+  bf16x8 pf_aw, pf_wf[3], pf_wd[3];
+  f32x4 pf_b2;
+
+  __device__ __forceinline__ void pf_load_fwd(const unsigned char* __restrict__ wp) {
+    const __bf16* wb = reinterpret_cast<const __bf16*>(wp);
+    if (h == 0) {
+      pf_aw = *reinterpret_cast<const bf16x8*>(wb + WP_AW1 + c * 8);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf_aw[j] = ecg::to_bf16(0.f);
+    }
+#pragma unroll
+    for (int s = 0; s < 3; ++s) pf_wf[s] = *reinterpret_cast<const bf16x8*>(wb + WP_FRAGF + (s * 64 + lane) * 8);
+    pf_b2 = *reinterpret_cast<const f32x4*>(wp + WP_B2_BYTE + 16 * h);
+  }
+  __device__ __forceinline__ void pf_load_dgrad(const unsigned char* __restrict__ wp) {
+    const __bf16* wb = reinterpret_cast<const __bf16*>(wp);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) pf_wd[s] = *reinterpret_cast<const bf16x8*>(wb + WP_FRAGD + (s * 64 + lane) * 8);
+  }
 
   __device__ __forceinline__ TinySample(unsigned char* smem, int L_, int nc_)
       : sm(make_smem(L_, WAVES, nc_, F32)), lay(make_layout(nc_)), L(L_), nc(nc_) {
@@ -258,7 +339,7 @@ struct TinySample {
   // them, so once per launch.
   __device__ __forceinline__ void zero_pads() {
     if constexpr (!F32) {
-      for (int e = tid; e < 2 * 32 * 8; e += NT) {
+      for (int e = PF ? 2 * 32 * 8 : tid; e < 2 * 32 * 8; e += NT) {  // (PF: the image holds its own pads)
         const int which = e >> 8, l = 32 + ((e >> 3) & 31), j = e & 7;
         (which ? fragD : fragF)[(2 * 64 + l) * 8 + j] = ecg::to_bf16(0.f);
       }
@@ -281,10 +362,14 @@ struct TinySample {
     if constexpr (!F32) {
       // A = W1ext[co][kk]: quarter 0 holds kk 0..7 (taps, then the bias), quarters 1..3 the zero K padding
       bf16x8 Aw;
+      if constexpr (PF) {
+        Aw = pf_aw;
+      } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float v = j < K1 ? ps[lay.w1 + c * K1 + j] : ps[lay.b1 + c];
-        Aw[j] = ecg::to_bf16(h == 0 ? v : 0.f);
+        for (int j = 0; j < 8; ++j) {
+          const float v = j < K1 ? ps[lay.w1 + c * K1 + j] : ps[lay.b1 + c];
+          Aw[j] = ecg::to_bf16(h == 0 ? v : 0.f);
+        }
       }
       // B = xcol[t][kk]: quarter 0 reads the im2col row of its time step, quarters 1..3 the zero row.  Each wave
       // builds the rows of its own tiles from xs first (same-wave LDS order; phase 4 reads them after barriers).
@@ -355,14 +440,20 @@ struct TinySample {
       // out^T[co][t]: A = W2[co][(k,ci)] (the fragments are lane-order symmetric: the same registers serve as
       // B[(k,ci)][co] or A[co][(k,ci)]), B = h1col[(k,ci)][t] read straight from the [t][ci] rows
       bf16x8 Wf[3];
-#pragma unroll
-      for (int s = 0; s < 3; ++s) Wf[s] = *reinterpret_cast<const bf16x8*>(fragF + (s * 64 + lane) * 8);
       float b2v[4], pool[4], cnt[4];
+      if constexpr (PF) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        b2v[i] = ps[lay.b2 + 4 * h + i];
-        pool[i] = cnt[i] = 0.f;
+        for (int s = 0; s < 3; ++s) Wf[s] = pf_wf[s];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b2v[i] = pf_b2[i];
+      } else {
+#pragma unroll
+        for (int s = 0; s < 3; ++s) Wf[s] = *reinterpret_cast<const bf16x8*>(fragF + (s * 64 + lane) * 8);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b2v[i] = ps[lay.b2 + 4 * h + i];
       }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pool[i] = cnt[i] = 0.f;
 #pragma unroll
       for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
         const int pair = w + pi * WAVES;
@@ -589,7 +680,12 @@ struct TinySample {
       // (g W2) fragments, used as A[ci][(k,co)]
 #pragma unroll
       for (int s = 0; s < 3; ++s) {
-        const bf16x8 raw = *reinterpret_cast<const bf16x8*>(fragD + (s * 64 + lane) * 8);
+        bf16x8 raw;
+        if constexpr (PF) {
+          raw = pf_wd[s];
+        } else {
+          raw = *reinterpret_cast<const bf16x8*>(fragD + (s * 64 + lane) * 8);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) Bd[s][j] = ecg::to_bf16(ecg::from_bf16(raw[j]) * gq[j]);
       }
@@ -729,7 +825,7 @@ struct TinySample {
 // MODE 0: full training step (grads -> slab row).  MODE 1: forward only (logits -> out [B, nc]).
 // MODE 2: diagnostic - every workgroup computes its training step twice; the second pass runs with warm
 //         instruction / scalar / data caches (phase stamps of both passes: scripts/diag_step_phases.py).
-template <int WAVES, int MODE, bool F32>
+template <int WAVES, int MODE, bool F32, bool PF>
 __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     const float* __restrict__ X, int L, long ldx,        // dataset windows [N, ldx], window length L
     const int* __restrict__ idx,                         // [B] rows of X for this step (nullptr: b)
@@ -737,9 +833,9 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     const float* __restrict__ params, int nc,            // flat fp32 params
     float* __restrict__ out, int out_stride,             // MODE0/2: slab [B][out_stride]; MODE1: logits
     float inv_B, unsigned long long* __restrict__ stamps,   // stamps: diagnostic phase clock (nullptr = off)
-    FusedOpt opt) {
+    FusedOpt opt, const unsigned char* __restrict__ wprep) {  // wprep: PF image of ``params`` (PF only)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  TinySample<WAVES, F32> S(smem, L, nc);
+  TinySample<WAVES, F32, PF> S(smem, L, nc);
   constexpr bool TRAIN = MODE != 1;
   const int tid = threadIdx.x;
   const int b = blockIdx.x;
@@ -757,24 +853,38 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     // The parameter loads are issued first, into registers, so their round trip overlaps the dependent
     // idx -> window chain instead of following the window's LDS stores.
     int ylab = 0;
-    constexpr int PR = 4;  // parameters per thread held in registers (P <= PR * NT for nc <= 40 at 8 waves)
-    float pv[PR];
+    if constexpr (PF) {
+      // conv operands: global image -> VGPRs; only the head's parameters go to LDS (plain fp32 copy)
+      S.pf_load_fwd(wprep);
+      const int i = S.lay.wh + tid;
+      const float hv = i < S.lay.P ? params[i] : 0.f;
+      {
+        const long row = idx ? (long)idx[b] : (long)b;
+        if (TRAIN) ylab = Y[row];
+        S.stage_x(X + row * ldx);
+      }
+      if (i < S.lay.P) S.ps[i] = hv;
+      static_assert(MAX_CLASSES * C + MAX_CLASSES <= 8 * 64, "head parameters: one per thread");
+    } else {
+      constexpr int PR = 4;  // parameters per thread held in registers (P <= PR * NT for nc <= 40 at 8 waves)
+      float pv[PR];
 #pragma unroll
-    for (int j = 0; j < PR; ++j) {
-      const int i = tid + j * S.NT;
-      pv[j] = i < S.lay.P ? params[i] : 0.f;
-    }
-    {
-      const long row = idx ? (long)idx[b] : (long)b;
-      if (TRAIN) ylab = Y[row];  // label prefetched with the window (used by the head)
-      S.stage_x(X + row * ldx);
-    }
+      for (int j = 0; j < PR; ++j) {
+        const int i = tid + j * S.NT;
+        pv[j] = i < S.lay.P ? params[i] : 0.f;
+      }
+      {
+        const long row = idx ? (long)idx[b] : (long)b;
+        if (TRAIN) ylab = Y[row];  // label prefetched with the window (used by the head)
+        S.stage_x(X + row * ldx);
+      }
 #pragma unroll
-    for (int j = 0; j < PR; ++j) {
-      const int i = tid + j * S.NT;
-      if (i < S.lay.P) S.put_param(i, pv[j]);
+      for (int j = 0; j < PR; ++j) {
+        const int i = tid + j * S.NT;
+        if (i < S.lay.P) S.put_param(i, pv[j]);
+      }
+      for (int i = tid + PR * S.NT; i < S.lay.P; i += S.NT) S.put_param(i, params[i]);
     }
-    for (int i = tid + PR * S.NT; i < S.lay.P; i += S.NT) S.put_param(i, params[i]);
     S.zero_pads();
     __syncthreads();
     ECG_STAMP(1)
@@ -782,6 +892,7 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     __syncthreads();
     ECG_STAMP(2)
     S.conv2();
+    if constexpr (PF && TRAIN) S.pf_load_dgrad(wprep);  // lands under the barrier and the head phase
     __syncthreads();
     ECG_STAMP(3)
     S.template head_and_M<TRAIN>(ylab, inv_B, out, out_stride, b);
@@ -923,7 +1034,8 @@ template <int RED_COLS>
 __global__ __launch_bounds__(RED_COLS * RED_ROWG) void slab_reduce_sgd_kernel(
     const float* __restrict__ slab, int G, int stride, int P,
     float* __restrict__ params, float* __restrict__ mom, float* __restrict__ grad_out,
-    float* __restrict__ loss_acc, float lr, float momentum, float wd, int nesterov, int apply) {
+    float* __restrict__ loss_acc, float lr, float momentum, float wd, int nesterov, int apply,
+    unsigned char* __restrict__ wprep) {  // wprep: PF image kept current with the updated parameters (nullable)
   __shared__ float part[RED_ROWG][RED_COLS + 1];
   const int cl = threadIdx.x % RED_COLS, rg = threadIdx.x / RED_COLS;
   const int col = blockIdx.x * RED_COLS + cl;
@@ -962,7 +1074,9 @@ __global__ __launch_bounds__(RED_COLS * RED_ROWG) void slab_reduce_sgd_kernel(
           mom[col] = bm;
           d = nesterov ? d + momentum * bm : bm;
         }
-        params[col] = p - lr * d;
+        const float pn = p - lr * d;
+        params[col] = pn;
+        if (wprep) wprep_put(wprep, col, pn);
       }
     }
   }
@@ -1197,15 +1311,27 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_round_kernel(RoundArgs a)
 
 unsigned long long* g_stamps = nullptr;  // diagnostic phase stamps (ecg_tiny_set_stamps)
 
-template <int WAVES, int MODE, bool F32>
+template <int WAVES, int MODE, bool F32, bool PF>
 int launch_step(const float* X, int L, long ldx, const int* idx, const int* Y, const float* params, int nc,
-                float* out, int out_stride, int B, float inv_B, const FusedOpt& opt, hipStream_t stream) {
+                float* out, int out_stride, int B, float inv_B, const FusedOpt& opt, const unsigned char* wprep,
+                hipStream_t stream) {
   const Smem sm = make_smem(L, WAVES, nc, F32);
-  auto kern = tiny_ecg_step_kernel<WAVES, MODE, F32>;
+  auto kern = tiny_ecg_step_kernel<WAVES, MODE, F32, PF>;
   if (sm.bytes > 64 * 1024)
     ECG_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, sm.bytes));
   hipLaunchKernelGGL(kern, dim3(B), dim3(WAVES * 64), sm.bytes, stream, X, L, ldx, idx, Y, params, nc, out,
-                     out_stride, inv_B, g_stamps, opt);
+                     out_stride, inv_B, g_stamps, opt, wprep);
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
+}
+
+// The prepared-fragment image of ``params`` (+ optional idx copy), one launch.
+int launch_prep(const float* params, unsigned char* wprep, const int* idx_src, int* idx_dst, long n_idx,
+                hipStream_t stream) {
+  if (!params || !wprep || (n_idx > 0 && (!idx_src || !idx_dst))) return ecg::kBadArg;
+  const long nb = 1 + (n_idx > 0 ? (n_idx + 1023) / 1024 : 0);
+  hipLaunchKernelGGL(tiny_prep_kernel, dim3((unsigned)nb), dim3(256), 0, stream, params, wprep, idx_src, idx_dst,
+                     n_idx > 0 ? n_idx : 0);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
@@ -1241,30 +1367,42 @@ int check_step_args(int L, int nc, int B, int out_stride, int mode, bool f32 = f
   return ecg::kOk;
 }
 
-template <bool F32>
-int dispatch_prec(int mode, const float* X, int L, long ldx, const int* idx, const int* Y, const float* params,
-                  int nc, float* out, int out_stride, int B, float inv_B, const FusedOpt& opt, hipStream_t stream) {
-  const int waves = pick_waves(L, F32);
+template <bool F32, bool PF>
+int dispatch_cfg(int mode, int waves, const float* X, int L, long ldx, const int* idx, const int* Y,
+                 const float* params, int nc, float* out, int out_stride, int B, float inv_B, const FusedOpt& opt,
+                 const unsigned char* wprep, hipStream_t stream) {
   if (mode == 2)  // diagnostic (one wave count is enough)
-    return launch_step<8, 2, F32>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream);
+    return launch_step<8, 2, F32, PF>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, wprep, stream);
   if (mode == 0)
     return waves == 8
-               ? launch_step<8, 0, F32>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream)
-               : launch_step<16, 0, F32>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream);
-  return waves == 8 ? launch_step<8, 1, F32>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream)
-                    : launch_step<16, 1, F32>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream);
+               ? launch_step<8, 0, F32, PF>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, wprep, stream)
+               : launch_step<16, 0, F32, PF>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, wprep,
+                                             stream);
+  return waves == 8
+             ? launch_step<8, 1, F32, PF>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, wprep, stream)
+             : launch_step<16, 1, F32, PF>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, wprep, stream);
 }
 
-// prec: 0 = bf16 MFMA operands (AMP), 1 = fp32 (exact f32 MFMA)
+// prec: 0 = bf16 MFMA operands (AMP), 1 = fp32 (exact f32 MFMA).  ``wprep`` (bf16 only, not with the in-kernel
+// reduction of ``opt``): the kernel reads its conv operands from that prepared-fragment image, which the caller
+// keeps equal to ``params`` (launch_prep / slab_reduce_sgd_kernel); nullptr: the in-LDS build from ``params``.
 int step_dispatch(int mode, int prec, const float* X, int L, long ldx, const int* idx, const int* Y,
                   const float* params, int nc, float* out, int out_stride, int B, float inv_B, const FusedOpt& opt,
-                  hipStream_t stream) {
+                  const unsigned char* wprep, hipStream_t stream) {
   if (prec != 0 && prec != 1) return ecg::kBadArg;
   int st = check_step_args(L, nc, B, out_stride, mode, prec == 1);
   if (st) return st;
   if (opt.ctl && (!opt.gslab || !opt.params || (opt.momentum != 0.f && !opt.mom) || opt.G != B)) return ecg::kBadArg;
-  return prec == 1 ? dispatch_prec<true>(mode, X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream)
-                   : dispatch_prec<false>(mode, X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, stream);
+  if (wprep && (prec == 1 || opt.ctl)) return ecg::kBadArg;
+  const int waves = pick_waves(L, prec == 1);
+  if (prec == 1)
+    return dispatch_cfg<true, false>(mode, waves, X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt,
+                                     nullptr, stream);
+  if (wprep)
+    return dispatch_cfg<false, true>(mode, waves, X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt,
+                                     wprep, stream);
+  return dispatch_cfg<false, false>(mode, waves, X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt,
+                                    nullptr, stream);
 }
 
 FusedOpt no_fuse() {
@@ -1274,7 +1412,7 @@ FusedOpt no_fuse() {
 
 int reduce_dispatch(const float* slab, int G, int stride, int P, float* params, float* mom, float* grad_out,
                     float* loss_acc, float lr, float momentum, float wd, int nesterov, int apply,
-                    hipStream_t stream) {
+                    unsigned char* wprep, hipStream_t stream) {
   if (G <= 0 || P <= 0 || stride < P + 1) return ecg::kBadArg;
   if (apply && (!params || (momentum != 0.f && !mom))) return ecg::kBadArg;
   static const int cols = [] {  // ECG_RED_COLS in {4, 8, 16, 32, 64}: columns per reduction block (A/B knob)
@@ -1285,19 +1423,19 @@ int reduce_dispatch(const float* slab, int G, int stride, int P, float* params, 
   const int blocks = (P + 1 + cols - 1) / cols;
   if (cols == 4)
     hipLaunchKernelGGL(slab_reduce_sgd_kernel<4>, dim3(blocks), dim3(4 * RED_ROWG), 0, stream, slab, G, stride, P,
-                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply);
+                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply, wprep);
   else if (cols == 8)
     hipLaunchKernelGGL(slab_reduce_sgd_kernel<8>, dim3(blocks), dim3(8 * RED_ROWG), 0, stream, slab, G, stride, P,
-                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply);
+                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply, wprep);
   else if (cols == 64)
     hipLaunchKernelGGL(slab_reduce_sgd_kernel<64>, dim3(blocks), dim3(64 * RED_ROWG), 0, stream, slab, G, stride, P,
-                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply);
+                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply, wprep);
   else if (cols == 32)
     hipLaunchKernelGGL(slab_reduce_sgd_kernel<32>, dim3(blocks), dim3(32 * RED_ROWG), 0, stream, slab, G, stride, P,
-                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply);
+                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply, wprep);
   else
     hipLaunchKernelGGL(slab_reduce_sgd_kernel<16>, dim3(blocks), dim3(16 * RED_ROWG), 0, stream, slab, G, stride, P,
-                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply);
+                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply, wprep);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
@@ -1418,24 +1556,47 @@ ECG_API int ecg_tiny_smem_bytes(int L, int prec) {
   return make_smem(L, pick_waves(L, prec == 1), MAX_CLASSES, prec == 1).bytes;
 }
 
+// Bytes of the prepared-fragment image (``wprep`` below; 16-byte aligned device memory).
+ECG_API int ecg_tiny_wprep_bytes(void) { return WP_BYTES; }
+
+// Build the prepared-fragment image of ``params`` (bf16 conv operands in MFMA lane order).
+ECG_API int ecg_tiny_prep(const float* params, void* wprep, hipStream_t stream) {
+  return launch_prep(params, static_cast<unsigned char*>(wprep), nullptr, nullptr, 0, stream);
+}
+
+// Entry points below take an optional ``wprep`` (bf16 only): when given, the image is first rebuilt from
+// ``params`` (one small launch) and the step kernel reads its conv operands from it (PF path); nullptr builds
+// them in every workgroup's LDS.  Both give bitwise-identical results.
+static int prep_then(int mode, int prec, const float* X, int L, long ldx, const int* idx, const int* Y,
+                     const float* params, int nc, float* out, int out_stride, int B, float inv_B, void* wprep,
+                     hipStream_t stream) {
+  if (wprep) {
+    if (prec != 0) return ecg::kBadArg;
+    const int st = launch_prep(params, static_cast<unsigned char*>(wprep), nullptr, nullptr, 0, stream);
+    if (st) return st;
+  }
+  return step_dispatch(mode, prec, X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, no_fuse(),
+                       static_cast<const unsigned char*>(wprep), stream);
+}
+
 // One fused training step's gradient pass: writes slab[B][slab_stride] (grads + loss at column P).
 ECG_API int ecg_tiny_step_grads(const float* X, int L, long ldx, const int* idx, const int* Y,
                                 const float* params, int nc, float* slab, int slab_stride, int B, float inv_B,
-                                int prec, hipStream_t stream) {
-  return step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, inv_B, no_fuse(), stream);
+                                int prec, void* wprep, hipStream_t stream) {
+  return prep_then(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, inv_B, wprep, stream);
 }
 
 // Diagnostic twin of ecg_tiny_step_grads: every workgroup computes its sample twice (cold, then warm caches).
 ECG_API int ecg_tiny_step_grads_twice(const float* X, int L, long ldx, const int* idx, const int* Y,
                                       const float* params, int nc, float* slab, int slab_stride, int B, float inv_B,
-                                      int prec, hipStream_t stream) {
-  return step_dispatch(2, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, inv_B, no_fuse(), stream);
+                                      int prec, void* wprep, hipStream_t stream) {
+  return prep_then(2, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, inv_B, wprep, stream);
 }
 
 // Inference: logits[B][nc] for windows X[idx[b]].
 ECG_API int ecg_tiny_forward(const float* X, int L, long ldx, const int* idx, const float* params, int nc,
-                             float* logits, int B, int prec, hipStream_t stream) {
-  return step_dispatch(1, prec, X, L, ldx, idx, nullptr, params, nc, logits, nc, B, 0.f, no_fuse(), stream);
+                             float* logits, int B, int prec, void* wprep, hipStream_t stream) {
+  return prep_then(1, prec, X, L, ldx, idx, nullptr, params, nc, logits, nc, B, 0.f, wprep, stream);
 }
 
 // Size of the control block (int32 counters, must be zero before the first fused step) and of the
@@ -1445,27 +1606,42 @@ ECG_API int ecg_tiny_gslab_rows(void) { return kMaxGroups; }
 
 ECG_API int ecg_slab_reduce_sgd(const float* slab, int G, int stride, int P, float* params, float* mom,
                                 float* grad_out, float* loss_acc, float lr, float momentum, float wd, int nesterov,
-                                int apply, hipStream_t stream) {
+                                int apply, void* wprep, hipStream_t stream) {
+  if (wprep && !apply) return ecg::kBadArg;
   return reduce_dispatch(slab, G, stride, P, params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply,
+                         static_cast<unsigned char*>(wprep), stream);
+}
+
+// One training step; ``prep``: rebuild the PF image from ``params`` first (a round graph does it once per round).
+static int train_step(const float* X, int L, long ldx, const int* idx, const int* Y, float* params, float* mom,
+                      int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr, float momentum, float wd,
+                      int nesterov, int* ctl, float* gslab, int prec, unsigned char* wprep, bool prep,
+                      hipStream_t stream) {
+  if (ctl) {
+    if (wprep) return ecg::kBadArg;
+    FusedOpt o{ctl, gslab, params, mom, loss_acc, lr, momentum, wd, nesterov, B};
+    return step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, o, nullptr,
                          stream);
+  }
+  int st = ecg::kOk;
+  if (wprep && prep) st = launch_prep(params, wprep, nullptr, nullptr, 0, stream);
+  if (st) return st;
+  st = step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, no_fuse(), wprep,
+                     stream);
+  if (st) return st;
+  return reduce_dispatch(slab, B, slab_stride, make_layout(nc).P, params, mom, nullptr, loss_acc, lr, momentum, wd,
+                         nesterov, 1, wprep, stream);
 }
 
 // Full training step.  With ``ctl``/``gslab`` (see ecg_tiny_ctl_ints) it is ONE launch: per-sample
 // gradients, the in-kernel deterministic reduction tree and SGD.  Without them it is two launches
-// (gradient slab, then slab_reduce_sgd_kernel).
+// (gradient slab, then slab_reduce_sgd_kernel) - three with ``wprep`` (the PF image is rebuilt first).
 ECG_API int ecg_tiny_train_step(const float* X, int L, long ldx, const int* idx, const int* Y, float* params,
                                 float* mom, int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr,
-                                float momentum, float wd, int nesterov, int* ctl, float* gslab, int prec,
+                                float momentum, float wd, int nesterov, int* ctl, float* gslab, int prec, void* wprep,
                                 hipStream_t stream) {
-  if (ctl) {
-    FusedOpt o{ctl, gslab, params, mom, loss_acc, lr, momentum, wd, nesterov, B};
-    return step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, o, stream);
-  }
-  int st = step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, no_fuse(),
-                         stream);
-  if (st) return st;
-  return reduce_dispatch(slab, B, slab_stride, make_layout(nc).P, params, mom, nullptr, loss_acc, lr, momentum, wd,
-                         nesterov, 1, stream);
+  return train_step(X, L, ldx, idx, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr, momentum, wd, nesterov,
+                    ctl, gslab, prec, static_cast<unsigned char*>(wprep), true, stream);
 }
 
 // ---- persistent round (tiny_ecg_round_kernel)
@@ -1489,7 +1665,8 @@ ECG_API int ecg_tiny_train_round(const float* X, int L, long ldx, const int* idx
 static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws, long ws_bytes, int prec,
                          const float* X, int L, long ldx, const int* idx_table, const int* Y, float* params,
                          float* mom, int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr,
-                         float momentum, float wd, int nesterov, int* ctl, float* gslab, const int* idx_stage) {
+                         float momentum, float wd, int nesterov, int* ctl, float* gslab, const int* idx_stage,
+                         unsigned char* wprep) {
   hipStream_t cap;
   ECG_HIP_CHECK(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
   RoundGraph* rg = new RoundGraph();
@@ -1502,17 +1679,21 @@ static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws
   }
   int st = 0;
   // Staged batches: the round's index rows were enqueued into idx_stage one round ahead (while the previous round
-  // computed); the graph's first node moves them into the table every replay reads.
-  if (idx_stage && hipMemcpyAsync(const_cast<int*>(idx_table), idx_stage, (size_t)steps * B * sizeof(int),
-                                  hipMemcpyDeviceToDevice, cap) != hipSuccess)
+  // computed); the graph's first node moves them into the table every replay reads.  With a PF image that node is
+  // the prep kernel, which also rebuilds the image from the round's starting weights.
+  if (wprep) {
+    st = launch_prep(params, wprep, idx_stage, const_cast<int*>(idx_table), idx_stage ? (long)steps * B : 0, cap);
+  } else if (idx_stage && hipMemcpyAsync(const_cast<int*>(idx_table), idx_stage, (size_t)steps * B * sizeof(int),
+                                         hipMemcpyDeviceToDevice, cap) != hipSuccess) {
     st = ecg::kHipError;
+  }
   if (st) {
   } else if (pa) {
     st = round_dispatch(*pa, ws, ws_bytes, prec, cap);
   } else {
     for (int s = 0; s < steps && st == 0; ++s)
-      st = ecg_tiny_train_step(X, L, ldx, idx_table + (long)s * B, Y, params, mom, nc, slab, slab_stride, B,
-                               loss_acc, lr, momentum, wd, nesterov, ctl, gslab, prec, cap);
+      st = train_step(X, L, ldx, idx_table + (long)s * B, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr,
+                      momentum, wd, nesterov, ctl, gslab, prec, wprep, false, cap);
   }
   e = hipStreamEndCapture(cap, &rg->graph);
   (void)hipStreamDestroy(cap);
@@ -1533,16 +1714,20 @@ static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws
 
 // Capture ``steps`` consecutive fused steps (batch s reads idx_table + s*B) into one hipGraph.
 // All pointers are baked into the graph: callers keep the buffers alive and refill idx_table in place.
-// ``idx_stage`` (optional): the graph first copies idx_stage[0 : steps*B] into idx_table.
+// ``idx_stage`` (optional): the graph first copies idx_stage[0 : steps*B] into idx_table.  ``wprep`` (optional,
+// bf16, two-launch steps only): the PF image, rebuilt by the graph's first node and kept by every step's SGD.
 ECG_API int ecg_round_graph_create(void** handle, const float* X, int L, long ldx, const int* idx_table,
                                    const int* Y, float* params, float* mom, int nc, float* slab, int slab_stride,
                                    int B, int steps, float* loss_acc, float lr, float momentum, float wd,
-                                   int nesterov, int* ctl, float* gslab, int prec, const int* idx_stage) {
+                                   int nesterov, int* ctl, float* gslab, int prec, const int* idx_stage,
+                                   void* wprep) {
   if (!handle || steps <= 0) return ecg::kBadArg;
   int st = check_step_args(L, nc, B, slab_stride, 0, prec == 1);
   if (st) return st;
+  if (wprep && (prec != 0 || ctl)) return ecg::kBadArg;
   return capture_round(handle, steps, nullptr, nullptr, 0, prec, X, L, ldx, idx_table, Y, params, mom, nc, slab,
-                       slab_stride, B, loss_acc, lr, momentum, wd, nesterov, ctl, gslab, idx_stage);
+                       slab_stride, B, loss_acc, lr, momentum, wd, nesterov, ctl, gslab, idx_stage,
+                       static_cast<unsigned char*>(wprep));
 }
 
 // The persistent round (workspace memset + one launch) captured as a hipGraph, replayed once per round.
@@ -1555,7 +1740,7 @@ ECG_API int ecg_round_graph_create_persistent(void** handle, const float* X, int
   const RoundArgs a = make_round_args(X, L, ldx, idx_table, Y, params, mom, nc, B, steps, loss_acc, lr, momentum, wd,
                                       nesterov, ws, status, nullptr);
   return capture_round(handle, steps, &a, ws, ws_bytes, prec, X, L, ldx, idx_table, Y, params, mom, nc, nullptr, 0,
-                       B, loss_acc, lr, momentum, wd, nesterov, nullptr, nullptr, idx_stage);
+                       B, loss_acc, lr, momentum, wd, nesterov, nullptr, nullptr, idx_stage, nullptr);
 }
 
 ECG_API int ecg_round_graph_launch(void* handle, hipStream_t stream) {

@@ -60,9 +60,12 @@ def main():
     idx = torch.randperm(N, device=dev)[:B].int()
     lib = _lib.kernels()
     slab = torch.empty(B, slab_stride(2), device=dev)
-    print(f"gradient-only kernel (eager loop): {ev_time(lambda: tiny_step_grads(flat, x, y32, idx, B, 2, slab), 200):.2f} us")
-    for name, kw in (("two-launch  ", dict(persistent=False)), ("single-launch", dict(single_launch=True)),
-                     ("persistent  ", dict(persistent=True))):
+    for pf in (False, True):
+        t = ev_time(lambda: tiny_step_grads(flat, x, y32, idx, B, 2, slab, prefrag=pf), 200)
+        print(f"gradient-only kernel (eager loop, prefrag={pf}, PF adds the prep launch): {t:.2f} us")
+    for name, kw in (("two-launch LDS", dict(persistent=False, prefrag=False)),
+                     ("two-launch PF ", dict(persistent=False, prefrag=True)),
+                     ("single-launch", dict(single_launch=True)), ("persistent  ", dict(persistent=True))):
         m = TinyECG().to(dev)
         tr = FusedTinyTrainer(m, x, y, B, 50, seed=0, **kw)
         tr.run_round()
@@ -74,24 +77,26 @@ def main():
         print(f"{name} round: graph {t:.2f} us/step, eager {te:.2f} us/step")
         tr.close()
 
-    # cold vs warm passes of the per-step kernel (MODE 2)
-    st = torch.zeros(B * 16, dtype=torch.int64, device=dev)
-    lib.ecg_tiny_set_stamps(st.data_ptr())
-    for _ in range(5):
-        st.zero_()
-        _lib.check(lib.ecg_tiny_step_grads_twice(x.data_ptr(), L, x.stride(0), idx.data_ptr(), y32.data_ptr(),
-                                                 flat.data_ptr(), 2, slab.data_ptr(), slab.shape[1], B, 1.0 / B, 0,
-                                                 _lib.stream_ptr(dev)), "twice")
-    torch.cuda.synchronize()
-    lib.ecg_tiny_set_stamps(None)
-    s = st.view(B, 16).cpu()
-    cyc = (s[:, 6] - s[:, 0]).double()
-    rt = (s[:, 14] - s[:, 15]).double() * 10.0  # 100 MHz -> ns (both passes)
-    ghz = statistics.median(((s[:, 13] - s[:, 0]).double() / rt).tolist())
-    print(f"in-kernel clock ~{ghz:.2f} GHz")
-    phase_table(s, 0, NAMES, "per-step kernel, COLD pass (fresh launch):")
-    phase_table(s, 7, NAMES, "per-step kernel, WARM pass (same workgroup, immediately after):")
-    print(f"  cold total median {statistics.median(cyc.tolist()):.0f} cyc")
+    # cold vs warm passes of the per-step kernel (MODE 2), operands built in LDS vs prepared fragments (PF)
+    wprep = torch.empty(lib.ecg_tiny_wprep_bytes(), dtype=torch.uint8, device=dev)
+    for label, wp in (("LDS-built operands", None), ("prepared fragments (PF)", wprep.data_ptr())):
+        st = torch.zeros(B * 16, dtype=torch.int64, device=dev)
+        lib.ecg_tiny_set_stamps(st.data_ptr())
+        for _ in range(5):
+            st.zero_()
+            _lib.check(lib.ecg_tiny_step_grads_twice(x.data_ptr(), L, x.stride(0), idx.data_ptr(), y32.data_ptr(),
+                                                     flat.data_ptr(), 2, slab.data_ptr(), slab.shape[1], B, 1.0 / B,
+                                                     0, wp, _lib.stream_ptr(dev)), "twice")
+        torch.cuda.synchronize()
+        lib.ecg_tiny_set_stamps(None)
+        s = st.view(B, 16).cpu()
+        cyc = (s[:, 6] - s[:, 0]).double()
+        rt = (s[:, 14] - s[:, 15]).double() * 10.0  # 100 MHz -> ns (both passes)
+        ghz = statistics.median(((s[:, 13] - s[:, 0]).double() / rt).tolist())
+        print(f"[{label}] in-kernel clock ~{ghz:.2f} GHz")
+        phase_table(s, 0, NAMES, f"[{label}] per-step kernel, COLD pass (fresh launch):")
+        phase_table(s, 7, NAMES, f"[{label}] per-step kernel, WARM pass (same workgroup, immediately after):")
+        print(f"  cold total median {statistics.median(cyc.tolist()):.0f} cyc")
 
     # persistent round, warm step 1
     m = TinyECG().to(dev)

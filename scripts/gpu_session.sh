@@ -37,6 +37,13 @@ for s in $STEPS; do
     diag_call) run diag_overhead 300 python scripts/diag_bench_overhead.py
                run diag_conv1d_call 300 python scripts/diag_conv1d_call.py ;;
     diag_resnet) run diag_resnet 600 python scripts/diag_resnet_numerics.py ;;
+    tiny_tests) run tiny_tests 600 python -u -m pytest tests/test_fused_tiny_gpu.py -x -v -p no:cacheprovider \
+                  --timeout 120 --timeout-method thread ;;
+    diag_phases) run diag_phases 600 python scripts/diag_step_phases.py ;;
+    diag_pf) run diag_pf 300 python scripts/diag_prefrag.py ;;
+    bench_ab) run bench_pf 300 python bench.py --steps 500 --warmup 100 --no-extras
+              run bench_lds 300 env ECG_TINY_PREFRAG=0 python bench.py --steps 500 --warmup 100 --no-extras
+              run bench_pf20 300 python bench.py --steps 20 --warmup 5 --no-extras ;;
     hbm) run hbm 600 python -m crossscale_ecg.bench.hbm --gb 16 --dir /tmp/ecg_hbm_shards --cleanup ;;
     module2) mkdir -p gpurun_out/results
              run module2 600 python benchmark_part_2.py --results-dir gpurun_out/results --batch-scaling ;;

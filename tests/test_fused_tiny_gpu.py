@@ -266,3 +266,52 @@ def test_prepare_rollback_and_staged_rounds_bitwise():
         tr.close()
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     assert outs[0][2] == outs[1][2] and torch.equal(outs[0][3][:2], outs[1][3][:2])
+
+
+@pytest.mark.parametrize("B", [16, 256])
+def test_prefrag_grads_bitwise_equal_lds_path(B):
+    """Prepared-fragment kernel (conv operands from the global image) == LDS-built operands, bit for bit, for the
+    gradient slab and the forward logits."""
+    from crossscale_ecg.ops.fused_tiny import tiny_step_grads, tiny_forward, labels_int32
+    dev, x, y, model, idx = _setup(B=B, N=max(4 * B, 64))
+    flat = model.flatten_parameters()
+    y32 = labels_int32(y, 2)
+    from crossscale_ecg.models.tiny_ecg import num_params
+    P = num_params(2)  # columns [0, P]: gradient row + loss (the slab's padding columns are never written)
+    a = tiny_step_grads(flat, x, y32, idx, idx.numel(), 2, prefrag=True)[:, :P + 1]
+    b = tiny_step_grads(flat, x, y32, idx, idx.numel(), 2, prefrag=False)[:, :P + 1]
+    torch.cuda.synchronize()
+    d = (a - b).abs()
+    assert torch.equal(a, b), (d.max().item(), (d.amax(0) > 0).nonzero().flatten()[:20].tolist(),
+                               (d.amax(1) > 0).nonzero().flatten().tolist())
+    fa = tiny_forward(flat, x, idx, idx.numel(), 2, prefrag=True)
+    fb = tiny_forward(flat, x, idx, idx.numel(), 2, prefrag=False)
+    assert torch.equal(fa, fb)
+
+
+def test_prefrag_round_graph_bitwise_equal_lds_eager_with_external_updates():
+    """PF round graphs (image rebuilt by the graph's first node, kept by every step's SGD epilogue) reproduce the
+    LDS-built eager steps bit for bit over several rounds - also after the weights are rewritten between rounds
+    (what a FedAvg all-reduce / broadcast does)."""
+    from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
+    dev, x, y, model, _ = _setup(B=128, N=1024)
+    m2 = TinyECG().to(dev)
+    m2.load_state_dict(model.state_dict())
+    a = FusedTinyTrainer(model, x, y, 128, 7, seed=9, use_graph=True, persistent=False, prefrag=True)
+    b = FusedTinyTrainer(m2, x, y, 128, 7, seed=9, use_graph=False, persistent=False, prefrag=False)
+    assert a.prefrag and not b.prefrag
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    for r in range(4):
+        a.run_round()
+        b.run_round()
+        if r == 1:  # external rewrite of the weights between rounds
+            noise = torch.randn(a.params.shape, device=dev, generator=g) * 1e-2
+            a.params.add_(noise)
+            b.params.add_(noise)
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params), (a.params - b.params).abs().max()
+    assert torch.equal(a.mom, b.mom)
+    assert a.avg_loss() == b.avg_loss()
+    a.close()
+    b.close()
