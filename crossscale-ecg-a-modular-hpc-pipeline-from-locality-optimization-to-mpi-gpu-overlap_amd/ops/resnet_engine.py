@@ -295,6 +295,10 @@ class ResNetStepEngine:
 
         # =============================== head (loss + dlogits + dW/db)
         seg_begin = len(ops)
+        # op-range marks for per-block (teacher-forced) numerics checks: tests/test_resnet_engine_gpu.py
+        self._blocks, self._shapes, self._acts, self._bns, self._bn0 = blocks, shapes, acts, bns, bn0
+        self._fwd_end = seg_begin
+        self._bwd_marks: List[Tuple[int, int, int, torch.Tensor, torch.Tensor]] = []
         gbuf = self._t(B, ncls, dtype=torch.float32)
         fbuf = self._t(B, self.Cf, dtype=torch.float32)
         lbuf = self._t(B, dtype=torch.float32)
@@ -321,6 +325,7 @@ class ResNetStepEngine:
         for bi in range(len(blocks) - 1, -1, -1):
             (Li, Ci, Lo, Co, s), blk, a, (b1, b2, bd) = shapes[bi], blocks[bi], acts[bi], bns[bi]
             R = B * Lo
+            blk_begin = len(ops)
             dzm, din = gcur, nxt  # dzm: ReLU-masked grad wrt this block's output
             if bn2_src is None:  # last block: gradient from the head
                 ch = chunk_for(Co)
@@ -359,6 +364,9 @@ class ResNetStepEngine:
                 bn2_src = (stats_b.data_ptr(), Tn)
             else:  # into the stem: plain gradient wrt the pooled activations
                 conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=add)
+            # (block bi's ops: [blk_begin, len(ops)); they read dzm (the last block: unmasked, masked in place by
+            # BN_BWD_REDUCE) and write din (ReLU-masked for block bi-1; the stem's unmasked pooled gradient at bi=0)
+            self._bwd_marks.append((bi, blk_begin, len(ops), dzm, din))
             gcur, nxt = din, dzm
             if bi == 0 or stage_of[bi - 1] != stage_of[bi]:  # stage boundary: close a grad segment
                 if stage_of[bi] == 0:
