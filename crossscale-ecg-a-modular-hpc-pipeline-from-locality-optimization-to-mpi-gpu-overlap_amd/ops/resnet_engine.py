@@ -18,6 +18,7 @@ The reference has no ResNet; parity is against PyTorch's own fp32 ResNet1D (test
 from __future__ import annotations
 
 import ctypes
+import os
 import struct
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -253,11 +254,45 @@ class ResNetStepEngine:
                P(tickets), _f(n), _f(eps), _f(bnm), P(bn.weight), P(bn.bias), 0, 0, 0, 0, 0, 0,
                self._gptr(bn.weight), self._gptr(bn.bias), P(st.c1), P(st.c2), G)
 
-        def conv(x, Lin, Cin, w_ptr, y, Lout, Cout, K, s, p, dil=1, st=None, add=None, add_mask=None, bnb=None):
+        # ---- BatchNorm finalize fused into the statistics-producing conv (csrc/include/bn_tail.h): replaces the
+        # BN_FIN op (two launches) after each conv forward and data-grad conv.  ECG_BN_TAIL=0: separate BN_FIN ops.
+        use_tail = os.environ.get("ECG_BN_TAIL", "1") != "0"
+        self.bn_tail = use_tail
+        tail_blobs: List[bytes] = []
+        tails_dev = self._t(160 * 304, dtype=torch.uint8)  # room for 160 fused finalizes (ResNet-34 uses 68)
+
+        def fin_fwd_words(st: _BN, n):
+            bn = st.bn
+            return struct.pack("<qqddd12q", 0, 1, float(n), eps, bnm, P(bn.weight), P(bn.bias), P(st.mean),
+                               P(st.rstd), P(st.scale), P(st.shift), P(bn.running_mean), P(bn.running_var), 0, 0, 0, 0)
+
+        def fin_bwd_words(st: _BN, n, statB):
+            bn = st.bn
+            return struct.pack("<qqddd12q", 1, statB, float(n), eps, bnm, P(bn.weight), P(bn.bias), 0, 0, 0, 0, 0, 0,
+                               self._gptr(bn.weight), self._gptr(bn.bias), P(st.c1), P(st.c2))
+
+        def tail(T, Cout, fins) -> int:
+            if not use_tail:
+                return 0
+            gs = max(8, -(-T // 32))  # <= 32 groups: level 2 is one batch of loads (bn_tail.h)
+            NG = (T + gs - 1) // gs
+            cnt = torch.zeros((Cout // 64) * (NG + 1), dtype=torch.int32, device=dev)
+            self._keep.append(cnt)
+            gpart = self._t((Cout // 64) * NG * 3 * 64, dtype=torch.float64)
+            blob = struct.pack("<qqqq", cnt.data_ptr(), gpart.data_ptr(), gs, len(fins)) + b"".join(fins)
+            blob += b"\0" * (304 - len(blob))
+            tail_blobs.append(blob)
+            if len(tail_blobs) > 160:
+                raise RuntimeError("too many fused BatchNorm finalizes")
+            return tails_dev.data_ptr() + 304 * (len(tail_blobs) - 1)
+
+        def conv(x, Lin, Cin, w_ptr, y, Lout, Cout, K, s, p, dil=1, st=None, add=None, add_mask=None, bnb=None,
+                 tail_ptr=0):
             # bnb = (mask, z, mean, rstd, zd, mean_d, rstd_d): BN-backward statistics fused into the epilogue
             extra = [P(t) if isinstance(t, torch.Tensor) else int(t or 0) for t in (bnb or ())]
+            extra += [0] * (7 - len(extra))
             op("CONV_FWD", P(x), w_ptr, 0, P(y), P(st), P(add), P(add_mask), B, Lin, Cin, Lout, Cout, K, s, p, dil, 0,
-               *extra)
+               *extra, tail_ptr)
 
         def wgrad(dy, x, Lin, Cin, Lout, Cout, K, s, p, weight):
             S = wsplits(B * Lout, Cout, K, Cin)
@@ -278,14 +313,20 @@ class ResNetStepEngine:
         xin = self.h0
         for (Li, Ci, Lo, Co, s), blk, a, (b1, b2, bd) in zip(shapes, blocks, acts, bns):
             T = self.lib.ecg_conv1d_nlc_fwd_stat_tiles(B * Lo, Co)  # rows of the epilogue's BN partials
-            conv(xin, Li, Ci, self._wf[id(blk.conv1)], a["z1"], Lo, Co, 3, s, 1, st=stats)
-            fin_fwd(b1, T, B * Lo)
+            conv(xin, Li, Ci, self._wf[id(blk.conv1)], a["z1"], Lo, Co, 3, s, 1, st=stats,
+                 tail_ptr=tail(T, Co, [fin_fwd_words(b1, B * Lo)]))
+            if not use_tail:
+                fin_fwd(b1, T, B * Lo)
             op("BN_ACT", 0, P(a["z1"]), P(b1.scale), P(b1.shift), 0, 0, 0, P(a["a1"]), B * Lo, Co)
-            conv(a["a1"], Lo, Co, self._wf[id(blk.conv2)], a["z2"], Lo, Co, 3, 1, 1, st=stats)
-            fin_fwd(b2, T, B * Lo)
+            conv(a["a1"], Lo, Co, self._wf[id(blk.conv2)], a["z2"], Lo, Co, 3, 1, 1, st=stats,
+                 tail_ptr=tail(T, Co, [fin_fwd_words(b2, B * Lo)]))
+            if not use_tail:
+                fin_fwd(b2, T, B * Lo)
             if bd is not None:
-                conv(xin, Li, Ci, self._wf[id(blk.downsample[0])], a["zd"], Lo, Co, 1, s, 0, st=stats)
-                fin_fwd(bd, T, B * Lo)
+                conv(xin, Li, Ci, self._wf[id(blk.downsample[0])], a["zd"], Lo, Co, 1, s, 0, st=stats,
+                     tail_ptr=tail(T, Co, [fin_fwd_words(bd, B * Lo)]))
+                if not use_tail:
+                    fin_fwd(bd, T, B * Lo)
                 op("BN_ACT", 2, P(a["z2"]), P(b2.scale), P(b2.shift), P(a["zd"]), P(bd.scale), P(bd.shift),
                    P(a["out"]), B * Lo, Co)
             else:
@@ -333,11 +374,12 @@ class ResNetStepEngine:
                 op("BN_BWD_REDUCE", 3 if bd is not None else 2, P(gcur), P(a["out"]), P(a["z2"]), P(b2.mean),
                    P(b2.rstd), P(a.get("zd")), P(bd.mean) if bd else 0, P(bd.rstd) if bd else 0, P(bpart), R, Co, ch,
                    P(dzm))
-                bn2_src = (bpart.data_ptr(), Tb)
-            base, T2 = bn2_src
-            fin_bwd(b2, T2, R, 1, base)
-            if bd is not None:
-                fin_bwd(bd, T2, R, 2, base)
+                bn2_src = (bpart.data_ptr(), Tb, False)
+            base, T2, fused = bn2_src
+            if not fused:  # (fused: the data-grad conv that produced the statistics already finalized them)
+                fin_bwd(b2, T2, R, 1, base)
+                if bd is not None:
+                    fin_bwd(bd, T2, R, 2, base)
             op("BN_BWD_APPLY", 1 if bd is not None else 0, P(dzm), 0, P(a["z2"]), P(b2.mean), P(b2.rstd),
                P(b2.scale), P(b2.c1), P(b2.c2), P(dz2), P(a.get("zd")), P(bd.mean) if bd else 0,
                P(bd.rstd) if bd else 0, P(bd.scale) if bd else 0, P(bd.c2) if bd else 0, P(dzd), R, Co)
@@ -345,8 +387,9 @@ class ResNetStepEngine:
             # dgrad conv2 (stride 1, pad 1) -> ReLU-masked grad wrt a1 + BN1 backward statistics
             T1 = self.lib.ecg_conv1d_nlc_fwd_stat_tiles(R, Co)
             conv(dz2, Lo, Co, self._wb[id(blk.conv2)], ga1, Lo, Co, 3, 1, 1, st=stats,
-                 bnb=(a["a1"], a["z1"], b1.mean, b1.rstd, 0, 0, 0))
-            fin_bwd(b1, T1, R, 1, stats.data_ptr())
+                 bnb=(a["a1"], a["z1"], b1.mean, b1.rstd, 0, 0, 0), tail_ptr=tail(T1, Co, [fin_bwd_words(b1, R, 1)]))
+            if not use_tail:
+                fin_bwd(b1, T1, R, 1, stats.data_ptr())
             op("BN_BWD_APPLY", 0, P(ga1), 0, P(a["z1"]), P(b1.mean), P(b1.rstd), P(b1.scale), P(b1.c1),
                P(b1.c2), P(dz1), 0, 0, 0, 0, 0, 0, R, Co)
             wgrad(dz1, a["in"], Li, Ci, Lo, Co, 3, s, 1, blk.conv1.weight)
@@ -358,10 +401,11 @@ class ResNetStepEngine:
             if bi > 0:  # din is the previous block's output gradient: mask it and emit that block's BN2 stats
                 pa, (_, pb2, pbd) = acts[bi - 1], bns[bi - 1]
                 Tn = self.lib.ecg_conv1d_nlc_fwd_stat_tiles_ex(B, Li, Ci, s)  # phase-decomposed when s > 1
+                fins = [fin_bwd_words(pb2, B * Li, 1)] + ([fin_bwd_words(pbd, B * Li, 2)] if pbd else [])
                 conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=add, st=stats_b,
                      bnb=(pa["out"], pa["z2"], pb2.mean, pb2.rstd, pa.get("zd") if pbd else 0,
-                          pbd.mean if pbd else 0, pbd.rstd if pbd else 0))
-                bn2_src = (stats_b.data_ptr(), Tn)
+                          pbd.mean if pbd else 0, pbd.rstd if pbd else 0), tail_ptr=tail(Tn, Ci, fins))
+                bn2_src = (stats_b.data_ptr(), Tn, use_tail)
             else:  # into the stem: plain gradient wrt the pooled activations
                 conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=add)
             # (block bi's ops: [blk_begin, len(ops)); they read dzm (the last block: unmasked, masked in place by
@@ -388,6 +432,10 @@ class ResNetStepEngine:
         # =============================== optimizer
         op("SGD", P(self.flat), P(self.grad), P(self.mom), self.space.param_numel, _f(self.lr), _f(self.momentum),
            _f(self.wd), int(self.nesterov))
+        if tail_blobs:
+            blob = torch.frombuffer(bytearray(b"".join(tail_blobs)), dtype=torch.uint8)
+            tails_dev[:blob.numel()].copy_(blob)
+        self.n_bn_tails = len(tail_blobs)
         self.ops = torch.tensor(ops, dtype=torch.int64)
         self.n_ops = len(ops)
         # grad segments must tile [0, param_numel) back to front

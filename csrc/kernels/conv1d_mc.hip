@@ -18,6 +18,7 @@
 // next tile's global loads issued before the current tile's MFMAs (register staging).
 #include "../include/ecg_common.h"
 
+#include "../include/bn_tail.h"
 #include <climits>
 #include <cstdlib>
 
@@ -50,6 +51,7 @@ struct FwdArgs {
   const __bf16* szd;
   const float* smean_d;
   const float* srstd_d;
+  const ecg::BnTail* tail;  // BatchNorm finalize fused into this launch's tail (bn_tail.h), or null
 };
 
 // A tile: 64 rows (b,t) x 64 kk (one tap k, channels c0..c0+63); element e (0..511) = row e>>3, 8 bf16 part e&7
@@ -228,7 +230,11 @@ __device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, f32x4 (&acc)[BM /
       float v = 0.f;
 #pragma unroll
       for (int r = 0; r < NWR; ++r) v += sred[(3 * r + st) * BN + c];
-      a.stats[((long)st * MT + mt) * a.Cout + n0 + c] = v;
+      float* dst = a.stats + ((long)st * MT + mt) * a.Cout + n0 + c;
+      if (a.tail)
+        ecg::st_sc1(dst, v);  // handed to the tail's last arriver inside this launch (write-through)
+      else
+        *dst = v;
     }
   }
 }
@@ -347,6 +353,7 @@ __global__ __launch_bounds__(THREADS, NBUF == 1 ? 3 : 2) void conv1d_nlc_fwd_ker
     }
   }
   fwd_epilogue<BM, BN, EPI>(a, acc, smem, m0, n0, mt, MT, Lrow, M, P, ph);
+  if (a.tail && a.stats) ecg::bn_tail<THREADS>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, MT, a.Cout, mt, n0, BN, smem);
 }
 
 // LDS-DMA main loop (forward and non-dilated data-grad): every 16-byte piece of the A (activation rows) and B
@@ -461,6 +468,8 @@ __global__ __launch_bounds__(128 * NWR, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_d
     }
   }
   fwd_epilogue<BM, BN, EPI, NWR>(a, acc, smem, m0, n0, mt, MT, a.Lout, M, 1, 0);
+  if (a.tail && a.stats)
+    ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, MT, a.Cout, mt, n0, BN, smem);
 }
 
 inline bool conv_dma();
@@ -973,11 +982,12 @@ inline bool wgrad_big(int Cout, int Cin) { return conv_big() >= 2 && Cout % 256 
 ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bias, void* y, float* stats,
                                   const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
                                   int Kw, int stride, int pad, int in_dil, int relu, const void* const* bnb,
-                                  hipStream_t stream) {
+                                  const void* tail, hipStream_t stream) {
   if (!x || !w || !y || B <= 0 || Lin <= 0 || Lout <= 0 || Kw <= 0 || stride <= 0 || in_dil <= 0 || pad < 0)
     return ecg::kBadArg;
   if (Cin % BK != 0 || Cout % 64 != 0 || (add_mask && !add)) return ecg::kBadArg;
   if (bnb && (!stats || !bnb[1] || !bnb[2] || !bnb[3] || (bnb[4] && (!bnb[5] || !bnb[6])))) return ecg::kBadArg;
+  if (tail && !stats) return ecg::kBadArg;
   FwdArgs a{static_cast<const __bf16*>(x), static_cast<const __bf16*>(w), bias, static_cast<__bf16*>(y), stats,
             static_cast<const __bf16*>(add), static_cast<const __bf16*>(add_mask),
             B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil, relu, bnb ? 1 : 0};
@@ -990,6 +1000,7 @@ ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bia
     a.smean_d = static_cast<const float*>(bnb[5]);
     a.srstd_d = static_cast<const float*>(bnb[6]);
   }
+  a.tail = static_cast<const ecg::BnTail*>(tail);
   int bm, bn;
   pick_fwd_tile((long)B * Lout, Cout, in_dil, &bm, &bn);
   if (bm == 256 && bn == 256) return launch_fwd<256, 256>(a, stream);
@@ -1026,7 +1037,7 @@ ECG_API int ecg_conv1d_nlc_fwd(const void* x, const void* w, const float* bias, 
                                int Lout, int Cout, int Kw, int stride, int pad, int in_dil, int relu,
                                hipStream_t stream) {
   return ecg_conv1d_nlc_fwd_ex(x, w, bias, y, nullptr, nullptr, nullptr, B, Lin, Cin, Lout, Cout, Kw, stride, pad,
-                               in_dil, relu, nullptr, stream);
+                               in_dil, relu, nullptr, nullptr, stream);
 }
 
 // Partial weight gradients: part[splits][Cout][Kw*Cin] fp32 (sum over dim 0 = dw in [Cout][Kw][Cin]).

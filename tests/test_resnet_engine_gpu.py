@@ -224,3 +224,25 @@ def test_engine_teacher_forced_numerics(depth):
     check("stem.conv1.weight", _g(eng, m.conv1.weight), dW0, 0.02)
     top = sorted(worst.items(), key=lambda kv: -kv[1])[:8]
     print(f"depth {depth}: worst per-tensor relative errors", [(k, round(v, 5)) for k, v in top])
+
+
+def test_engine_bn_tail_matches_separate_finalize(monkeypatch):
+    """BatchNorm finalize fused into the statistics-producing convs (default) == the separate two-launch BN_FIN
+    ops (ECG_BN_TAIL=0) up to fp64 summation order, with one fewer plan op per fused finalize."""
+    depth = 34
+    monkeypatch.setenv("ECG_BN_TAIL", "1")
+    m, ref, eng, x, y = _setup(depth, B=64, use_graph=True)
+    monkeypatch.setenv("ECG_BN_TAIL", "0")
+    from crossscale_ecg.ops.resnet_engine import ResNetStepEngine
+    eng0 = ResNetStepEngine(ref, 64, 500, use_graph=True)
+    eng0.set_batch(x, y)
+    assert eng.bn_tail and not eng0.bn_tail and eng.n_bn_tails > 0
+    assert eng0.n_ops > eng.n_ops + eng.n_bn_tails - 1  # every fused tail removed at least one BN_FIN op
+    for _ in range(3):  # the counters are reset by every launch's final reducers
+        eng.forward_backward()
+        eng0.forward_backward()
+    torch.cuda.synchronize()
+    assert _rel(eng.grad, eng0.grad) < 1e-5
+    for (n, b), (_, b0) in zip(m.named_buffers(), ref.named_buffers()):
+        if b.is_floating_point():
+            assert _rel(b, b0) < 1e-5, n
