@@ -20,6 +20,7 @@
 #include "../include/ecg_common.h"
 
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace {
@@ -371,31 +372,42 @@ struct TinySample {
           Aw[j] = ecg::to_bf16(h == 0 ? v : 0.f);
         }
       }
-      // B = xcol[t][kk]: quarter 0 reads the im2col row of its time step, quarters 1..3 the zero row.  Each wave
-      // builds the rows of its own tiles from xs first (same-wave LDS order; phase 4 reads them after barriers).
-      const __bf16* xb = xcol + (h == 0 ? (lane & 15) * 8 : Lp * 8);
-      const int tstride = h == 0 ? 16 * 8 : 0;
+      // B = xcol[t][kk] (K = 32: quarter 0 holds kk 0..7, quarters 1..3 the zero padding).  Quarter-0 lane n reads
+      // the 7 window samples of its time step t = 16*tile + n straight from xs into registers (no write -> read
+      // round trip through the im2col image) and stores the row once for phase 4's conv1 wgrad.  Tiles go two
+      // at a time, every LDS read of the pair issued before the first MFMA.
       const int ntiles = Lp / 16;
+#pragma unroll 1
+      for (int pi = 0; pi < 2 * MAX_PAIRS_PER_WAVE; pi += 2) {
+        if (w + pi * WAVES >= ntiles) break;  // wave-uniform
+        float xv[2][K1];
+        int tq[2];
 #pragma unroll
-      for (int pi = 0; pi < 2 * MAX_PAIRS_PER_WAVE; ++pi) {
-        const int tile = w + pi * WAVES;
-        if (tile < ntiles) {
-          {  // this wave's im2col rows of the tile: lane (n, h) writes columns 2h, 2h+1 of row t = 16*tile + n
-            const int t = 16 * tile + (lane & 15), j0 = 2 * h;
-            const bool tv = t < L;
-            const float v0 = xs[t + j0], v1 = j0 + 1 < K1 ? xs[t + j0 + 1] : 1.f;  // column 7: bias x 1
-            bf16x2 pr;
-            pr[0] = ecg::to_bf16(tv ? v0 : 0.f);
-            pr[1] = ecg::to_bf16(tv ? v1 : 0.f);
-            *reinterpret_cast<bf16x2*>(xcol + t * 8 + j0) = pr;
+        for (int u = 0; u < 2; ++u) {
+          const int tile = min(w + (pi + u) * WAVES, ntiles - 1);  // clamped: loads never branch
+          tq[u] = 16 * tile + (lane & 15);
+#pragma unroll
+          for (int j = 0; j < K1; ++j) xv[u][j] = xs[tq[u] + j];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int tile = w + (pi + u) * WAVES;
+          const bool tv = tq[u] < L;
+          bf16x8 Bx;
+#pragma unroll
+          for (int j = 0; j < K1; ++j) Bx[j] = ecg::to_bf16(tv ? xv[u][j] : 0.f);
+          Bx[7] = ecg::to_bf16(tv ? 1.f : 0.f);  // column 7: bias x "t < L"
+          if (tile < ntiles && h == 0) *reinterpret_cast<bf16x8*>(xcol + tq[u] * 8) = Bx;
+          if (h != 0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) Bx[j] = ecg::to_bf16(0.f);
           }
-          const bf16x8 Bx = *reinterpret_cast<const bf16x8*>(xb + tile * tstride);
           const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Aw, Bx, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
           // acc[i] = conv1(x)[t = 16*tile + (lane&15)][co = 4h + i] + bias (exactly 0 for t >= L)
           bf16x4 o;
 #pragma unroll
           for (int i = 0; i < 4; ++i) o[i] = (AT)fmaxf(acc[i], 0.f);
-          *reinterpret_cast<bf16x4*>(h1s + (16 * tile + (lane & 15) + 2) * C + 4 * h) = o;
+          if (tile < ntiles) *reinterpret_cast<bf16x4*>(h1s + (16 * tile + (lane & 15) + 2) * C + 4 * h) = o;
         }
       }
       return;
@@ -458,17 +470,27 @@ struct TinySample {
       for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
         const int pair = w + pi * WAVES;
         if (pair < NP) {
+          // all six B fragments of the pair first (one LDS round trip), then two independent MFMA chains
+          bf16x8 Bh[2][3];
+#pragma unroll
+          for (int half = 0; half < 2; ++half)
+#pragma unroll
+            for (int s = 0; s < 3; ++s) {
+              const int r = 32 * pair + 16 * half + (lane & 15) + 2 * s + (h >> 1) - 2;  // h1 time index
+              Bh[half][s] = *reinterpret_cast<const bf16x8*>(h1s + (r + 2) * C + 8 * (h & 1));
+            }
+          f32x4 accs[2];
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            accs[half] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 3; ++s)
+              accs[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Wf[s], Bh[half][s], accs[half], 0, 0, 0);
+          }
 #pragma unroll
           for (int half = 0; half < 2; ++half) {
             const int t0 = 32 * pair + 16 * half;
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int s = 0; s < 3; ++s) {
-              const int tap = 2 * s + (h >> 1);
-              const int r = t0 + (lane & 15) + tap - 2;  // h1 time index
-              const bf16x8 Bh = *reinterpret_cast<const bf16x8*>(h1s + (r + 2) * C + 8 * (h & 1));
-              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Wf[s], Bh, acc, 0, 0, 0);
-            }
+            const f32x4 acc = accs[half];
             // acc[i] = conv2(h1)[t = t0 + (lane&15)][co = 4h + i]
             const int t = t0 + (lane & 15);
             const bool tv = t < L;
@@ -696,24 +718,35 @@ struct TinySample {
       for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
         const int pair = w + pi * WAVES;
         if (pair < NP) {
+          // both halves' mask fragments and h1 values first (one LDS round trip), then the two MFMA chains
+          bf16x8 Am[2][3];
+          bf16x4 hv[2];
 #pragma unroll
           for (int half = 0; half < 2; ++half) {
             const int t0 = 32 * pair + 16 * half;
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int s = 0; s < 3; ++s) {
-              const int k = 2 * s + (h >> 1);
-              const int r = t0 + (lane & 15) - k + 2;  // mask time index
-              const bf16x8 Am = *reinterpret_cast<const bf16x8*>(ms + (r + 4) * C + 8 * (h & 1));
-              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Bd[s], Am, acc, 0, 0, 0);
+              const int r = t0 + (lane & 15) - (2 * s + (h >> 1)) + 2;  // mask time index
+              Am[half][s] = *reinterpret_cast<const bf16x8*>(ms + (r + 4) * C + 8 * (h & 1));
             }
+            hv[half] = *reinterpret_cast<const bf16x4*>(h1s + (t0 + (lane & 15) + 2) * C + 4 * h);
+          }
+          f32x4 accs[2];
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            accs[half] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 3; ++s)
+              accs[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Bd[s], Am[half][s], accs[half], 0, 0, 0);
+          }
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
             // acc[i] = dh1[t = t0 + (lane&15)][ci = 4h + i]; times relu'(h1), written over h1 (this wave's rows)
-            AT* hp = h1s + (t0 + (lane & 15) + 2) * C + 4 * h;
-            const bf16x4 hv = *reinterpret_cast<const bf16x4*>(hp);
+            const int t0 = 32 * pair + 16 * half;
             bf16x4 dv;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) dv[i] = ecg::to_bf16((float)hv[i] > 0.f ? acc[i] : 0.f);
-            *reinterpret_cast<bf16x4*>(hp) = dv;
+            for (int i = 0; i < 4; ++i) dv[i] = ecg::to_bf16((float)hv[half][i] > 0.f ? accs[half][i] : 0.f);
+            *reinterpret_cast<bf16x4*>(h1s + (t0 + (lane & 15) + 2) * C + 4 * h) = dv;
           }
           // conv1 wgrad over the pair's 32 steps: A[ci][t] = dh1 (transposing reads of the rows just written by
           // this wave), B[t][kk] = xcol (columns 8..15 come from the zero row); reduction slots as in phase 3
@@ -1311,6 +1344,20 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_round_kernel(RoundArgs a)
 
 unsigned long long* g_stamps = nullptr;  // diagnostic phase stamps (ecg_tiny_set_stamps)
 
+// Diagnostic ablation (timing only, results are wrong): ECG_TINY_ABLATE=reduce|step|both replaces the slab
+// reduction and/or the step kernel by an empty kernel of the same grid and LDS (scripts/diag_ablate.py).
+__global__ void ablate_kernel(float* out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0 && out) out[0] = 0.f;
+}
+inline int ablate_mode() {
+  static int m = -1;
+  if (m < 0) {
+    const char* e = getenv("ECG_TINY_ABLATE");
+    m = !e ? 0 : (strcmp(e, "reduce") == 0 ? 1 : strcmp(e, "step") == 0 ? 2 : strcmp(e, "both") == 0 ? 3 : 0);
+  }
+  return m;
+}
+
 template <int WAVES, int MODE, bool F32, bool PF>
 int launch_step(const float* X, int L, long ldx, const int* idx, const int* Y, const float* params, int nc,
                 float* out, int out_stride, int B, float inv_B, const FusedOpt& opt, const unsigned char* wprep,
@@ -1319,6 +1366,11 @@ int launch_step(const float* X, int L, long ldx, const int* idx, const int* Y, c
   auto kern = tiny_ecg_step_kernel<WAVES, MODE, F32, PF>;
   if (sm.bytes > 64 * 1024)
     ECG_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, sm.bytes));
+  if (MODE == 0 && (ablate_mode() & 2)) {
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)ablate_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, sm.bytes));
+    hipLaunchKernelGGL(ablate_kernel, dim3(B), dim3(WAVES * 64), sm.bytes, stream, nullptr);
+    return ecg::kOk;
+  }
   hipLaunchKernelGGL(kern, dim3(B), dim3(WAVES * 64), sm.bytes, stream, X, L, ldx, idx, Y, params, nc, out,
                      out_stride, inv_B, g_stamps, opt, wprep);
   ECG_HIP_CHECK(hipGetLastError());
@@ -1421,6 +1473,10 @@ int reduce_dispatch(const float* slab, int G, int stride, int P, float* params, 
     return (v == 4 || v == 8 || v == 16 || v == 32 || v == 64) ? v : kRedColsDefault;
   }();
   const int blocks = (P + 1 + cols - 1) / cols;
+  if (ablate_mode() & 1) {
+    hipLaunchKernelGGL(ablate_kernel, dim3(blocks), dim3(cols * RED_ROWG), 0, stream, nullptr);
+    return ecg::kOk;
+  }
   if (cols == 4)
     hipLaunchKernelGGL(slab_reduce_sgd_kernel<4>, dim3(blocks), dim3(4 * RED_ROWG), 0, stream, slab, G, stride, P,
                        params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply, wprep);

@@ -41,6 +41,7 @@ for s in $STEPS; do
                   --timeout 120 --timeout-method thread ;;
     diag_phases) run diag_phases 600 python scripts/diag_step_phases.py ;;
     diag_pf) run diag_pf 300 python scripts/diag_prefrag.py ;;
+    diag_labl) run diag_labl 300 python scripts/diag_labl.py ;;
     bench_ab) run bench_pf 300 python bench.py --steps 500 --warmup 100 --no-extras
               run bench_lds 300 env ECG_TINY_PREFRAG=0 python bench.py --steps 500 --warmup 100 --no-extras
               run bench_pf20 300 python bench.py --steps 20 --warmup 5 --no-extras ;;
