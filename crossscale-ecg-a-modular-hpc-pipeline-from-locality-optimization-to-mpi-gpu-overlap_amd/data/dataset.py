@@ -17,6 +17,7 @@ MI355X-first additions:
 """
 from __future__ import annotations
 
+import warnings
 from typing import Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -96,15 +97,22 @@ def load_shards_to_gpu(shard_paths: Sequence[str], device, max_windows: Optional
         return ds.x.to(device), ds.y.to(device)
 
     if use_native is None or use_native:
-        try:
-            from ..ops import native_io
-            if native_io.available():
+        from ..ops import native_io
+        if native_io.available():
+            try:
                 x = native_io.upload_shards(shard_paths, device, n_total, L)
                 y = _labels_on_device(x, labels)
                 return x, y
-        except Exception:
-            if use_native:
-                raise
+            except Exception as e:  # the native uploader exists but failed: say so, then take the torch path
+                if use_native:
+                    raise
+                warnings.warn(f"load_shards_to_gpu: native upload failed ({e!r}); using the torch pinned path",
+                              RuntimeWarning, stacklevel=2)
+        elif use_native:
+            raise RuntimeError("load_shards_to_gpu(use_native=True): libecg_io.so is not available")
+        else:
+            warnings.warn("load_shards_to_gpu: libecg_io.so not available; using the torch pinned path",
+                          RuntimeWarning, stacklevel=2)
 
     x = torch.empty((n_total, L), dtype=torch.float32, device=device)
     copy_stream = torch.cuda.Stream(device=device)

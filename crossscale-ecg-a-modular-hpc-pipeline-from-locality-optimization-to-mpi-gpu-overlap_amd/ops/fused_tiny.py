@@ -47,8 +47,9 @@ def prefrag_default() -> bool:
 
 
 def new_wprep(device) -> torch.Tensor:
-    """Device buffer for the prepared-fragment image (bf16 conv operands of the flat weights, MFMA lane order)."""
-    return torch.empty(_lib.kernels().ecg_tiny_wprep_bytes(), dtype=torch.uint8, device=device)
+    """Device buffer for the prepared-fragment image (bf16 conv operands of the flat weights, MFMA lane order).
+    Zero-initialised: the K-padding slots are never written by the SGD epilogue that keeps the image current."""
+    return torch.zeros(_lib.kernels().ecg_tiny_wprep_bytes(), dtype=torch.uint8, device=device)
 
 
 def _wprep_ptr(precision: str, prefrag: Optional[bool], device, wprep: Optional[torch.Tensor] = None):
@@ -193,8 +194,9 @@ class FusedTinyTrainer:
         if persistent and not fits:
             raise ValueError(f"persistent round needs all {self.B} workgroups resident at once (B <= #CUs)")
         self.persistent = bool(persistent) and fits and not self.single_launch
-        # prepared fragments (two-launch bf16 steps): the round graph's first node rebuilds the image from the
-        # round's starting weights, every step's SGD keeps it current
+        # prepared fragments (two-launch bf16 steps): a round's first step runs on the LDS path (the weights may
+        # have been rewritten since: FedAvg, broadcast, checkpoint) and its SGD epilogue rewrites the whole image;
+        # every later step of the round reads it
         pf = prefrag_default() if prefrag is None else bool(prefrag)
         self.prefrag = pf and precision == "bf16" and not self.single_launch and not self.persistent
         self.wprep = new_wprep(self.device) if self.prefrag else None
@@ -205,7 +207,10 @@ class FusedTinyTrainer:
 
     # ------------------------------------------------------------------ graph management
     def _graph_for(self, n: int) -> C.c_void_p:
-        g = self._graphs.get(n)
+        # PF rounds read the staged table in place (no copy node) and the two index buffers swap roles after every
+        # launch, so there is one graph per (size, buffer)
+        key = (n, self.idx_stage.data_ptr()) if self.prefrag else n
+        g = self._graphs.get(key)
         if g is not None:
             return g
         g = C.c_void_p()
@@ -218,15 +223,21 @@ class FusedTinyTrainer:
                 self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd, int(self.nesterov), self.ws.data_ptr(),
                 self.ws.numel(), self.status.data_ptr(), self.prec, self.idx_stage.data_ptr())
         else:
+            tab, stage = (self.idx_stage, None) if self.prefrag else (self.idx_table, self.idx_stage)
             st = lib.ecg_round_graph_create(C.byref(g), self.x.data_ptr(), self.x.shape[1], self.x.stride(0),
-                                            self.idx_table.data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
+                                            tab.data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
                                             self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
                                             n, self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd,
                                             int(self.nesterov), *self._fuse_ptrs(), self.prec,
-                                            self.idx_stage.data_ptr(), _lib.ptr(self.wprep))
+                                            _lib.ptr(stage), _lib.ptr(self.wprep))
         _lib.check(st, "ecg_round_graph_create")
-        self._graphs[n] = g
+        self._graphs[key] = g
         return g
+
+    def _swap_tables(self) -> None:
+        """After a PF graph launch: the buffer it read becomes ``idx_table`` (the last round's batches), the other
+        one receives the next staging (enqueued behind the replay on the same stream)."""
+        self.idx_table, self.idx_stage = self.idx_stage, self.idx_table
 
     def close(self):
         graphs, self._graphs = getattr(self, "_graphs", {}), {}
@@ -246,6 +257,15 @@ class FusedTinyTrainer:
 
     def _eager_step(self, s: int):
         lib = _lib.kernels()
+        if self.prefrag:
+            st = lib.ecg_tiny_train_step_pf(self.x.data_ptr(), self.x.shape[1], self.x.stride(0),
+                                            self.idx_table[s].data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
+                                            self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
+                                            self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd,
+                                            int(self.nesterov), self.wprep.data_ptr(), int(s > 0),
+                                            _lib.stream_ptr(self.device))
+            _lib.check(st, "ecg_tiny_train_step_pf")
+            return
         st = lib.ecg_tiny_train_step(self.x.data_ptr(), self.x.shape[1], self.x.stride(0),
                                      self.idx_table[s].data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
                                      self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
@@ -278,13 +298,17 @@ class FusedTinyTrainer:
             return
         lib = _lib.kernels()
         sizes = [self._check_n(n) for n in sizes]
-        snap = [t.clone() for t in (self.params, self.mom, self.loss_acc, self.idx_stage, self.status)]
+        state = (self.params, self.mom, self.loss_acc, self.idx_stage, self.idx_table, self.status)
+        snap = [t.clone() for t in state]
         stream = _lib.stream_ptr(self.device)
         for n in sizes:
-            g = self._graph_for(n)
-            _lib.check(lib.ecg_round_graph_upload(g, stream), "ecg_round_graph_upload")
-            _lib.check(lib.ecg_round_graph_launch(g, stream), "ecg_round_graph_launch")
-        for t, v in zip((self.params, self.mom, self.loss_acc, self.idx_stage, self.status), snap):
+            for _ in range(2 if self.prefrag else 1):  # PF: both index buffers
+                g = self._graph_for(n)
+                _lib.check(lib.ecg_round_graph_upload(g, stream), "ecg_round_graph_upload")
+                _lib.check(lib.ecg_round_graph_launch(g, stream), "ecg_round_graph_launch")
+                if self.prefrag:
+                    self._swap_tables()
+        for t, v in zip(state, snap):
             t.copy_(v)
         torch.cuda.synchronize(self.device)
 
@@ -329,6 +353,8 @@ class FusedTinyTrainer:
             g = self._graph_for(n)
             _lib.check(_lib.kernels().ecg_round_graph_launch(g, _lib.stream_ptr(self.device)),
                        "ecg_round_graph_launch")
+            if self.prefrag:
+                self._swap_tables()
         else:
             self.idx_table[:n].copy_(self.idx_stage[:n])
             if self.persistent:

@@ -206,6 +206,8 @@ def run_fedavg(cfg: FedAvgConfig, ctx: DistContext) -> List[Dict]:
         # ResNet engine: the tail step applies SGD per backward segment and all-reduces each segment at once
         seg_tail = mode == "tail" and hasattr(trainer, "tail_fedavg")
         fround = FedAvgRound(model_flat(model), fcomm, "none" if seg_tail else mode)
+        if hasattr(trainer, "prepare"):  # capture + upload + warm the round graphs outside round 0's timing
+            trainer.prepare([cfg.local_steps - 1 if seg_tail else cfg.local_steps])
         recs = []
         for r in range(start_round, cfg.rounds):
             t_round0 = time.perf_counter()

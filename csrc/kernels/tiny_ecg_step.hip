@@ -75,6 +75,7 @@ struct FusedOpt {
   float lr, momentum, wd;
   int nesterov;
   int G;             // number of workgroups (= batch)
+  int slab_wt;       // two-launch path: store the gradient rows write-through (ECG_TINY_SLAB_WT, default on)
 };
 // conv2 wgrad work split: 5 taps x msplit(WAVES) pair ranges, one (tap, range) per wave 1.. (wave 0 runs the head)
 __host__ __device__ constexpr int msplit(int waves) { return (waves - 1) / 5 < 1 ? 1 : (waves - 1) / 5; }
@@ -937,7 +938,7 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     ECG_STAMP(5)
     // phase 5: combine partials, scale by g, write this sample's gradient row.  The single-launch reduction
     // below reads it inside this launch (write-through stores); otherwise the kernel boundary publishes it.
-    if (opt.ctl != nullptr) {
+    if (opt.ctl != nullptr || opt.slab_wt) {
       for (int i = tid; i <= S.lay.P; i += S.NT) st_wt(slab_r, rowbase + i, S.row_value(i));
     } else {
       for (int i = tid; i <= S.lay.P; i += S.NT) out[rowbase + i] = S.row_value(i);
@@ -1459,6 +1460,14 @@ int step_dispatch(int mode, int prec, const float* X, int L, long ldx, const int
 
 FusedOpt no_fuse() {
   FusedOpt o{};
+  // Write-through gradient rows (default): the rows leave the XCD L2s while the step runs instead of in the
+  // boundary's write-back, and the reduce kernel finds them beyond L2: 11.1 vs 11.4 us/step (bench, A/B x2,
+  // profiles/r2/bench_slab_wt.txt).  ECG_TINY_SLAB_WT=0 restores plain stores.
+  static const int wt = [] {
+    const char* e = getenv("ECG_TINY_SLAB_WT");
+    return e && atoi(e) == 0 ? 0 : 1;
+  }();
+  o.slab_wt = wt;
   return o;
 }
 
@@ -1668,10 +1677,13 @@ ECG_API int ecg_slab_reduce_sgd(const float* slab, int G, int stride, int P, flo
                          static_cast<unsigned char*>(wprep), stream);
 }
 
-// One training step; ``prep``: rebuild the PF image from ``params`` first (a round graph does it once per round).
+// One training step.  With a PF image ``wprep``: ``image`` 0 = rebuild it from ``params`` first (prep launch),
+// 1 = it is current (read it), 2 = it is stale - run this step's kernel on the LDS path and let its SGD epilogue
+// rewrite the whole image (every parameter slot is updated every step; the K-padding slots stay zero from the
+// zero-initialised allocation), which is how a round starts without a prep launch.
 static int train_step(const float* X, int L, long ldx, const int* idx, const int* Y, float* params, float* mom,
                       int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr, float momentum, float wd,
-                      int nesterov, int* ctl, float* gslab, int prec, unsigned char* wprep, bool prep,
+                      int nesterov, int* ctl, float* gslab, int prec, unsigned char* wprep, int image,
                       hipStream_t stream) {
   if (ctl) {
     if (wprep) return ecg::kBadArg;
@@ -1680,10 +1692,10 @@ static int train_step(const float* X, int L, long ldx, const int* idx, const int
                          stream);
   }
   int st = ecg::kOk;
-  if (wprep && prep) st = launch_prep(params, wprep, nullptr, nullptr, 0, stream);
+  if (wprep && image == 0) st = launch_prep(params, wprep, nullptr, nullptr, 0, stream);
   if (st) return st;
-  st = step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, no_fuse(), wprep,
-                     stream);
+  st = step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, no_fuse(),
+                     image == 2 ? nullptr : wprep, stream);
   if (st) return st;
   return reduce_dispatch(slab, B, slab_stride, make_layout(nc).P, params, mom, nullptr, loss_acc, lr, momentum, wd,
                          nesterov, 1, wprep, stream);
@@ -1697,7 +1709,19 @@ ECG_API int ecg_tiny_train_step(const float* X, int L, long ldx, const int* idx,
                                 float momentum, float wd, int nesterov, int* ctl, float* gslab, int prec, void* wprep,
                                 hipStream_t stream) {
   return train_step(X, L, ldx, idx, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr, momentum, wd, nesterov,
-                    ctl, gslab, prec, static_cast<unsigned char*>(wprep), true, stream);
+                    ctl, gslab, prec, static_cast<unsigned char*>(wprep), 0, stream);
+}
+
+// Two-launch training step that keeps a zero-initialised PF image current without prep launches: ``image_current``
+// 0 runs the LDS-path kernel (e.g. the first step after the weights were changed outside the step loop) and its
+// SGD epilogue rewrites the whole image; 1 reads the image (every later step).
+ECG_API int ecg_tiny_train_step_pf(const float* X, int L, long ldx, const int* idx, const int* Y, float* params,
+                                   float* mom, int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr,
+                                   float momentum, float wd, int nesterov, void* wprep, int image_current,
+                                   hipStream_t stream) {
+  if (!wprep) return ecg::kBadArg;
+  return train_step(X, L, ldx, idx, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr, momentum, wd, nesterov,
+                    nullptr, nullptr, 0, static_cast<unsigned char*>(wprep), image_current ? 1 : 2, stream);
 }
 
 // ---- persistent round (tiny_ecg_round_kernel)
@@ -1735,10 +1759,12 @@ static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws
   }
   int st = 0;
   // Staged batches: the round's index rows were enqueued into idx_stage one round ahead (while the previous round
-  // computed); the graph's first node moves them into the table every replay reads.  With a PF image that node is
-  // the prep kernel, which also rebuilds the image from the round's starting weights.
+  // computed); the graph's first node moves them into the table every replay reads.  The PF round needs no such
+  // node: its steps read idx_stage itself (the next round's staging is enqueued behind the replay on the same
+  // stream), and its first step runs on the LDS path, whose SGD epilogue rewrites the image for the rest.
+  const int* tab = idx_table;
   if (wprep) {
-    st = launch_prep(params, wprep, idx_stage, const_cast<int*>(idx_table), idx_stage ? (long)steps * B : 0, cap);
+    if (idx_stage) tab = idx_stage;
   } else if (idx_stage && hipMemcpyAsync(const_cast<int*>(idx_table), idx_stage, (size_t)steps * B * sizeof(int),
                                          hipMemcpyDeviceToDevice, cap) != hipSuccess) {
     st = ecg::kHipError;
@@ -1748,8 +1774,8 @@ static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws
     st = round_dispatch(*pa, ws, ws_bytes, prec, cap);
   } else {
     for (int s = 0; s < steps && st == 0; ++s)
-      st = train_step(X, L, ldx, idx_table + (long)s * B, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr,
-                      momentum, wd, nesterov, ctl, gslab, prec, wprep, false, cap);
+      st = train_step(X, L, ldx, tab + (long)s * B, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr,
+                      momentum, wd, nesterov, ctl, gslab, prec, wprep, s == 0 ? 2 : 1, cap);
   }
   e = hipStreamEndCapture(cap, &rg->graph);
   (void)hipStreamDestroy(cap);

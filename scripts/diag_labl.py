@@ -17,14 +17,20 @@ from crossscale_ecg.data.shards import write_shard  # noqa: E402
 from crossscale_ecg.ops.native_io import NativePrefetcher  # noqa: E402
 
 
-def main(shard_dir="/tmp/diag_labl_shards"):
+def make_shards(shard_dir="/tmp/diag_labl_shards"):
     os.makedirs(shard_dir, exist_ok=True)
     rng = np.random.default_rng(1337)
     paths = []
     for i in range(2):
         p = os.path.join(shard_dir, f"ecg_{i:05d}.bin")
-        write_shard(p, rng.normal(0, 1, (32768, 500)).astype(np.float32))
+        if not os.path.exists(p):
+            write_shard(p, rng.normal(0, 1, (32768, 500)).astype(np.float32))
         paths.append(p)
+    return paths
+
+
+def main(shard_dir="/tmp/diag_labl_shards"):
+    paths = make_shards(shard_dir)
     dev = torch.device("cuda:0")
     for B in (128, 256, 512):
         for compute in ("torch", "fused"):
@@ -80,9 +86,8 @@ if __name__ == "__main__" and len(sys.argv) == 1:
 def trace_bench_labl(shard_dir="/tmp/diag_labl_shards"):
     """The real A4 loop (bench.module1.bench_labl) at B=128/256/512, then a torch.profiler trace of B=256:
     top device kernels and the host-side calls that wait."""
-    import glob
     from crossscale_ecg.bench.module1 import bench_labl
-    paths = sorted(glob.glob(os.path.join(shard_dir, "ecg_*.bin")))
+    paths = make_shards(shard_dir)
     dev = torch.device("cuda:0")
     for B in (128, 256, 512, 256):
         r = bench_labl(paths, B, 100, True, dev)

@@ -289,7 +289,8 @@ def test_prefrag_grads_bitwise_equal_lds_path(B):
     assert torch.equal(fa, fb)
 
 
-def test_prefrag_round_graph_bitwise_equal_lds_eager_with_external_updates():
+@pytest.mark.parametrize("graph", [True, False])
+def test_prefrag_round_graph_bitwise_equal_lds_eager_with_external_updates(graph):
     """PF round graphs (image rebuilt by the graph's first node, kept by every step's SGD epilogue) reproduce the
     LDS-built eager steps bit for bit over several rounds - also after the weights are rewritten between rounds
     (what a FedAvg all-reduce / broadcast does)."""
@@ -297,7 +298,7 @@ def test_prefrag_round_graph_bitwise_equal_lds_eager_with_external_updates():
     dev, x, y, model, _ = _setup(B=128, N=1024)
     m2 = TinyECG().to(dev)
     m2.load_state_dict(model.state_dict())
-    a = FusedTinyTrainer(model, x, y, 128, 7, seed=9, use_graph=True, persistent=False, prefrag=True)
+    a = FusedTinyTrainer(model, x, y, 128, 7, seed=9, use_graph=graph, persistent=False, prefrag=True)
     b = FusedTinyTrainer(m2, x, y, 128, 7, seed=9, use_graph=False, persistent=False, prefrag=False)
     assert a.prefrag and not b.prefrag
     g = torch.Generator(device=dev)
