@@ -21,6 +21,7 @@ the fused HIP step fed from the same device batch buffer.
 """
 from __future__ import annotations
 
+import gc
 import os
 import time
 from typing import Dict, List, Optional, Sequence
@@ -255,6 +256,10 @@ def run_locality(shard_dir: str, batch_sizes: List[int], iters: int = 100, num_w
                             pin_memory=pin and dev.type == "cuda", drop_last=True,
                             persistent_workers=num_workers > 0)
             st = measure_step(dl, dev, non_blocking=nb, iters=iters, compute=compute)
+            # retire this loader's persistent worker processes (and its pin-memory thread) before the next
+            # config is timed: left alive they prefetch beside it (the A4 B=256 outlier of round 1)
+            del dl
+            gc.collect()
             row = dict(config=name, batch_size=bs, pin_memory=pin, contiguous=contiguous, non_blocking=nb, **st)
             print(row, flush=True)
             rows.append(row)

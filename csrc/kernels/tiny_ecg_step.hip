@@ -373,42 +373,49 @@ struct TinySample {
           Aw[j] = ecg::to_bf16(h == 0 ? v : 0.f);
         }
       }
-      // B = xcol[t][kk] (K = 32: quarter 0 holds kk 0..7, quarters 1..3 the zero padding).  Quarter-0 lane n reads
-      // the 7 window samples of its time step t = 16*tile + n straight from xs into registers (no write -> read
-      // round trip through the im2col image) and stores the row once for phase 4's conv1 wgrad.  Tiles go two
-      // at a time, every LDS read of the pair issued before the first MFMA.
+      // B = xcol[t][kk] (K = 32: quarter 0 holds kk 0..7, quarters 1..3 read the zero row Lp).  The four lane
+      // quarters build each im2col row together (quarter h writes columns 2h, 2h+1 of row t = 16*tile + n;
+      // column 7 = bias x "t < L"), quarter 0 reads the whole row back as its operand.  Tiles go two at a time
+      // with every LDS access of a kind issued for both before the next kind (one round trip per kind, not per
+      // tile); each wave only reads rows it wrote itself (same-wave LDS order, no barrier).
+      const __bf16* xb = xcol + (h == 0 ? (lane & 15) * 8 : Lp * 8);
+      const int tstride = h == 0 ? 16 * 8 : 0;
       const int ntiles = Lp / 16;
+      const int j0 = 2 * h;
 #pragma unroll 1
       for (int pi = 0; pi < 2 * MAX_PAIRS_PER_WAVE; pi += 2) {
         if (w + pi * WAVES >= ntiles) break;  // wave-uniform
-        float xv[2][K1];
-        int tq[2];
+        int tile[2];
+        float v0[2], v1[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          const int tile = min(w + (pi + u) * WAVES, ntiles - 1);  // clamped: loads never branch
-          tq[u] = 16 * tile + (lane & 15);
-#pragma unroll
-          for (int j = 0; j < K1; ++j) xv[u][j] = xs[tq[u] + j];
+          tile[u] = min(w + (pi + u) * WAVES, ntiles - 1);  // clamped: the second tile may not exist
+          const int t = 16 * tile[u] + (lane & 15);
+          v0[u] = xs[t + j0];
+          v1[u] = j0 + 1 < K1 ? xs[t + j0 + 1] : 1.f;
         }
+        const bool has2 = w + (pi + 1) * WAVES < ntiles;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          const int tile = w + (pi + u) * WAVES;
-          const bool tv = tq[u] < L;
-          bf16x8 Bx;
+          const int t = 16 * tile[u] + (lane & 15);
+          const bool tv = t < L;
+          bf16x2 pr;
+          pr[0] = ecg::to_bf16(tv ? v0[u] : 0.f);
+          pr[1] = ecg::to_bf16(tv ? v1[u] : 0.f);
+          *reinterpret_cast<bf16x2*>(xcol + t * 8 + j0) = pr;  // (a clamped duplicate rewrites the same values)
+        }
+        bf16x8 Bx[2];
 #pragma unroll
-          for (int j = 0; j < K1; ++j) Bx[j] = ecg::to_bf16(tv ? xv[u][j] : 0.f);
-          Bx[7] = ecg::to_bf16(tv ? 1.f : 0.f);  // column 7: bias x "t < L"
-          if (tile < ntiles && h == 0) *reinterpret_cast<bf16x8*>(xcol + tq[u] * 8) = Bx;
-          if (h != 0) {
+        for (int u = 0; u < 2; ++u) Bx[u] = *reinterpret_cast<const bf16x8*>(xb + tile[u] * tstride);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) Bx[j] = ecg::to_bf16(0.f);
-          }
-          const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Aw, Bx, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        for (int u = 0; u < 2; ++u) {
+          if (u == 1 && !has2) break;
+          const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Aw, Bx[u], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
           // acc[i] = conv1(x)[t = 16*tile + (lane&15)][co = 4h + i] + bias (exactly 0 for t >= L)
           bf16x4 o;
 #pragma unroll
           for (int i = 0; i < 4; ++i) o[i] = (AT)fmaxf(acc[i], 0.f);
-          if (tile < ntiles) *reinterpret_cast<bf16x4*>(h1s + (16 * tile + (lane & 15) + 2) * C + 4 * h) = o;
+          *reinterpret_cast<bf16x4*>(h1s + (16 * tile[u] + (lane & 15) + 2) * C + 4 * h) = o;
         }
       }
       return;
