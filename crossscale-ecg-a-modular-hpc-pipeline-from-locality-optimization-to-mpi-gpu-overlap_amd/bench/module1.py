@@ -34,7 +34,7 @@ from torch.utils.data import DataLoader, RandomSampler, SequentialSampler
 from ..utils.timing import warm_until_stable
 
 from ..data.dataset import ShardDataset
-from ..data.shards import ensure_synthetic_shards, list_shards
+from ..data.shards import ensure_synthetic_shards, list_shards, shard_header
 from ..models.tiny_ecg import TinyECG
 from ..utils.csvio import LOCALITY_COLUMNS, LABL_COLUMNS, write_csv
 
@@ -194,6 +194,13 @@ def bench_labl(shard_paths: Sequence[str], batch_size: int, iters: int, normaliz
                 consumed[i % 2].record(main)
 
         warm_until_stable(warm, dev)
+        # The producer hands out each shard's tail as a short batch (n = windows % B); a new batch shape is a new
+        # MIOpen problem whose first call runs the solver search (~0.2 s).  Round 1 timed that once at B=256 (its
+        # 78-batch epoch put the 32-window tail inside the 100 timed steps: compute_ms 2.6-3.1 ms vs 0.75).  Warm
+        # every tail shape here, outside the timing.
+        for n_tail in sorted({shard_header(p)[0] % batch_size for p in shard_paths} - {0}):
+            for _ in range(3):
+                step(bufs[0][:n_tail], y[:n_tail])
         _sync(dev)
         data_ms = h2d_ms = comp_ms = 0.0
         total = 0
