@@ -120,6 +120,13 @@ constexpr int WP_B2_BYTE = (WP_AW1 + C * 8) * 2;  // 6400
 constexpr int WP_BYTES = WP_B2_BYTE + C * 4;     // 6464
 constexpr int kParamsW2End = C * K1 + C + C * C * K2;  // == make_layout(nc).b2 for every nc (1408)
 
+// conv2's bias rides in the MFMA: reduction row r = 80 (tap 5 = K padding, ci 0) of the forward operand holds
+// bf16(b2[co]) and the matching B-operand row is a constant 1 (autocast semantics: the bias of a bf16 conv is bf16
+// too), so the epilogue adds nothing.  Element (r = 80, co) of fragF: fragment s = 2, lane 32 + co, slot j = 0.
+__host__ __device__ constexpr int frag_bias_elem(int co) { return (2 * 64 + 32 + co) * 8; }
+// the K-padding elements (r in [80, 96)) of a fragment set that stay zero: all of them except the bias row
+__host__ __device__ constexpr bool frag_pad_is_bias(int which, int l, int j) { return which == 0 && j == 0 && l < 48; }
+
 // Write flat parameter i's slots of the image (parameters past b2 - the head - have none).
 __device__ __forceinline__ void wprep_put(unsigned char* wp, int i, float v) {
   __bf16* wb = reinterpret_cast<__bf16*>(wp);
@@ -136,6 +143,7 @@ __device__ __forceinline__ void wprep_put(unsigned char* wp, int i, float v) {
     wb[WP_FRAGD + ((rd >> 5) * 64 + 16 * ((rd & 31) >> 3) + ci) * 8 + (rd & 7)] = bv;
   } else if (i < kParamsW2End + C) {
     reinterpret_cast<float*>(wp + WP_B2_BYTE)[i - kParamsW2End] = v;
+    wb[WP_FRAGF + frag_bias_elem(i - kParamsW2End)] = ecg::to_bf16(v);
   }
 }
 
@@ -151,7 +159,7 @@ __global__ __launch_bounds__(256) void tiny_prep_kernel(const float* __restrict_
     __bf16* wb = reinterpret_cast<__bf16*>(wp);
     for (int e = tid; e < 2 * 32 * 8; e += 256) {
       const int which = e >> 8, l = 32 + ((e >> 3) & 31), j = e & 7;
-      wb[(which ? WP_FRAGD : WP_FRAGF) + (2 * 64 + l) * 8 + j] = ecg::to_bf16(0.f);
+      if (!frag_pad_is_bias(which, l, j)) wb[(which ? WP_FRAGD : WP_FRAGF) + (2 * 64 + l) * 8 + j] = ecg::to_bf16(0.f);
     }
     return;
   }
@@ -244,7 +252,6 @@ struct TinySample {
   uint32_t mask1 = 0u;     // relu'(h1) bits of this lane's conv1 outputs (phase 1 -> phase 4)
   // PF: this lane's conv operands in registers, loaded from the global image (phase 0 / end of phase 2)
   bf16x8 pf_aw, pf_wf[3], pf_wd[3];
-  f32x4 pf_b2;
 
   __device__ __forceinline__ void pf_load_fwd(const unsigned char* __restrict__ wp) {
     const __bf16* wb = reinterpret_cast<const __bf16*>(wp);
@@ -256,7 +263,6 @@ struct TinySample {
     }
 #pragma unroll
     for (int s = 0; s < 3; ++s) pf_wf[s] = *reinterpret_cast<const bf16x8*>(wb + WP_FRAGF + (s * 64 + lane) * 8);
-    pf_b2 = *reinterpret_cast<const f32x4*>(wp + WP_B2_BYTE + 16 * h);
   }
   __device__ __forceinline__ void pf_load_dgrad(const unsigned char* __restrict__ wp) {
     const __bf16* wb = reinterpret_cast<const __bf16*>(wp);
@@ -321,6 +327,9 @@ struct TinySample {
   // fp32 (16x16x4): element (r, col) at frag[s = r>>2][lane = 16*(r&3) + col].
   __device__ __forceinline__ void put_param(int i, float v) {
     ps[i] = v;
+    if constexpr (!F32) {
+      if (i >= lay.b2 && i < lay.b2 + C) fragF[frag_bias_elem(i - lay.b2)] = ecg::to_bf16(v);
+    }
     const int e = i - lay.w2;
     if (e >= 0 && e < C * C * K2) {
       const int co = e / (C * K2), ci = (e / K2) % C, k = e % K2;
@@ -343,7 +352,7 @@ struct TinySample {
     if constexpr (!F32) {
       for (int e = PF ? 2 * 32 * 8 : tid; e < 2 * 32 * 8; e += NT) {  // (PF: the image holds its own pads)
         const int which = e >> 8, l = 32 + ((e >> 3) & 31), j = e & 7;
-        (which ? fragD : fragF)[(2 * 64 + l) * 8 + j] = ecg::to_bf16(0.f);
+        if (!frag_pad_is_bias(which, l, j)) (which ? fragD : fragF)[(2 * 64 + l) * 8 + j] = ecg::to_bf16(0.f);
       }
       if (tid < 4) reinterpret_cast<uint32_t*>(xcol + Lp * 8)[tid] = 0u;  // im2col zero row
     }
@@ -458,20 +467,21 @@ struct TinySample {
   __device__ __forceinline__ void conv2() {
     if constexpr (!F32) {
       // out^T[co][t]: A = W2[co][(k,ci)] (the fragments are lane-order symmetric: the same registers serve as
-      // B[(k,ci)][co] or A[co][(k,ci)]), B = h1col[(k,ci)][t] read straight from the [t][ci] rows
+      // B[(k,ci)][co] or A[co][(k,ci)]), B = h1col[(k,ci)][t] read straight from the [t][ci] rows.  The K padding
+      // (tap 5) carries the bias: B rows r = 80..95 are the constant {1, 0, ...} (quarter 2) / 0 (quarter 3).
       bf16x8 Wf[3];
-      float b2v[4], pool[4], cnt[4];
+      float pool[4], cnt[4];
       if constexpr (PF) {
 #pragma unroll
         for (int s = 0; s < 3; ++s) Wf[s] = pf_wf[s];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) b2v[i] = pf_b2[i];
       } else {
 #pragma unroll
         for (int s = 0; s < 3; ++s) Wf[s] = *reinterpret_cast<const bf16x8*>(fragF + (s * 64 + lane) * 8);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) b2v[i] = ps[lay.b2 + 4 * h + i];
       }
+      bf16x8 Bone;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Bone[j] = ecg::to_bf16(0.f);
+      if (h == 2) Bone[0] = ecg::to_bf16(1.f);
 #pragma unroll
       for (int i = 0; i < 4; ++i) pool[i] = cnt[i] = 0.f;
 #pragma unroll
@@ -485,7 +495,10 @@ struct TinySample {
 #pragma unroll
             for (int s = 0; s < 3; ++s) {
               const int r = 32 * pair + 16 * half + (lane & 15) + 2 * s + (h >> 1) - 2;  // h1 time index
-              Bh[half][s] = *reinterpret_cast<const bf16x8*>(h1s + (r + 2) * C + 8 * (h & 1));
+              if (s == 2 && h >= 2)
+                Bh[half][s] = Bone;  // tap 5: the bias row
+              else
+                Bh[half][s] = *reinterpret_cast<const bf16x8*>(h1s + (r + 2) * C + 8 * (h & 1));
             }
           f32x4 accs[2];
 #pragma unroll
@@ -495,24 +508,29 @@ struct TinySample {
             for (int s = 0; s < 3; ++s)
               accs[half] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Wf[s], Bh[half][s], accs[half], 0, 0, 0);
           }
+          // acc[i] = conv2(h1)[t = t0 + (lane&15)][co = 4h + i] + b2[co]; the window mask t < L only matters in
+          // the pair that straddles L (wave-uniform branch: every other pair runs the mask-free epilogue)
+          auto epilogue = [&](auto masked) {
 #pragma unroll
-          for (int half = 0; half < 2; ++half) {
-            const int t0 = 32 * pair + 16 * half;
-            const f32x4 acc = accs[half];
-            // acc[i] = conv2(h1)[t = t0 + (lane&15)][co = 4h + i]
-            const int t = t0 + (lane & 15);
-            const bool tv = t < L;
-            bf16x4 mk;
+            for (int half = 0; half < 2; ++half) {
+              const int t = 32 * pair + 16 * half + (lane & 15);
+              const bool tv = !decltype(masked)::value || t < L;
+              bf16x4 mk;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float v = tv ? fmaxf(acc[i] + b2v[i], 0.f) : 0.f;
-              const bool on = v > 0.f;
-              pool[i] += v;
-              cnt[i] += on ? 1.f : 0.f;
-              mk[i] = ecg::to_bf16(on ? 1.f : 0.f);
+              for (int i = 0; i < 4; ++i) {
+                const float v = tv ? fmaxf(accs[half][i], 0.f) : 0.f;
+                const bool on = v > 0.f;
+                pool[i] += v;
+                cnt[i] += on ? 1.f : 0.f;
+                mk[i] = ecg::to_bf16(on ? 1.f : 0.f);
+              }
+              *reinterpret_cast<bf16x4*>(ms + (t + 4) * C + 4 * h) = mk;
             }
-            *reinterpret_cast<bf16x4*>(ms + (t + 4) * C + 4 * h) = mk;
-          }
+          };
+          if (32 * pair + 32 <= L)
+            epilogue(std::false_type{});
+          else
+            epilogue(std::true_type{});
         }
       }
 #pragma unroll
@@ -751,10 +769,23 @@ struct TinySample {
           for (int half = 0; half < 2; ++half) {
             // acc[i] = dh1[t = t0 + (lane&15)][ci = 4h + i]; times relu'(h1), written over h1 (this wave's rows)
             const int t0 = 32 * pair + 16 * half;
-            bf16x4 dv;
+            // dv = bf16(acc) where h1 > 0, else +0: h1 >= 0 (a ReLU output, possibly -0), so "h1 > 0" is "the 15
+            // magnitude bits are non-zero"; (bits & 0x7fff) + 0x7fff carries into bit 15 exactly then, and an
+            // arithmetic 16-bit shift by 15 widens that bit to the whole half - two packed halves per dword
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 hb = __builtin_bit_cast(u32x2, hv[half]);
+            u32x2 db;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) dv[i] = ecg::to_bf16((float)hv[half][i] > 0.f ? accs[half][i] : 0.f);
-            *reinterpret_cast<bf16x4*>(h1s + (t0 + (lane & 15) + 2) * C + 4 * h) = dv;
+            for (int q2 = 0; q2 < 2; ++q2) {
+              const unsigned nz = (hb[q2] & 0x7fff7fffu) + 0x7fff7fffu;
+              typedef short s16x2 __attribute__((ext_vector_type(2)));
+              const s16x2 m = __builtin_bit_cast(s16x2, nz) >> (short)15;
+              bf16x2 pr;
+              pr[0] = ecg::to_bf16(accs[half][2 * q2]);
+              pr[1] = ecg::to_bf16(accs[half][2 * q2 + 1]);
+              db[q2] = __builtin_bit_cast(unsigned, pr) & __builtin_bit_cast(unsigned, m);
+            }
+            *reinterpret_cast<u32x2*>(h1s + (t0 + (lane & 15) + 2) * C + 4 * h) = db;
           }
           // conv1 wgrad over the pair's 32 steps: A[ci][t] = dh1 (transposing reads of the rows just written by
           // this wave), B[t][kk] = xcol (columns 8..15 come from the zero row); reduction slots as in phase 3
