@@ -194,7 +194,10 @@ class ResNetStepEngine:
             chunks = (R + 63) // 64
             tiles = self.lib.ecg_conv1d_nlc_wgrad_tiles(Cout, K, Cin)
             target = self.lib.ecg_conv1d_nlc_wgrad_target_wgs(Cout, K, Cin)
-            return max(1, min(256, max(1, chunks // 8), max(1, target // tiles)))
+            # A/B knob: capping the splits shrinks the reduce (S x |dW|) but starves the wgrad kernel of workgroups
+            # (B=1024: cap 16 -> 5.86, cap 8 -> 7.66 ms/step vs 4.61 uncapped, profiles/r2/resnet_conv_ab.txt)
+            cap = int(os.environ.get("ECG_WGRAD_MAX_SPLITS", "256"))
+            return max(1, min(cap, 256, max(1, chunks // 8), max(1, target // tiles)))
 
         ws_need = 0
         for (Li, Ci, Lo, Co, s), blk in zip(shapes, blocks):

@@ -372,8 +372,9 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned voff, u
 }
 
 // NWR = waves along M: 2 -> 4 waves (2x2), 4 -> 8 waves (4x2, 2 per SIMD at one workgroup per CU).  256-row
-// tiles need one workgroup per CU (2 x 64 KB of stages at 256x256).
-template <int BM, int BN, int EPI, int NWR>
+// tiles need one workgroup per CU (2 x 64 KB of stages at 256x256).  NST = LDS stages: 2 (one K step in flight
+// while the MFMAs run) or 3 (two in flight; the 24 KB stages of the 128x64 tile still fit two workgroups per CU).
+template <int BM, int BN, int EPI, int NWR, int NST = 2>
 __global__ __launch_bounds__(128 * NWR, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_dma_kernel(FwdArgs a, int MT, int NT) {
   using Cfg = FwdCfg<BM, BN, NWR>;
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NW = Cfg::NW;
@@ -456,16 +457,34 @@ __global__ __launch_bounds__(128 * NWR, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_d
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   };
-  if (nk > 0) {
-    issue(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);  // lands during this step's MFMAs
-      mma(kt & 1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next stage has landed (this wave's pieces) ...
-      __syncthreads();                                  // ... for every wave, and nobody reads stage kt any more
+  if constexpr (NST == 2) {
+    if (nk > 0) {
+      issue(0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);  // lands during this step's MFMAs
+        mma(kt & 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next stage has landed (this wave's pieces) ...
+        __syncthreads();                                  // ... for every wave, and nobody reads stage kt any more
+      }
     }
+  } else {
+    // three stages: K steps kt+1 and kt+2 stream in while step kt's MFMAs run.  Each thread issues AP + BP
+    // DMA loads per stage, so "stage kt landed" = at most one younger stage's loads still outstanding.
+    constexpr int LPS = AP + BP;
+    if (nk > 0) issue(0, 0);
+    if (nk > 1) issue(1, 1);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // stage kt landed for every wave; every wave is past mma(kt - 1)
+      if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);  // into the buffer mma(kt - 1) read
+      mma(kt % 3);
+    }
+    __syncthreads();  // the epilogue reuses the stage buffers
   }
   fwd_epilogue<BM, BN, EPI, NWR>(a, acc, smem, m0, n0, mt, MT, a.Lout, M, 1, 0);
   if (a.tail && a.stats)
@@ -533,24 +552,44 @@ inline int conv_big() {
   return g_conv_big;
 }
 
-template <int BM, int BN, int EPI>
-int launch_fwd_dma(const FwdArgs& a, hipStream_t stream) {
+// ECG_CONV_NST=3 gives the 64-column tiles a three-stage loop (opt-in: ResNet1D-34 B=1024 4.64-4.66 vs 4.61
+// ms/step with two stages, profiles/r2/resnet_conv_ab.txt - the K loops are not bound by DMA latency alone).
+inline int conv_nst64() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ECG_CONV_NST");
+    v = (e && atoi(e) == 3) ? 3 : 2;
+  }
+  return v;
+}
+
+template <int BM, int BN, int EPI, int NST>
+int launch_fwd_dma_st(const FwdArgs& a, hipStream_t stream) {
   constexpr int NWR = BM >= 256 ? 4 : 2;  // 256-row tiles: 8 waves of 64 x BN/2
   using Cfg = FwdCfg<BM, BN, NWR>;
-  constexpr int STAGE_BYTES = 2 * (BM + BN) * 128;
+  constexpr int STAGE_BYTES = NST * (BM + BN) * 128;
   constexpr int SMEM = STAGE_BYTES > Cfg::EP_BYTES ? STAGE_BYTES : Cfg::EP_BYTES;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static bool attr = false;
   if (!attr) {
-    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_dma_kernel<BM, BN, EPI, NWR>,
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_dma_kernel<BM, BN, EPI, NWR, NST>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
     attr = true;
   }
   const int MT = (int)(((long)a.B * a.Lout + BM - 1) / BM), NT = a.Cout / BN;
-  hipLaunchKernelGGL((conv1d_nlc_fwd_dma_kernel<BM, BN, EPI, NWR>), dim3((unsigned)(MT * NT)), dim3(Cfg::NTHR), SMEM,
-                     stream, a, MT, NT);
+  hipLaunchKernelGGL((conv1d_nlc_fwd_dma_kernel<BM, BN, EPI, NWR, NST>), dim3((unsigned)(MT * NT)), dim3(Cfg::NTHR),
+                     SMEM, stream, a, MT, NT);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
+}
+
+// ECG_CONV_NST=3: 64-column tiles take three LDS stages (two workgroups per CU still fit: 2 x 72 KB at 128x64).
+template <int BM, int BN, int EPI>
+int launch_fwd_dma(const FwdArgs& a, hipStream_t stream) {
+  if constexpr (BN == 64 && BM <= 128) {
+    if (conv_nst64() == 3) return launch_fwd_dma_st<BM, BN, EPI, 3>(a, stream);
+  }
+  return launch_fwd_dma_st<BM, BN, EPI, 2>(a, stream);
 }
 
 template <int BM, int BN, int EPI, int NBUF>
