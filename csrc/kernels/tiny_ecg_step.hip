@@ -93,6 +93,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, long 
 __device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, int idx, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, idx * 4, 0, 16);
 }
+__device__ __forceinline__ void st_wt4(__amdgpu_buffer_rsrc_t r, int idx, f32x4 v) {  // idx: float index, 16-B aligned
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v), r, idx * 4, 0, 16);
+}
 __device__ __forceinline__ float ld_wt(__amdgpu_buffer_rsrc_t r, int idx) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, idx * 4, 0, 16));
 }
@@ -892,6 +896,30 @@ struct TinySample {
     }
     return v;
   }
+
+  // Phase 5 with one job per thread and no loop: threads [0, 320) each write 4 consecutive conv2-weight
+  // gradients (one 16-B LDS read per partial, one 16-B write-through store), threads [320, 448) the 128 conv1
+  // weight/bias elements, threads [448, ...) conv2 bias, head and loss (row_value's sums, same order).
+  __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t r, int rowbase) const {
+    constexpr int NQ = C * C * K2 / 4;  // 320 quads of conv2 weights
+    static_assert(NQ + 128 + C <= NT || WAVES < 16, "one job per thread at 16 waves");
+    if (tid < NQ) {
+      const int e0 = 4 * tid;
+      f32x4 v = *reinterpret_cast<const f32x4*>(red + red_m(WAVES) + e0);
+#pragma unroll
+      for (int part = 1; part < msplit(WAVES); ++part) {
+        const f32x4 u = *reinterpret_cast<const f32x4*>(red + red_m(WAVES) + part * 1280 + e0);
+        v[0] += u[0]; v[1] += u[1]; v[2] += u[2]; v[3] += u[3];
+      }
+      const float g = red[RED_G + e0 / (C * K2)];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] *= g;
+      st_wt4(r, rowbase + lay.w2 + e0, v);
+    } else {
+      const int i = tid < NQ + 128 ? tid - NQ : lay.b2 + (tid - NQ - 128);
+      if (i <= lay.P) st_wt(r, rowbase + i, row_value(i));
+    }
+  }
 };
 
 // MODE 0: full training step (grads -> slab row).  MODE 1: forward only (logits -> out [B, nc]).
@@ -976,7 +1004,9 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     ECG_STAMP(5)
     // phase 5: combine partials, scale by g, write this sample's gradient row.  The single-launch reduction
     // below reads it inside this launch (write-through stores); otherwise the kernel boundary publishes it.
-    if (opt.ctl != nullptr || opt.slab_wt) {
+    if (WAVES == 16 && opt.ctl == nullptr && opt.slab_wt && S.lay.P - S.lay.b2 + 1 <= S.NT - 448) {
+      S.row_store(slab_r, rowbase);
+    } else if (opt.ctl != nullptr || opt.slab_wt) {
       for (int i = tid; i <= S.lay.P; i += S.NT) st_wt(slab_r, rowbase + i, S.row_value(i));
     } else {
       for (int i = tid; i <= S.lay.P; i += S.NT) out[rowbase + i] = S.row_value(i);
@@ -1462,8 +1492,11 @@ template <bool F32, bool PF>
 int dispatch_cfg(int mode, int waves, const float* X, int L, long ldx, const int* idx, const int* Y,
                  const float* params, int nc, float* out, int out_stride, int B, float inv_B, const FusedOpt& opt,
                  const unsigned char* wprep, hipStream_t stream) {
-  if (mode == 2)  // diagnostic (one wave count is enough)
-    return launch_step<8, 2, F32, PF>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, wprep, stream);
+  if (mode == 2)  // diagnostic: the production wave count
+    return waves == 8
+               ? launch_step<8, 2, F32, PF>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, wprep, stream)
+               : launch_step<16, 2, F32, PF>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, wprep,
+                                             stream);
   if (mode == 0)
     return waves == 8
                ? launch_step<8, 0, F32, PF>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, wprep, stream)
