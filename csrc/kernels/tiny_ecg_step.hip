@@ -76,6 +76,7 @@ struct FusedOpt {
   int nesterov;
   int G;             // number of workgroups (= batch)
   int slab_wt;       // two-launch path: store the gradient rows write-through (ECG_TINY_SLAB_WT, default on)
+  const int* idx_next;  // next step's batch rows: touch this sample's next window on the way out (L2/MALL warm-up)
 };
 // conv2 wgrad work split: 5 taps x msplit(WAVES) pair ranges, one (tap, range) per wave 1.. (wave 0 runs the head)
 __host__ __device__ constexpr int msplit(int waves) { return (waves - 1) / 5 < 1 ? 1 : (waves - 1) / 5; }
@@ -1016,6 +1017,13 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     if (MODE == 2) __syncthreads();  // the second pass reuses the LDS
   }
   if (stamps && tid == 0) stamps[(long)b * 16 + 14] = __builtin_amdgcn_s_memrealtime();
+  if (MODE == 0 && opt.idx_next != nullptr) {
+    // Fire-and-forget loads of the next step's window (one dword per 64-byte line) so the next launch's phase 0
+    // finds it in cache: nothing waits for them (the values are unused), the workgroup just retires.
+    const long row = opt.idx_next[b];
+    const int i = tid * 16;
+    if (i < L) (void)*reinterpret_cast<const volatile float*>(X + row * ldx + i);
+  }
   if (MODE == 0 && opt.ctl != nullptr) {
     // ---------------- phase 6: two-level deterministic cross-sample reduction + SGD --------------
     const Layout& lay = S.lay;
@@ -1492,11 +1500,9 @@ template <bool F32, bool PF>
 int dispatch_cfg(int mode, int waves, const float* X, int L, long ldx, const int* idx, const int* Y,
                  const float* params, int nc, float* out, int out_stride, int B, float inv_B, const FusedOpt& opt,
                  const unsigned char* wprep, hipStream_t stream) {
-  if (mode == 2)  // diagnostic: the production wave count
-    return waves == 8
-               ? launch_step<8, 2, F32, PF>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, wprep, stream)
-               : launch_step<16, 2, F32, PF>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, wprep,
-                                             stream);
+  if (mode == 2)  // diagnostic (8 waves: the 16-wave two-pass variant spills registers; the production kernel's own
+                 // phase stamps come from MODE 0 with ecg_tiny_set_stamps, scripts/diag_step_phases.py)
+    return launch_step<8, 2, F32, PF>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, wprep, stream);
   if (mode == 0)
     return waves == 8
                ? launch_step<8, 0, F32, PF>(X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt, wprep, stream)
@@ -1755,7 +1761,7 @@ ECG_API int ecg_slab_reduce_sgd(const float* slab, int G, int stride, int P, flo
 static int train_step(const float* X, int L, long ldx, const int* idx, const int* Y, float* params, float* mom,
                       int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr, float momentum, float wd,
                       int nesterov, int* ctl, float* gslab, int prec, unsigned char* wprep, int image,
-                      hipStream_t stream) {
+                      hipStream_t stream, const int* idx_next = nullptr) {
   if (ctl) {
     if (wprep) return ecg::kBadArg;
     FusedOpt o{ctl, gslab, params, mom, loss_acc, lr, momentum, wd, nesterov, B};
@@ -1765,7 +1771,15 @@ static int train_step(const float* X, int L, long ldx, const int* idx, const int
   int st = ecg::kOk;
   if (wprep && image == 0) st = launch_prep(params, wprep, nullptr, nullptr, 0, stream);
   if (st) return st;
-  st = step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, no_fuse(),
+  FusedOpt o = no_fuse();
+  // ECG_TINY_PREFETCH=1: warm-up loads of the next step's windows in the step kernel's tail (opt-in: 11.11 vs
+  // 11.08 us/step without, A/B x2 - the windows already sit in the Infinity Cache; profiles/r2/bench_prefetch.txt)
+  static const bool warm_next = [] {
+    const char* e = getenv("ECG_TINY_PREFETCH");
+    return e && atoi(e) == 1;
+  }();
+  o.idx_next = warm_next ? idx_next : nullptr;
+  st = step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, o,
                      image == 2 ? nullptr : wprep, stream);
   if (st) return st;
   return reduce_dispatch(slab, B, slab_stride, make_layout(nc).P, params, mom, nullptr, loss_acc, lr, momentum, wd,
@@ -1846,7 +1860,8 @@ static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws
   } else {
     for (int s = 0; s < steps && st == 0; ++s)
       st = train_step(X, L, ldx, tab + (long)s * B, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr,
-                      momentum, wd, nesterov, ctl, gslab, prec, wprep, s == 0 ? 2 : 1, cap);
+                      momentum, wd, nesterov, ctl, gslab, prec, wprep, s == 0 ? 2 : 1, cap,
+                      s + 1 < steps ? tab + (long)(s + 1) * B : nullptr);
   }
   e = hipStreamEndCapture(cap, &rg->graph);
   (void)hipStreamDestroy(cap);

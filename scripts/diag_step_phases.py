@@ -77,7 +77,19 @@ def main():
         print(f"{name} round: graph {t:.2f} us/step, eager {te:.2f} us/step")
         tr.close()
 
-    # cold vs warm passes of the per-step kernel (MODE 2), operands built in LDS vs prepared fragments (PF)
+    # the production kernel (MODE 0, 16 waves at L=500) stamped in a single, cold pass
+    for label, pf in (("LDS-built operands", False), ("prepared fragments (PF)", True)):
+        st = torch.zeros(B * 16, dtype=torch.int64, device=dev)
+        wp = torch.zeros(lib.ecg_tiny_wprep_bytes(), dtype=torch.uint8, device=dev)
+        for _ in range(5):
+            st.zero_()
+            lib.ecg_tiny_set_stamps(st.data_ptr())
+            tiny_step_grads(flat, x, y32, idx, B, 2, slab, prefrag=pf, wprep=wp if pf else None)
+            torch.cuda.synchronize()
+            lib.ecg_tiny_set_stamps(None)
+        phase_table(st.view(B, 16).cpu(), 0, NAMES, f"[{label}] PRODUCTION per-step kernel (16 waves), cold:")
+
+    # cold vs warm passes of the per-step kernel (MODE 2, 8 waves), operands built in LDS vs prepared fragments
     wprep = torch.empty(lib.ecg_tiny_wprep_bytes(), dtype=torch.uint8, device=dev)
     for label, wp in (("LDS-built operands", None), ("prepared fragments (PF)", wprep.data_ptr())):
         st = torch.zeros(B * 16, dtype=torch.int64, device=dev)

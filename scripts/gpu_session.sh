@@ -42,6 +42,10 @@ for s in $STEPS; do
     diag_phases) run diag_phases 600 python scripts/diag_step_phases.py ;;
     diag_pf) run diag_pf 300 python scripts/diag_prefrag.py ;;
     diag_labl) run diag_labl 300 python scripts/diag_labl.py ;;
+    bench_pref) run bench_pref1 300 python bench.py --steps 500 --warmup 100 --no-extras
+                run bench_pref0 300 env ECG_TINY_PREFETCH=0 python bench.py --steps 500 --warmup 100 --no-extras
+                run bench_pref1b 300 python bench.py --steps 500 --warmup 100 --no-extras
+                run bench_pref0b 300 env ECG_TINY_PREFETCH=0 python bench.py --steps 500 --warmup 100 --no-extras ;;
     bench_wt) run bench_wt0 300 python bench.py --steps 500 --warmup 100 --no-extras
               run bench_wt1 300 env ECG_TINY_SLAB_WT=1 python bench.py --steps 500 --warmup 100 --no-extras
               run bench_wt0b 300 python bench.py --steps 500 --warmup 100 --no-extras
