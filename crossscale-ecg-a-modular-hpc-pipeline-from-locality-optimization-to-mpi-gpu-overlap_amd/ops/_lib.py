@@ -69,6 +69,8 @@ def _bind_kernels(lib: C.CDLL) -> None:
     _sig(lib, "ecg_tiny_wprep_bytes", [])
     _sig(lib, "ecg_tiny_train_step_pf", [vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, vp, f32, f32, f32, i32,
                                          vp, i32, vp])
+    _sig(lib, "ecg_tiny_train_steps_pf", [vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, i32, vp, f32, f32, f32,
+                                          i32, vp, i32, vp])
     _sig(lib, "ecg_tiny_prep", [vp, vp, vp])
     _sig(lib, "ecg_slab_reduce_sgd", [vp, i32, i32, i32, vp, vp, vp, vp, f32, f32, f32, i32, i32, vp, vp])
     _sig(lib, "ecg_tiny_train_step", [vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, vp, f32, f32, f32, i32,

@@ -146,7 +146,7 @@ class FusedTinyTrainer:
 
     def __init__(self, model: TinyECG, x_gpu: torch.Tensor, y_gpu: torch.Tensor, batch_size: int,
                  steps_per_round: int, lr: float = 1e-2, momentum: float = 0.9, weight_decay: float = 0.0,
-                 nesterov: bool = False, seed: Optional[int] = None, use_graph: bool = True,
+                 nesterov: bool = False, seed: Optional[int] = None, use_graph: Optional[bool] = None,
                  single_launch: bool = False, precision: str = "bf16", persistent: Optional[bool] = None,
                  prefrag: Optional[bool] = None):
         self.device = x_gpu.device
@@ -174,7 +174,8 @@ class FusedTinyTrainer:
         self.idx_stage = torch.zeros((self.S, self.B), dtype=torch.int32, device=self.device)
         self._staged: Optional[int] = None  # rows staged for the next round (None: nothing staged)
         self.sampler = DeviceIndexSampler(self.x.shape[0], self.B, self.device, seed=seed)
-        self.use_graph = use_graph
+        # a round = one hipGraph replay, or (ECG_TINY_GRAPH=0) the same kernels enqueued from a C++ loop
+        self.use_graph = (os.environ.get("ECG_TINY_GRAPH", "1") != "0") if use_graph is None else bool(use_graph)
         self._graphs = {}  # n_steps -> native hipGraphExec handle
         self.steps_done = 0
         lib = _lib.kernels()
@@ -356,6 +357,13 @@ class FusedTinyTrainer:
                        "ecg_round_graph_launch")
             if self.prefrag:
                 self._swap_tables()
+        elif self.prefrag:  # the graph's kernels enqueued from one C++ loop, reading the staged table in place
+            _lib.check(_lib.kernels().ecg_tiny_train_steps_pf(
+                self.x.data_ptr(), self.x.shape[1], self.x.stride(0), self.idx_stage.data_ptr(), self.y32.data_ptr(),
+                self.params.data_ptr(), self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B, n,
+                self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd, int(self.nesterov),
+                self.wprep.data_ptr(), 0, _lib.stream_ptr(self.device)), "ecg_tiny_train_steps_pf")
+            self._swap_tables()
         else:
             self.idx_table[:n].copy_(self.idx_stage[:n])
             if self.persistent:

@@ -1809,6 +1809,22 @@ ECG_API int ecg_tiny_train_step_pf(const float* X, int L, long ldx, const int* i
                     nullptr, nullptr, 0, static_cast<unsigned char*>(wprep), image_current ? 1 : 2, stream);
 }
 
+// ``steps`` two-launch PF steps (batch s reads idx_table + s*B) enqueued directly from C++: the same kernels and
+// order as a round graph replay (first step on the LDS path unless ``image_current``), without the graph launch.
+ECG_API int ecg_tiny_train_steps_pf(const float* X, int L, long ldx, const int* idx_table, const int* Y,
+                                    float* params, float* mom, int nc, float* slab, int slab_stride, int B, int steps,
+                                    float* loss_acc, float lr, float momentum, float wd, int nesterov, void* wprep,
+                                    int image_current, hipStream_t stream) {
+  if (!wprep || steps < 1) return ecg::kBadArg;
+  int st = ecg::kOk;
+  for (int s = 0; s < steps && st == 0; ++s)
+    st = train_step(X, L, ldx, idx_table + (long)s * B, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr,
+                    momentum, wd, nesterov, nullptr, nullptr, 0, static_cast<unsigned char*>(wprep),
+                    (s > 0 || image_current) ? 1 : 2, stream,
+                    s + 1 < steps ? idx_table + (long)(s + 1) * B : nullptr);
+  return st;
+}
+
 // ---- persistent round (tiny_ecg_round_kernel)
 // Bytes of the granule workspace (tags zeroed by the launcher before every launch).
 ECG_API long ecg_tiny_round_ws_bytes(int nc, int B) { return round_ws_bytes(nc, B); }

@@ -59,6 +59,50 @@ def main():
     for k in (20, 50, 100, 500):
         med, mn = timed(plan(k))
         print(f"plan K={k:4d}: median {med:8.1f} us  min {mn:8.1f} us  -> {med / k:6.2f} us/step (min {mn / k:6.2f})")
+    # replay only, batches staged outside the timing (as bench.py's first timed round): host wall, time for the
+    # launch call to return, and the GPU span between events recorded just before / after the replay
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for n in (1, 2, 20, 50):
+        wall, call, span = [], [], []
+        for _ in range(9):
+            tr.prepare_round(n, reset_loss=False)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            e0.record()
+            t1 = time.perf_counter()
+            tr.launch_round(n)
+            t2 = time.perf_counter()
+            e1.record()
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            wall.append((t3 - t0) * 1e6)
+            call.append((t2 - t1) * 1e6)
+            span.append(e0.elapsed_time(e1) * 1e3)
+        med = statistics.median
+        print(f"replay n={n:3d}: wall {med(wall):8.1f} us  launch call {med(call):6.1f} us  "
+              f"gpu span {med(span):8.1f} us  -> wall {med(wall) / n:6.2f} / span {med(span) / n:6.2f} us/step")
+    # the same kernels enqueued one by one from a C++ loop (no graph)
+    from crossscale_ecg.ops import _lib
+    lib = _lib.kernels()
+    stream = _lib.stream_ptr(dev)
+    for n in (1, 2, 20, 50):
+        wall, call = [], []
+        for _ in range(9):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            st = lib.ecg_tiny_train_steps_pf(tr.x.data_ptr(), tr.x.shape[1], tr.x.stride(0), tr.idx_table.data_ptr(),
+                                             tr.y32.data_ptr(), tr.params.data_ptr(), tr.mom.data_ptr(), tr.nc,
+                                             tr.slab.data_ptr(), tr.stride, tr.B, n, tr.loss_acc.data_ptr(), tr.lr,
+                                             tr.momentum, tr.wd, int(tr.nesterov), tr.wprep.data_ptr(), 0, stream)
+            t1 = time.perf_counter()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            _lib.check(st, "ecg_tiny_train_steps_pf")
+            wall.append((t2 - t0) * 1e6)
+            call.append((t1 - t0) * 1e6)
+        med = statistics.median
+        print(f"eager C loop n={n:3d}: wall {med(wall):8.1f} us  enqueue {med(call):6.1f} us  "
+              f"-> {med(wall) / n:6.2f} us/step")
     tr.close()
 
 

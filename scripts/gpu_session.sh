@@ -53,6 +53,12 @@ for s in $STEPS; do
     bench_ab) run bench_pf 300 python bench.py --steps 500 --warmup 100 --no-extras
               run bench_lds 300 env ECG_TINY_PREFRAG=0 python bench.py --steps 500 --warmup 100 --no-extras
               run bench_pf20 300 python bench.py --steps 20 --warmup 5 --no-extras ;;
+    bench_graph) for r in a b; do
+                   run bench_g1_20$r 300 python bench.py --steps 20 --warmup 5 --no-extras
+                   run bench_g0_20$r 300 env ECG_TINY_GRAPH=0 python bench.py --steps 20 --warmup 5 --no-extras
+                   run bench_g1_500$r 300 python bench.py --steps 500 --warmup 100 --no-extras
+                   run bench_g0_500$r 300 env ECG_TINY_GRAPH=0 python bench.py --steps 500 --warmup 100 --no-extras
+                 done ;;
     hbm) run hbm 600 python -m crossscale_ecg.bench.hbm --gb 16 --dir /tmp/ecg_hbm_shards --cleanup ;;
     module2) mkdir -p gpurun_out/results
              run module2 600 python benchmark_part_2.py --results-dir gpurun_out/results --batch-scaling ;;
