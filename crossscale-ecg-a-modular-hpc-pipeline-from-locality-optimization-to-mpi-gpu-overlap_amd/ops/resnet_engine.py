@@ -170,6 +170,11 @@ class ResNetStepEngine:
         # backward scratch (reused block to block: the plan is stream-ordered)
         gA, gB = self._t(maxel), self._t(maxel)  # ping-pong: grad wrt block output / block input
         dz2, ga1, dz1, dzd, tmp = (self._t(maxel) for _ in range(5))
+        # weight gradients on a side stream (csrc/kernels/resnet_nlc.hip, OP_LANE): the BN-backward outputs they
+        # read (dz2, dz1, dzd) get one buffer per block instead of block-to-block reuse, and their split-K
+        # partials a workspace of their own.  ECG_RESNET_SIDE=0: one stream, as captured before.
+        side = os.environ.get("ECG_RESNET_SIDE", "1") != "0"
+        self.side_lane = side
         dz0 = self._t(B, Lz, 64)
         # BN states
         bn0 = _BN(m.bn1, dev)
@@ -210,6 +215,7 @@ class ResNetStepEngine:
         Gb = max(1, min(64, B // 64))
         ws_need = max(ws_need, stem_blocks * 64 * Ks, Gb * (ncls * self.Cf + ncls + 1))
         ws = self._t(ws_need, dtype=torch.float32)
+        ws_w = self._t(ws_need, dtype=torch.float32) if side else ws
 
         # ---- bf16 weight arena (fwd + flipped dgrad layouts) and prep table
         convs = []
@@ -234,10 +240,10 @@ class ResNetStepEngine:
         ops: List[List[int]] = []
         self._segments: List[Tuple[int, int, int, int]] = []  # (op_begin, op_end, grad_lo, grad_hi) elements
 
-        def op(kind, *args):
+        def op(kind, *args, lane=0):
             w = [OP[kind]] + [int(a) for a in args]
-            assert len(w) <= OP_WORDS, kind
-            ops.append(w + [0] * (OP_WORDS - len(w)))
+            assert len(w) < OP_WORDS, kind  # the last word is the lane (0 main, 1 side, 2 main after a join)
+            ops.append(w + [0] * (OP_WORDS - 1 - len(w)) + [lane if side else 0])
 
         P = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
         eps, bnm = m.bn1.eps, (m.bn1.momentum if m.bn1.momentum is not None else 0.1)
@@ -299,8 +305,8 @@ class ResNetStepEngine:
 
         def wgrad(dy, x, Lin, Cin, Lout, Cout, K, s, p, weight):
             S = wsplits(B * Lout, Cout, K, Cin)
-            op("CONV_WGRAD", P(dy), P(x), P(ws), S, B, Lin, Cin, Lout, Cout, K, s, p)
-            op("REDUCE_WGRAD", P(ws), S, Cout, K, Cin, self._gptr(weight))
+            op("CONV_WGRAD", P(dy), P(x), P(ws_w), S, B, Lin, Cin, Lout, Cout, K, s, p, lane=1)
+            op("REDUCE_WGRAD", P(ws_w), S, Cout, K, Cin, self._gptr(weight), lane=1)
 
         # =============================== forward
         if self.source is not None:
@@ -370,6 +376,8 @@ class ResNetStepEngine:
             (Li, Ci, Lo, Co, s), blk, a, (b1, b2, bd) = shapes[bi], blocks[bi], acts[bi], bns[bi]
             R = B * Lo
             blk_begin = len(ops)
+            if side and bi < len(blocks) - 1:  # per-block BN-backward outputs (read by the side-stream wgrads)
+                dz2, dz1, dzd = self._t(maxel), self._t(maxel), (self._t(maxel) if bd is not None else dzd)
             dzm, din = gcur, nxt  # dzm: ReLU-masked grad wrt this block's output
             if bn2_src is None:  # last block: gradient from the head
                 ch = chunk_for(Co)
@@ -434,7 +442,7 @@ class ResNetStepEngine:
         self._fb_end = len(ops)
         # =============================== optimizer
         op("SGD", P(self.flat), P(self.grad), P(self.mom), self.space.param_numel, _f(self.lr), _f(self.momentum),
-           _f(self.wd), int(self.nesterov))
+           _f(self.wd), int(self.nesterov), lane=2)
         if tail_blobs:
             blob = torch.frombuffer(bytearray(b"".join(tail_blobs)), dtype=torch.uint8)
             tails_dev[:blob.numel()].copy_(blob)
@@ -472,7 +480,10 @@ class ResNetStepEngine:
         return h
 
     def _exec(self, key: str, begin: int, end: int):
-        if self.use_graph:
+        # With the side lane the plan runs eagerly: measured on MI355X (ResNet1D-34 B=1024, scripts/
+        # diag_resnet_side.py) the fork-join plan takes 3.94 ms/step enqueued directly but 8.05 as a replayed
+        # hipGraph (one stream: 4.56 either way).  ECG_RESNET_SIDE_GRAPH=1 replays the fork-join graph anyway.
+        if self.use_graph and (not self.side_lane or os.environ.get("ECG_RESNET_SIDE_GRAPH") == "1"):
             st = self.lib.ecg_plan_graph_launch(self._graph(key, begin, end), _lib.stream_ptr(self.dev))
             _lib.check(st, "ecg_plan_graph_launch")
         else:

@@ -20,6 +20,7 @@
 
 #include "../include/bn_tail.h"
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 
 namespace {
@@ -496,9 +497,21 @@ inline int conv_big();
 
 // Tile choice: with the LDS-DMA loop (undilated input) 256x256 (8 waves of 64x128) when that gives >= 2 tiles
 // per CU (one workgroup per CU; half the L2->LDS bytes per MAC of 128x128: 1.04 vs 0.87 PF/s on the
-// ResNet layer4 shape, profiles/r1_resnet/cmb_p3_big*.log), [256x128 opt-in: measured slower], else 128x128 when that still gives >= 2 workgroups per CU (256 CUs), else 128x64,
+// ResNet layer4 shape, profiles/r1_resnet/cmb_p3_big*.log), [256x128 opt-in: measured slower], else 128x128 when that still gives >= 1 workgroup per CU (256 CUs), else 128x64,
 // else 64x64.
 inline void pick_fwd_tile(long M, int Cout, int in_dil, int* bm, int* bn) {
+  // ECG_CONV_TILE=<bm>x<bn> forces one tile family wherever it applies (A/B experiments; read once)
+  static int force_bm = -1, force_bn = 0;
+  if (force_bm < 0) {
+    const char* e = getenv("ECG_CONV_TILE");
+    force_bm = 0;
+    if (e && sscanf(e, "%dx%d", &force_bm, &force_bn) != 2) force_bm = 0;
+  }
+  if (force_bm > 0 && Cout % force_bn == 0 && (force_bm <= 128 || (in_dil == 1 && conv_dma()))) {
+    *bm = force_bm;
+    *bn = force_bn;
+    return;
+  }
   const long mt128 = (M + 127) / 128, mt256 = (M + 255) / 256;
   const int big = (in_dil == 1 && conv_dma()) ? conv_big() : 0;
   if (big >= 1 && Cout % 256 == 0 && mt256 * (Cout / 256) >= 512) {
@@ -507,8 +520,8 @@ inline void pick_fwd_tile(long M, int Cout, int in_dil, int* bm, int* bn) {
   } else if (big >= 2 && Cout % 128 == 0 && mt256 * (Cout / 128) >= 512) {
     *bm = 256;
     *bn = 128;
-  } else if (Cout % 128 == 0 && mt128 * (Cout / 128) >= 512) {
-    *bm = 128;
+  } else if (Cout % 128 == 0 && mt128 * (Cout / 128) >= 256) {  // >= one tile per CU: 15.1 vs 17.7 us for 128x64
+    *bm = 128;                                                      // at M=64512 C=128 (profiles/r2/conv_tiles.txt)
     *bn = 128;
   } else if (mt128 * (Cout / 64) >= 512) {
     *bm = 128;

@@ -1086,18 +1086,83 @@ ECG_API int ecg_plan_stem_rows() { return STEM_ROWS; }
 // Number of blocks the weight-prep op needs for a table; fills WEntry.block0 in a host-side copy.
 ECG_API int ecg_plan_wentry_bytes() { return (int)sizeof(WEntry); }
 
-// Run ``nops`` encoded ops back to back on ``stream``.  Returns the first failing op's status (ops before it
-// have been enqueued).  ``first_bad`` (optional) receives its index.
+namespace {
+// Lanes (word OP_LANE of an op): the weight-gradient ops (CONV_WGRAD + REDUCE_WGRAD) are off the backward's
+// critical path - only the optimizer reads what they write - so the plan can put them on a side stream: the
+// MFMA-bound weight-gradient kernels then fill the data-gradient chain's idle time (kernel boundaries, the
+// BatchNorm finalize tails, the memory-bound BN_BWD_APPLY passes).  Ordering: before a side op, the side
+// stream waits for everything enqueued on the main stream so far (it reads the gradient the main chain just
+// produced); LANE_JOIN ops (the optimizer) and the end of every run wait for the side stream.  Inside a
+// capture the same event record / wait pairs become graph edges, so a graph is the fork-join DAG.
+constexpr int OP_LANE = OP_WORDS - 1;
+enum : int { LANE_MAIN = 0, LANE_SIDE = 1, LANE_JOIN = 2 };
+
+struct SideLane {
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+int side_lane(SideLane** out) {
+  static SideLane lanes[64];
+  int dev = 0;
+  ECG_HIP_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return ecg::kBadArg;
+  SideLane& l = lanes[dev];
+  if (!l.side) {
+    int lo = 0, hi = 0;
+    ECG_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    ECG_HIP_CHECK(hipStreamCreateWithPriority(&l.side, hipStreamNonBlocking, lo));  // lo: the least urgent
+    ECG_HIP_CHECK(hipEventCreateWithFlags(&l.fork, hipEventDisableTiming));
+    ECG_HIP_CHECK(hipEventCreateWithFlags(&l.join, hipEventDisableTiming));
+  }
+  *out = &l;
+  return ecg::kOk;
+}
+}  // namespace
+
+// Run ``nops`` encoded ops back to back on ``stream`` (side-lane ops on the device's side stream, joined back
+// before LANE_JOIN ops and before returning).  Returns the first failing op's status (ops before it have been
+// enqueued).  ``first_bad`` (optional) receives its index.
 ECG_API int ecg_plan_run(const int64_t* ops, int nops, int* first_bad, hipStream_t stream) {
   if (!ops || nops < 0) return ecg::kBadArg;
-  for (int i = 0; i < nops; ++i) {
-    const int st = run_op(ops + (long)i * OP_WORDS, stream);
-    if (st) {
-      if (first_bad) *first_bad = i;
-      return st;
+  SideLane* lane = nullptr;
+  bool side_busy = false, main_ahead = true;  // side has unjoined work / main has work the side has not waited for
+  int st = ecg::kOk;
+  auto join = [&]() -> int {
+    if (!side_busy) return ecg::kOk;
+    ECG_HIP_CHECK(hipEventRecord(lane->join, lane->side));
+    ECG_HIP_CHECK(hipStreamWaitEvent(stream, lane->join, 0));
+    side_busy = false;
+    return ecg::kOk;
+  };
+  int bad = -1;
+  for (int i = 0; i < nops && bad < 0; ++i) {
+    const int64_t* o = ops + (long)i * OP_WORDS;
+    const int64_t ln = o[OP_LANE];
+    if (ln == LANE_SIDE) {
+      if (!lane) st = side_lane(&lane);
+      if (st == 0 && main_ahead) {
+        ECG_HIP_CHECK(hipEventRecord(lane->fork, stream));
+        ECG_HIP_CHECK(hipStreamWaitEvent(lane->side, lane->fork, 0));
+        main_ahead = false;
+      }
+      if (st == 0) {
+        st = run_op(o, lane->side);
+        side_busy = true;
+      }
+    } else {
+      if (ln == LANE_JOIN) st = join();
+      if (st == 0) st = run_op(o, stream);
+      main_ahead = true;
     }
+    if (st) bad = i;
   }
-  return ecg::kOk;
+  if (st) {
+    if (first_bad) *first_bad = bad;
+    (void)join();  // leave no side work unjoined (a capture must end with every stream joined)
+    return st;
+  }
+  return join();
 }
 
 // Capture the plan into one hipGraph (all pointers baked in; callers keep every buffer alive).

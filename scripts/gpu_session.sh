@@ -84,6 +84,13 @@ for s in $STEPS; do
       run pmc1 120 rocprofv3 --pmc $P1 --kernel-trace --output-format csv -d "$OUT/pmc1" -o tiny -- python3 scripts/pmc_tiny_step.py
       run pmc2 120 rocprofv3 --pmc $P2 --kernel-trace --output-format csv -d "$OUT/pmc2" -o tiny -- python3 scripts/pmc_tiny_step.py
       ;;
+    conv_ab) run conv_picker 120 python scripts/conv_micro.py
+             for t in 64x64 128x64 128x128 256x256; do run conv_$t 120 env ECG_CONV_TILE=$t python scripts/conv_micro.py; done ;;
+    conv_pmc)
+      export TMPDIR=/tmp
+      P3="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY"
+      run conv_pmc 120 rocprofv3 --pmc $P3 --kernel-trace --output-format csv -d "$OUT/conv_pmc" -o conv -- python3 scripts/conv_micro.py
+      ;;
     prof)
       export TMPDIR=/tmp
       run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \

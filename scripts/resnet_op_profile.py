@@ -38,31 +38,44 @@ def main(depth=34, B=1024, reps=20):
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / reps
-        flop, desc = 0.0, ""
+        flop, desc, nbytes = 0.0, "", 0.0
         if kind == "CONV_FWD":
             Bq, Lin, Cin, Lout, Cout, K, s, p, dil = o[8:17]
             M = Bq * Lout
             flop = 2.0 * M * Cout * K * Cin / (dil if dil > 1 else 1)
+            nbytes = 2.0 * (Bq * Lin * Cin + M * Cout + Cout * K * Cin)
             desc = f"{'dgrad' if o[19] or dil > 1 or o[6] else 'fwd'} M={M} N={Cout} K={K}x{Cin} s={s} dil={dil}"
         elif kind == "CONV_WGRAD":
             S, Bq, Lin, Cin, Lout, Cout, K = o[4:11]
             flop = 2.0 * Bq * Lout * Cout * K * Cin
+            nbytes = 2.0 * (Bq * Lin * Cin + Bq * Lout * Cout) + 4.0 * S * Cout * K * Cin
             desc = f"wgrad R={Bq * Lout} Cout={Cout} K={K}x{Cin} splits={S}"
         elif kind == "REDUCE_WGRAD":
             desc = f"S={o[2]} |dW|={o[3] * o[4] * o[5]}"
-        rows.append((us, kind, desc, flop))
+        rows.append((us, kind, desc, flop, nbytes))
     tot = sum(r[0] for r in rows)
     print(f"ResNet1D-{depth} B={B}: {len(rows)} ops, sum of per-op times {tot / 1e3:.3f} ms "
           f"(back-to-back single-op launches; the captured step graph overlaps nothing, so this is an upper bound)")
     by = collections.defaultdict(lambda: [0.0, 0])
-    for us, kind, desc, flop in rows:
+    for us, kind, desc, flop, _ in rows:
         by[kind][0] += us
         by[kind][1] += 1
     for k, (us, n) in sorted(by.items(), key=lambda kv: -kv[1][0]):
         print(f"  {k:16s} {n:4d} ops {us / 1e3:7.3f} ms ({100 * us / tot:5.1f} %)")
     print("slowest conv / wgrad ops:")
-    for us, kind, desc, flop in sorted([r for r in rows if r[3] > 0], key=lambda r: -r[0])[:25]:
-        print(f"  {us:8.1f} us  {flop / us / 1e6:7.1f} TFLOP/s  {kind:10s} {desc}")
+    for us, kind, desc, flop, nb in sorted([r for r in rows if r[3] > 0], key=lambda r: -r[0])[:25]:
+        print(f"  {us:8.1f} us  {flop / us / 1e6:7.1f} TFLOP/s  {nb / us / 1e6:6.2f} TB/s  {kind:10s} {desc}")
+    print("all ops grouped by shape (count, total, mean, TFLOP/s, TB/s of the compulsory bytes):")
+    grp = collections.OrderedDict()
+    for us, kind, desc, flop, nb in rows:
+        g = grp.setdefault((kind, desc), [0, 0.0, flop, nb])
+        g[0] += 1
+        g[1] += us
+    for (kind, desc), (n, us, flop, nb) in sorted(grp.items(), key=lambda kv: -kv[1][1]):
+        mean = us / n
+        rate = f"{flop / mean / 1e6:7.1f} TF/s" if flop else " " * 12
+        bw = f"{nb / mean / 1e6:6.2f} TB/s" if nb else " " * 11
+        print(f"  {n:3d} x {mean:7.1f} us = {us:7.1f} us  {rate} {bw}  {kind:14s} {desc}")
 
 
 if __name__ == "__main__":

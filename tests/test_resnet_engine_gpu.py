@@ -74,14 +74,38 @@ def test_engine_large_batch_tiles():
             assert _rel(b, br) < 2e-2, n
 
 
-def test_engine_graph_equals_eager_bitwise():
+@pytest.mark.parametrize("side", ["0", "1"])
+def test_engine_graph_equals_eager_bitwise(side, monkeypatch):
+    # side "1": weight gradients on the side stream, the graph is the captured fork-join DAG (forced: by default
+    # the side-lane plan runs eagerly)
+    monkeypatch.setenv("ECG_RESNET_SIDE", side)
+    monkeypatch.setenv("ECG_RESNET_SIDE_GRAPH", "1")
     m, ref, eng, x, y = _setup(18, B=16, use_graph=False)
+    assert eng.side_lane == (side == "1")
     eng.forward_backward()
     g_eager = eng.grad.clone()
     eng.use_graph = True
     eng.forward_backward()
     torch.cuda.synchronize()
     assert torch.equal(eng.grad, g_eager)
+
+
+def test_side_lane_steps_bitwise_equal_single_stream(monkeypatch):
+    """Weight gradients on the side stream change when kernels run, never what they compute: two SGD steps of
+    ResNet1D-34 give the same parameters, momentum and BN running stats as the one-stream plan, bit for bit."""
+    outs = []
+    for side in ("0", "1"):
+        monkeypatch.setenv("ECG_RESNET_SIDE", side)
+        m, ref, eng, x, y = _setup(34, B=64, seed=3)
+        assert eng.side_lane == (side == "1")
+        eng.step()
+        eng.step()
+        torch.cuda.synchronize()
+        outs.append((eng.flat.clone(), eng.mom.clone(), [b.clone() for b in m.buffers()]))
+        del eng, m, ref
+    (f0, m0, b0), (f1, m1, b1) = outs
+    assert torch.equal(f0, f1) and torch.equal(m0, m1)
+    assert all(torch.equal(a, b) for a, b in zip(b0, b1))
 
 
 def test_engine_sgd_step_and_training_progress():
