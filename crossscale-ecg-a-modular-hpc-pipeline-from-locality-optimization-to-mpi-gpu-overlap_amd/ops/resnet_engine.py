@@ -296,12 +296,12 @@ class ResNetStepEngine:
             return tails_dev.data_ptr() + 304 * (len(tail_blobs) - 1)
 
         def conv(x, Lin, Cin, w_ptr, y, Lout, Cout, K, s, p, dil=1, st=None, add=None, add_mask=None, bnb=None,
-                 tail_ptr=0):
+                 tail_ptr=0, lane=0):
             # bnb = (mask, z, mean, rstd, zd, mean_d, rstd_d): BN-backward statistics fused into the epilogue
             extra = [P(t) if isinstance(t, torch.Tensor) else int(t or 0) for t in (bnb or ())]
             extra += [0] * (7 - len(extra))
             op("CONV_FWD", P(x), w_ptr, 0, P(y), P(st), P(add), P(add_mask), B, Lin, Cin, Lout, Cout, K, s, p, dil, 0,
-               *extra, tail_ptr)
+               *extra, tail_ptr, lane=lane)
 
         def wgrad(dy, x, Lin, Cin, Lout, Cout, K, s, p, weight):
             S = wsplits(B * Lout, Cout, K, Cin)
@@ -320,8 +320,15 @@ class ResNetStepEngine:
         fin_fwd(bn0, T0, B * Lz)
         op("STEM_POOL", P(self.z0), P(bn0.scale), P(bn0.shift), P(self.h0), B, Lz, Lp, 64)
         xin = self.h0
+        # side lane (with fused finalizes): a block's downsample conv runs beside conv1 -> BN_ACT -> conv2, on BN
+        # partials of its own; the BN_ACT that adds it joins the lanes
+        ds_side = side and use_tail
+        stats_d = self._t(2 * max_T * 512, dtype=torch.float32) if ds_side else stats
         for (Li, Ci, Lo, Co, s), blk, a, (b1, b2, bd) in zip(shapes, blocks, acts, bns):
             T = self.lib.ecg_conv1d_nlc_fwd_stat_tiles(B * Lo, Co)  # rows of the epilogue's BN partials
+            if bd is not None and ds_side:
+                conv(xin, Li, Ci, self._wf[id(blk.downsample[0])], a["zd"], Lo, Co, 1, s, 0, st=stats_d,
+                     tail_ptr=tail(T, Co, [fin_fwd_words(bd, B * Lo)]), lane=1)
             conv(xin, Li, Ci, self._wf[id(blk.conv1)], a["z1"], Lo, Co, 3, s, 1, st=stats,
                  tail_ptr=tail(T, Co, [fin_fwd_words(b1, B * Lo)]))
             if not use_tail:
@@ -332,12 +339,13 @@ class ResNetStepEngine:
             if not use_tail:
                 fin_fwd(b2, T, B * Lo)
             if bd is not None:
-                conv(xin, Li, Ci, self._wf[id(blk.downsample[0])], a["zd"], Lo, Co, 1, s, 0, st=stats,
-                     tail_ptr=tail(T, Co, [fin_fwd_words(bd, B * Lo)]))
+                if not ds_side:
+                    conv(xin, Li, Ci, self._wf[id(blk.downsample[0])], a["zd"], Lo, Co, 1, s, 0, st=stats,
+                         tail_ptr=tail(T, Co, [fin_fwd_words(bd, B * Lo)]))
                 if not use_tail:
                     fin_fwd(bd, T, B * Lo)
                 op("BN_ACT", 2, P(a["z2"]), P(b2.scale), P(b2.shift), P(a["zd"]), P(bd.scale), P(bd.shift),
-                   P(a["out"]), B * Lo, Co)
+                   P(a["out"]), B * Lo, Co, lane=2)
             else:
                 op("BN_ACT", 1, P(a["z2"]), P(b2.scale), P(b2.shift), P(xin), 0, 0, P(a["out"]), B * Lo, Co)
             a["in"] = xin
