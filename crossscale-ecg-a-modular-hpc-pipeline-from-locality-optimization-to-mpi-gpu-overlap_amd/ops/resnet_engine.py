@@ -201,7 +201,7 @@ class ResNetStepEngine:
             target = self.lib.ecg_conv1d_nlc_wgrad_target_wgs(Cout, K, Cin)
             # A/B knob: capping the splits shrinks the reduce (S x |dW|) but starves the wgrad kernel of workgroups
             # (B=1024: cap 16 -> 5.86, cap 8 -> 7.66 ms/step vs 4.61 uncapped, profiles/r2/resnet_conv_ab.txt)
-            cap = int(os.environ.get("ECG_WGRAD_MAX_SPLITS", "256"))
+            cap = int(os.environ.get("ECG_WGRAD_MAX_SPLITS", "64"))
             return max(1, min(cap, 256, max(1, chunks // 8), max(1, target // tiles)))
 
         ws_need = 0

@@ -576,9 +576,8 @@ inline int conv_nst64() {
   return v;
 }
 
-template <int BM, int BN, int EPI, int NST>
+template <int BM, int BN, int EPI, int NST, int NWR = (BM >= 256 ? 4 : 2)>  // 256-row tiles: 8 waves of 64 x BN/2
 int launch_fwd_dma_st(const FwdArgs& a, hipStream_t stream) {
-  constexpr int NWR = BM >= 256 ? 4 : 2;  // 256-row tiles: 8 waves of 64 x BN/2
   using Cfg = FwdCfg<BM, BN, NWR>;
   constexpr int STAGE_BYTES = NST * (BM + BN) * 128;
   constexpr int SMEM = STAGE_BYTES > Cfg::EP_BYTES ? STAGE_BYTES : Cfg::EP_BYTES;
@@ -597,10 +596,28 @@ int launch_fwd_dma_st(const FwdArgs& a, hipStream_t stream) {
 }
 
 // ECG_CONV_NST=3: 64-column tiles take three LDS stages (two workgroups per CU still fit: 2 x 72 KB at 128x64).
+// ECG_CONV_V128=1|2|3: the 128x128 tile with three stages (one workgroup per CU) | eight waves of 32x64 | both.
+inline int conv_v128() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ECG_CONV_V128");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
 template <int BM, int BN, int EPI>
 int launch_fwd_dma(const FwdArgs& a, hipStream_t stream) {
   if constexpr (BN == 64 && BM <= 128) {
     if (conv_nst64() == 3) return launch_fwd_dma_st<BM, BN, EPI, 3>(a, stream);
+  }
+  if constexpr (BN == 128 && BM == 128) {
+    switch (conv_v128()) {
+      case 1: return launch_fwd_dma_st<BM, BN, EPI, 3, 2>(a, stream);
+      case 2: return launch_fwd_dma_st<BM, BN, EPI, 2, 4>(a, stream);
+      case 3: return launch_fwd_dma_st<BM, BN, EPI, 3, 4>(a, stream);
+      default: break;
+    }
   }
   return launch_fwd_dma_st<BM, BN, EPI, 2>(a, stream);
 }

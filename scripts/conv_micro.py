@@ -16,7 +16,7 @@ SHAPES = [(1024, 125, 64), (1024, 63, 128), (1024, 32, 256), (1024, 16, 512)]
 def main(reps=50):
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    tag = os.environ.get("ECG_CONV_TILE", "picker")
+    tag = os.environ.get("ECG_CONV_TILE", "picker") + "|v128=" + os.environ.get("ECG_CONV_V128", "0")
     for B, L, C in SHAPES:
         x = torch.randn(B, L, C, device=dev).bfloat16()
         w = (torch.randn(C, 3, C, device=dev) * 0.05).bfloat16()

@@ -86,6 +86,7 @@ for s in $STEPS; do
       ;;
     conv_ab) run conv_picker 120 python scripts/conv_micro.py
              for t in 64x64 128x64 128x128 256x256; do run conv_$t 120 env ECG_CONV_TILE=$t python scripts/conv_micro.py; done ;;
+    conv_v128) for v in 0 1 2 3; do run conv_v128_$v 120 env ECG_CONV_V128=$v python scripts/conv_micro.py; done ;;
     conv_pmc)
       export TMPDIR=/tmp
       P3="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY"
