@@ -34,6 +34,9 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_tiles", [i32, i32, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_target_wgs", [i32, i32, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_set_big", [i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_set_mt", [i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_fwd_ex", [vp] * 7 + [i32] * 10 + [vp, vp, vp])
+    _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles", [_lib.C.c_long, i32])
     lib._conv_mc_bound = True
 
 
@@ -48,6 +51,36 @@ def set_tile_family(big: int) -> int:
     returns the previous setting.  Step plans built before a change keep the tiling they were built with: set it
     first."""
     return _lib_k().ecg_conv1d_nlc_set_big(int(big))
+
+
+def set_multi_tile(mode: int) -> int:
+    """Multi-tile forward workgroups (0: one tile per workgroup, 1 (default): 128x64 tiles of launches with more
+    tiles than two resident workgroups per CU, 2: + the 128-channel shapes); returns the previous mode.  Step plans
+    size their BatchNorm partial rows when built: set it first."""
+    return _lib_k().ecg_conv1d_nlc_set_mt(int(mode))
+
+
+def stat_rows(M: int, c_out: int) -> int:
+    """Rows of BatchNorm partials the forward kernel writes for M output rows and c_out channels."""
+    return _lib_k().ecg_conv1d_nlc_fwd_stat_tiles(int(M), int(c_out))
+
+
+def fwd_stats_raw(x: torch.Tensor, w_t: torch.Tensor, stride: int, pad: int, L_out: int):
+    """Forward conv with the BatchNorm-statistics epilogue (the ResNet plan's CONV_FWD, no fused finalize):
+    returns y [B, L_out, Cout] bf16 and the partial rows [2, rows, Cout] fp32 (sum y, sum y^2 of the stored bf16
+    values; summed over rows they are the per-channel batch statistics)."""
+    B, Lin, Cin = x.shape
+    Cout, K, _ = w_t.shape
+    if not (x.dtype == w_t.dtype == torch.bfloat16 and x.is_contiguous() and w_t.is_contiguous()):
+        raise ValueError("conv1d_nlc: contiguous bf16 operands required")
+    rows = stat_rows(B * L_out, Cout)
+    y = torch.empty((B, L_out, Cout), dtype=torch.bfloat16, device=x.device)
+    stats = torch.empty((2, rows, Cout), dtype=torch.float32, device=x.device)
+    st = _lib_k().ecg_conv1d_nlc_fwd_ex(x.data_ptr(), w_t.data_ptr(), None, y.data_ptr(), stats.data_ptr(), None,
+                                        None, B, Lin, Cin, L_out, Cout, K, stride, pad, 1, 0, None, None,
+                                        _lib.stream_ptr(x.device))
+    _lib.check(st, "ecg_conv1d_nlc_fwd_ex")
+    return y, stats
 
 
 def fwd_raw(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor], stride: int, pad: int,

@@ -102,39 +102,52 @@ struct FwdCfg {
   static constexpr int smem(int nbuf) { return stage_bytes(nbuf) > EP_BYTES ? stage_bytes(nbuf) : EP_BYTES; }
 };
 
-// Forward / data-grad epilogue shared by both main loops: accumulators -> LDS (fp32, per-wave region, two halves
+// Forward / data-grad epilogue shared by the main loops: accumulators -> LDS (fp32, per-wave region, two halves
 // of WM/2 rows) -> row-major pass with 8 channels per lane: + bias, + residual (optionally ReLU-masked), ReLU,
 // bf16 round, and the per-channel BatchNorm partials of the rounded values (stat_mode 0) or the BN-backward
 // partials (stat_mode 1).  The staging buffers must be dead (all waves past the main loop's last barrier).
+// Split in three so the multi-tile kernel can store several M tiles and emit ONE partial row for all of them:
+// EpiConst (per-lane channel constants, fixed for a column block), fwd_epi_tile (one tile's store + the
+// lane's running statistics), fwd_epi_stats (cross-lane / cross-wave reduction and the partial-row store).
+template <int BN, int NWR>
+struct EpiLane {
+  static constexpr int WN = BN / 2, CG = WN / 8;
+  __device__ static int n(int n0) { return n0 + ((threadIdx.x >> 6) & 1) * WN + ((threadIdx.x & 63) % CG) * 8; }
+};
+
+struct EpiConst {
+  float bv[8], mu[8], rsd[8], mud[8], rsdd[8];
+  float s1[8], s2[8], s3[8];
+  template <bool BWD>
+  __device__ __forceinline__ void load(const FwdArgs& a, int n) {
+    const bool ds = BWD && a.szd != nullptr;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bv[e] = a.bias ? a.bias[n + e] : 0.f;
+      s1[e] = s2[e] = s3[e] = 0.f;
+      mu[e] = BWD ? a.smean[n + e] : 0.f;
+      rsd[e] = BWD ? a.srstd[n + e] : 0.f;
+      mud[e] = ds ? a.smean_d[n + e] : 0.f;
+      rsdd[e] = ds ? a.srstd_d[n + e] : 0.f;
+    }
+  }
+};
+
 template <int BM, int BN, int EPI, int NWR = 2>
-__device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, f32x4 (&acc)[BM / NWR / 16][BN / 32],
-                                             unsigned char* smem, int m0, int n0, int mt, int MT, int Lrow, int M,
-                                             int P, int ph) {
+__device__ __forceinline__ void fwd_epi_tile(const FwdArgs& a, f32x4 (&acc)[BM / NWR / 16][BN / 32],
+                                             unsigned char* smem, EpiConst& k, int m0, int n0, int Lrow, int M, int P,
+                                             int ph) {
   using Cfg = FwdCfg<BM, BN, NWR>;
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wr = wv >> 1, wc = wv & 1;
+  const int wr = wv >> 1;
   constexpr int EP_LD = Cfg::EP_LD, HR = WM / 2;
   float* ep = reinterpret_cast<float*>(smem) + wv * HR * EP_LD;
   constexpr int CG = WN / 8, RSTEP = 64 / CG, ITEMS = HR / RSTEP;
   const int cg = lane % CG, rs = lane / CG;
-  const int n = n0 + wc * WN + cg * 8;
+  const int n = EpiLane<BN, NWR>::n(n0);
   constexpr bool bwd = EPI == 1;  // compile-time: the forward epilogue carries none of the backward code
   const bool ds = bwd && a.szd != nullptr;
-  float bv[8], s1[8], s2[8], s3[8], mu[8], rsd[8], mud[8], rsdd[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    bv[e] = a.bias ? a.bias[n + e] : 0.f;
-    s1[e] = s2[e] = s3[e] = 0.f;
-    mu[e] = 0.f;
-    rsd[e] = 0.f;
-    if constexpr (bwd) {
-      mu[e] = a.smean[n + e];
-      rsd[e] = a.srstd[n + e];
-    }
-    mud[e] = ds ? a.smean_d[n + e] : 0.f;
-    rsdd[e] = ds ? a.srstd_d[n + e] : 0.f;
-  }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if (h) __syncthreads();  // previous half fully read
@@ -159,7 +172,7 @@ __device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, f32x4 (&acc)[BM /
         const float4 v1 = *reinterpret_cast<const float4*>(ep + rl * EP_LD + cg * 8 + 4);
         float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += bv[e];
+        for (int e = 0; e < 8; ++e) v[e] += k.bv[e];
         if (a.add) {
           const bf16x8 ad = *reinterpret_cast<const bf16x8*>(a.add + o);
           if (a.add_mask) {
@@ -188,56 +201,76 @@ __device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, f32x4 (&acc)[BM /
           const bf16x8 zz = *reinterpret_cast<const bf16x8*>(a.sz + o);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            s1[e] += v[e];
-            s2[e] += v[e] * ((float)zz[e] - mu[e]) * rsd[e];
+            k.s1[e] += v[e];
+            k.s2[e] += v[e] * ((float)zz[e] - k.mu[e]) * k.rsd[e];
           }
           if (ds) {
             const bf16x8 zd = *reinterpret_cast<const bf16x8*>(a.szd + o);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) s3[e] += v[e] * ((float)zd[e] - mud[e]) * rsdd[e];
+            for (int e = 0; e < 8; ++e) k.s3[e] += v[e] * ((float)zd[e] - k.mud[e]) * k.rsdd[e];
           }
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            s1[e] += v[e];
-            s2[e] += v[e] * v[e];
+            k.s1[e] += v[e];
+            k.s2[e] += v[e] * v[e];
           }
         }
       }
     }
   }
-  if (a.stats) {  // block-uniform
-    const int NS = ds ? 3 : 2;
+}
+
+// The lanes' running statistics -> one partial row ``row`` of ``nrows`` (columns n0 .. n0 + BN).  Block-uniform
+// call (a.stats != null); ``smem``: the dead epilogue region.
+template <int BM, int BN, int EPI, int NWR = 2>
+__device__ __forceinline__ void fwd_epi_stats(const FwdArgs& a, unsigned char* smem, EpiConst& k, int n0, int row,
+                                              int nrows) {
+  using Cfg = FwdCfg<BM, BN, NWR>;
+  constexpr int WN = Cfg::WN, HR = Cfg::WM / 2, EP_LD = Cfg::EP_LD, CG = WN / 8;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1, cg = lane % CG;
+  const bool ds = EPI == 1 && a.szd != nullptr;
+  const int NS = ds ? 3 : 2;
 #pragma unroll
-    for (int off = CG; off < 64; off <<= 1)
+  for (int off = CG; off < 64; off <<= 1)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        s1[e] += __shfl_xor(s1[e], off);
-        s2[e] += __shfl_xor(s2[e], off);
-        if (ds) s3[e] += __shfl_xor(s3[e], off);
-      }
-    float* sred = reinterpret_cast<float*>(smem) + Cfg::NW * HR * EP_LD;  // [wr][stat][BN]
-    if (lane < CG) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        sred[(wr * 3 + 0) * BN + wc * WN + cg * 8 + e] = s1[e];
-        sred[(wr * 3 + 1) * BN + wc * WN + cg * 8 + e] = s2[e];
-        sred[(wr * 3 + 2) * BN + wc * WN + cg * 8 + e] = s3[e];
-      }
+    for (int e = 0; e < 8; ++e) {
+      k.s1[e] += __shfl_xor(k.s1[e], off);
+      k.s2[e] += __shfl_xor(k.s2[e], off);
+      if (ds) k.s3[e] += __shfl_xor(k.s3[e], off);
     }
-    __syncthreads();
-    for (int i = tid; i < NS * BN; i += Cfg::NTHR) {
-      const int st = i / BN, c = i % BN;
-      float v = 0.f;
+  float* sred = reinterpret_cast<float*>(smem) + Cfg::NW * HR * EP_LD;  // [wr][stat][BN]
+  if (lane < CG) {
 #pragma unroll
-      for (int r = 0; r < NWR; ++r) v += sred[(3 * r + st) * BN + c];
-      float* dst = a.stats + ((long)st * MT + mt) * a.Cout + n0 + c;
-      if (a.tail)
-        ecg::st_sc1(dst, v);  // handed to the tail's last arriver inside this launch (write-through)
-      else
-        *dst = v;
+    for (int e = 0; e < 8; ++e) {
+      sred[(wr * 3 + 0) * BN + wc * WN + cg * 8 + e] = k.s1[e];
+      sred[(wr * 3 + 1) * BN + wc * WN + cg * 8 + e] = k.s2[e];
+      sred[(wr * 3 + 2) * BN + wc * WN + cg * 8 + e] = k.s3[e];
     }
   }
+  __syncthreads();
+  for (int i = tid; i < NS * BN; i += Cfg::NTHR) {
+    const int st = i / BN, c = i % BN;
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < NWR; ++r) v += sred[(3 * r + st) * BN + c];
+    float* dst = a.stats + ((long)st * nrows + row) * a.Cout + n0 + c;
+    if (a.tail)
+      ecg::st_sc1(dst, v);  // handed to the tail's last arriver inside this launch (write-through)
+    else
+      *dst = v;
+  }
+}
+
+template <int BM, int BN, int EPI, int NWR = 2>
+__device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, f32x4 (&acc)[BM / NWR / 16][BN / 32],
+                                             unsigned char* smem, int m0, int n0, int mt, int MT, int Lrow, int M,
+                                             int P, int ph) {
+  EpiConst k;
+  k.load<EPI == 1>(a, EpiLane<BN, NWR>::n(n0));
+  fwd_epi_tile<BM, BN, EPI, NWR>(a, acc, smem, k, m0, n0, Lrow, M, P, ph);
+  if (a.stats) fwd_epi_stats<BM, BN, EPI, NWR>(a, smem, k, n0, mt, MT);  // block-uniform
 }
 
 // NBUF = 2: double-buffered LDS, one barrier per K tile (2 workgroups / CU at 128x128).
@@ -492,8 +525,134 @@ __global__ __launch_bounds__(128 * NWR, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_d
     ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, MT, a.Cout, mt, n0, BN, smem);
 }
 
+// Multi-tile LDS-DMA forward (shapes with many more tiles than resident workgroups: the 64/128-channel ResNet
+// stages, where one 128x64 tile is only 3-6 64-deep K steps).  Each workgroup walks M tiles mt = gm, gm + GM, ...
+// of one column block as ONE stream of K steps: the next tile's first stage is DMA'd while this tile's last MFMAs
+// and its epilogue run (the epilogue stages through an LDS region of its own), and the workgroup's statistics
+// accumulate over its tiles into ONE partial row (row gm of GM) - so the BatchNorm tail's ticket, write-through
+// drain and grid-wide hand-off are paid once per workgroup instead of once per tile.  Two workgroups per CU.
+template <int BM, int BN, int EPI, int NWR = 2>
+__global__ __launch_bounds__(128 * NWR, 2) void conv1d_nlc_fwd_dma_mt_kernel(FwdArgs a, int MT, int NT, int GM) {
+  using Cfg = FwdCfg<BM, BN, NWR>;
+  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NW = Cfg::NW;
+  constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
+  constexpr int AP = BM / (8 * NW), BP = BN / (8 * NW);
+  static_assert(AP * 8 * NW == BM && BP * 8 * NW == BN, "tile rows must split into 8-row pieces over the waves");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* const eps = smem + 2 * STAGE;  // epilogue region (live while the next tile's stage lands)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int gm = wgid / NT, nt = wgid % NT;
+  const int n0 = nt * BN;
+  const int CB = a.Cin / BK, nk = a.Kw * CB, K = a.Kw * a.Cin;
+  const int M = a.B * a.Lout;
+  const int ntiles = gm < MT ? (MT - gm + GM - 1) / GM : 0;
+  const int total = ntiles * nk;
+  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, (long)a.Cout * K * 2);
+  unsigned wbase[BP];
+#pragma unroll
+  for (int i = 0; i < BP; ++i) {
+    const int r = 8 * (wv + NW * i) + (lane >> 3);
+    const int cs = (lane & 7) ^ ((r >> 1) & 7);
+    wbase[i] = (unsigned)(((long)(n0 + r) * K + cs * 8) * 2);
+  }
+  // addressing of the tile being loaded (rebuilt when the K-step stream crosses into the next tile)
+  int lt = -1;
+  __amdgpu_buffer_rsrc_t xr = wrs;
+  unsigned abase[AP];
+  int apos[AP];
+  auto setup = [&](int j) {
+    const int m0 = (gm + j * GM) * BM;
+    const int b0 = m0 / a.Lout;
+    const long xrem = (long)(a.B - b0) * a.Lin * a.Cin * 2;
+    xr = make_rsrc(a.x + (long)b0 * a.Lin * a.Cin, xrem < 0x7fff0000L ? xrem : 0x7fff0000L);
+#pragma unroll
+    for (int i = 0; i < AP; ++i) {
+      const int r = 8 * (wv + NW * i) + (lane >> 3), m = m0 + r;
+      const int b = m / a.Lout, t = m - b * a.Lout;
+      const int cs = (lane & 7) ^ ((r >> 1) & 7);
+      abase[i] = m < M ? (unsigned)(((long)(b - b0) * a.Lin * a.Cin + cs * 8) * 2) : 0u;
+      apos[i] = m < M ? t * a.stride - a.pad : INT_MIN / 2;
+    }
+    lt = j;
+  };
+  auto issue = [&](int step, int st) {
+    const int j = step / nk, kt = step - j * nk;
+    if (j != lt) setup(j);
+    const int k = kt / CB, c0 = (kt - k * CB) * BK;
+    unsigned char* As = smem + st * STAGE;
+#pragma unroll
+    for (int i = 0; i < AP; ++i) {
+      const int u = apos[i] + k;
+      const unsigned voff = (u >= 0 && u < a.Lin) ? abase[i] + (unsigned)((u * a.Cin + c0) * 2) : 0x7ffffff0u;
+      dma16(xr, voff, As + (wv + NW * i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < BP; ++i)
+      dma16(wrs, wbase[i] + (unsigned)((k * a.Cin + c0) * 2), As + A_BYTES + (wv + NW * i) * 1024);
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](int st) {
+    const unsigned char* As = smem + st * STAGE;
+    const unsigned char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int cc = 4 * ks + (lane >> 4);
+      bf16x8 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wr * WM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + r * 128 + ((cc ^ ((r >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = wc * WN + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + n * 128 + ((cc ^ ((n >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  EpiConst k;
+  k.load<EPI == 1>(a, EpiLane<BN, NWR>::n(n0));
+  if (total > 0) {  // block-uniform
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int s = 0; s < total; ++s) {
+      if (s + 1 < total) issue(s + 1, (s + 1) & 1);  // lands during this step's MFMAs (and epilogue)
+      mma(s & 1);
+      const int j = s / nk;
+      if (s - j * nk == nk - 1) {  // tile j complete: store it (the epilogue region is not a stage)
+        fwd_epi_tile<BM, BN, EPI, NWR>(a, acc, eps, k, (gm + j * GM) * BM, n0, a.Lout, M, 1, 0);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int q = 0; q < FN; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  if (a.stats) {
+    fwd_epi_stats<BM, BN, EPI, NWR>(a, eps, k, n0, gm, GM);
+    if (a.tail) ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, GM, a.Cout, gm, n0, BN, smem);
+  }
+}
+
 inline bool conv_dma();
 inline int conv_big();
+inline int conv_mt();
 
 // Tile choice: with the LDS-DMA loop (undilated input) 256x256 (8 waves of 64x128) when that gives >= 2 tiles
 // per CU (one workgroup per CU; half the L2->LDS bytes per MAC of 128x128: 1.04 vs 0.87 PF/s on the
@@ -520,6 +679,9 @@ inline void pick_fwd_tile(long M, int Cout, int in_dil, int* bm, int* bn) {
   } else if (big >= 2 && Cout % 128 == 0 && mt256 * (Cout / 128) >= 512) {
     *bm = 256;
     *bn = 128;
+  } else if (Cout == 128 && in_dil == 1 && conv_dma() && conv_mt() >= 2 && mt128 * 2 > 512) {
+    *bm = 128;  // multi-tile 128x64 (ECG_CONV_MT=2)
+    *bn = 64;
   } else if (Cout % 128 == 0 && mt128 * (Cout / 128) >= 256) {  // >= one tile per CU: 15.1 vs 17.7 us for 128x64
     *bm = 128;                                                      // at M=64512 C=128 (profiles/r2/conv_tiles.txt)
     *bn = 128;
@@ -530,6 +692,29 @@ inline void pick_fwd_tile(long M, int Cout, int in_dil, int* bm, int* bn) {
     *bm = 64;
     *bn = 64;
   }
+}
+
+// ECG_CONV_MT=0|1|2: multi-tile forward workgroups (conv1d_nlc_fwd_dma_mt_kernel) for 128x64 tiles when the
+// launch has more tiles than two resident workgroups per CU (1, default), and also for the 128-channel shapes
+// that would otherwise take 128x128 tiles (2); 0 = one tile per workgroup.  Read once.
+int g_conv_mt = -1;
+inline int conv_mt() {
+  if (g_conv_mt < 0) {
+    const char* e = getenv("ECG_CONV_MT");
+    g_conv_mt = e ? atoi(e) : 1;
+  }
+  return g_conv_mt;
+}
+
+// Workgroups along M of the multi-tile forward (0: the one-tile-per-workgroup kernels run).  A function of the
+// shape and the tile alone, so the host can size the BatchNorm partial rows (ecg_conv1d_nlc_fwd_stat_tiles).
+inline int fwd_mt_groups(long M, int Cout, int in_dil, int bm, int bn) {
+  if (in_dil != 1 || !conv_dma() || conv_mt() == 0 || bm != 128 || bn != 64) return 0;
+  const long MT = (M + bm - 1) / bm, NT = Cout / bn;
+  const long slots = 2L * 256;  // two workgroups per CU
+  if (MT * NT <= slots) return 0;
+  const long tpw = (MT * NT + slots - 1) / slots;
+  return (int)((MT + tpw - 1) / tpw);
 }
 
 // ECG_CONV_NBUF=1|2 selects the LDS buffering of the forward/data-grad kernel (read once; default 1).
@@ -607,7 +792,29 @@ inline int conv_v128() {
 }
 
 template <int BM, int BN, int EPI>
+int launch_fwd_dma_mt(const FwdArgs& a, int GM, hipStream_t stream) {
+  using Cfg = FwdCfg<BM, BN, 2>;
+  constexpr int SMEM = 2 * (BM + BN) * 128 + Cfg::EP_BYTES;
+  static_assert(2 * SMEM <= 160 * 1024, "two workgroups per CU");
+  static bool attr = false;
+  if (!attr) {
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_dma_mt_kernel<BM, BN, EPI, 2>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
+    attr = true;
+  }
+  const int MT = (int)(((long)a.B * a.Lout + BM - 1) / BM), NT = a.Cout / BN;
+  hipLaunchKernelGGL((conv1d_nlc_fwd_dma_mt_kernel<BM, BN, EPI, 2>), dim3((unsigned)(GM * NT)), dim3(Cfg::NTHR), SMEM,
+                     stream, a, MT, NT, GM);
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
+}
+
+template <int BM, int BN, int EPI>
 int launch_fwd_dma(const FwdArgs& a, hipStream_t stream) {
+  if constexpr (BM == 128 && BN == 64) {
+    const int GM = fwd_mt_groups((long)a.B * a.Lout, a.Cout, a.in_dil, BM, BN);
+    if (GM > 0) return launch_fwd_dma_mt<BM, BN, EPI>(a, GM, stream);
+  }
   if constexpr (BN == 64 && BM <= 128) {
     if (conv_nst64() == 3) return launch_fwd_dma_st<BM, BN, EPI, 3>(a, stream);
   }
@@ -655,6 +862,8 @@ int launch_fwd(const FwdArgs& a, hipStream_t stream) {
                       (long)a.Cout * a.Kw * a.Cin * 2 < 0x7fff0000L;
   if (conv_dma() && dma_ok)
     return a.stat_mode == 1 ? launch_fwd_dma<BM, BN, 1>(a, stream) : launch_fwd_dma<BM, BN, 0>(a, stream);
+  if (a.stats && fwd_mt_groups((long)a.B * a.Lout, a.Cout, a.in_dil, BM, BN) > 0)
+    return ecg::kBadArg;  // the host sized the partial rows for the multi-tile kernel
   if constexpr (BM > 128) return ecg::kBadArg;  // 256-row tiles exist only as DMA kernels (the picker ensures it)
   else {
     if (conv_nbuf() == 2)
@@ -1086,18 +1295,27 @@ ECG_API int ecg_conv1d_nlc_set_big(int big) {
   return prev;
 }
 
+// Select the multi-tile forward mode (see conv_mt); returns the previous setting.  Plans built before a change
+// keep their BatchNorm partial-row counts: build them after setting the mode.
+ECG_API int ecg_conv1d_nlc_set_mt(int mode) {
+  const int prev = conv_mt();
+  g_conv_mt = mode < 0 ? 0 : (mode > 2 ? 2 : mode);
+  return prev;
+}
+
 // Number of M tiles (rows of the BN-statistics partials) the forward kernel uses for this shape.
 ECG_API int ecg_conv1d_nlc_fwd_stat_tiles(long M, int Cout) {
   int bm, bn;
   pick_fwd_tile(M, Cout, 1, &bm, &bn);
-  return (int)((M + bm - 1) / bm);
+  const int gm = fwd_mt_groups(M, Cout, 1, bm, bn);
+  return gm > 0 ? gm : (int)((M + bm - 1) / bm);
 }
 
 // Same for a call with batch B, output length Lout and input dilation in_dil (phase-decomposed data-grad).
 ECG_API int ecg_conv1d_nlc_fwd_stat_tiles_ex(int B, int Lout, int Cout, int in_dil) {
   int bm, bn;
   pick_fwd_tile((long)B * Lout, Cout, in_dil, &bm, &bn);
-  if (in_dil <= 1) return (int)(((long)B * Lout + bm - 1) / bm);
+  if (in_dil <= 1) return ecg_conv1d_nlc_fwd_stat_tiles((long)B * Lout, Cout);
   const int Lph = (Lout + in_dil - 1) / in_dil;
   return in_dil * (int)(((long)B * Lph + bm - 1) / bm);
 }

@@ -33,7 +33,23 @@ for s in $STEPS; do
     bench20) run bench20 300 python bench.py --steps 20 --warmup 5
              run bench20b 300 python bench.py --steps 20 --warmup 5 --no-extras
              run bench500 300 python bench.py --steps 500 --warmup 100 --no-extras ;;
+    resnet) run bench_resnet34 600 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras ;;
+    resnet_tests) run resnet_tests 600 python -u -m pytest tests/test_resnet_engine_gpu.py tests/test_conv_mc_gpu.py \
+                    -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    mt_ab) for r in a b; do
+             for v in 0 1 2; do
+               run bench_resnet34_mt${v}$r 300 env ECG_CONV_MT=$v python bench.py --model resnet1d34 --steps 20 \
+                 --warmup 5 --no-extras
+             done
+           done
+           run op_profile_mt1 300 env ECG_CONV_MT=1 python scripts/resnet_op_profile.py 34 1024
+           run op_profile_mt2 300 env ECG_CONV_MT=2 python scripts/resnet_op_profile.py 34 1024 ;;
     diag_g1) run diag_g1 600 python scripts/diag_g1_overlap.py "$OUT/diag_g1" ;;
+    diag_region) run diag_region 300 python scripts/diag_timed_region.py 20 9 ;;
+    op_prof) run op_profile_mt0 300 env ECG_CONV_MT=0 python scripts/resnet_op_profile.py 34 1024
+             run op_profile_mt1 300 env ECG_CONV_MT=1 python scripts/resnet_op_profile.py 34 1024 ;;
+    mt_tests) run mt_tests 600 python -u -m pytest tests/test_conv_mc_gpu.py -k "stats_multi_tile" \
+                tests/test_resnet_engine_gpu.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     diag_call) run diag_overhead 300 python scripts/diag_bench_overhead.py
                run diag_conv1d_call 300 python scripts/diag_conv1d_call.py ;;
     diag_resnet) run diag_resnet 600 python scripts/diag_resnet_numerics.py ;;

@@ -102,3 +102,30 @@ def test_resnet1d_hip_backend_matches_torch():
     for n in g32:
         e_amp, e_hip = _rel(gam[n], g32[n]), _rel(ghp[n], g32[n])
         assert e_hip < 1.5 * e_amp + 0.05 and e_hip < 0.6, (n, e_hip, e_amp)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("B,L,C", [(1024, 125, 64), (1024, 63, 128), (700, 125, 64)])
+def test_conv1d_nlc_stats_multi_tile(mode, B, L, C):
+    """BatchNorm-statistics epilogue (the ResNet plan's CONV_FWD) on every forward mode: the stored outputs are the
+    same bits whichever kernel runs (multi-tile workgroups compute each tile exactly like one-tile workgroups), and
+    the partial rows sum to the fp64 statistics of those stored bf16 values."""
+    from crossscale_ecg.ops import conv_mc
+    torch.manual_seed(1)
+    x = torch.randn(B, L, C, device="cuda").bfloat16()
+    w = (torch.randn(C, 3, C, device="cuda") * 0.05).bfloat16()
+    prev = conv_mc.set_multi_tile(0)
+    try:
+        y0, _ = conv_mc.fwd_stats_raw(x, w, 1, 1, L)
+        conv_mc.set_multi_tile(mode)
+        y, stats = conv_mc.fwd_stats_raw(x, w, 1, 1, L)
+        torch.cuda.synchronize()
+    finally:
+        conv_mc.set_multi_tile(prev)
+    assert torch.equal(y, y0)
+    if mode == 1 and C == 64 or mode == 2:
+        assert stats.shape[1] < (B * L + 127) // 128  # the multi-tile kernel ran (fewer partial rows than tiles)
+    yd = y.double().reshape(-1, C)
+    s1, s2 = stats.double().sum(1)
+    torch.testing.assert_close(s1, yd.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(s2, (yd * yd).sum(0), rtol=1e-5, atol=1e-3)

@@ -74,6 +74,40 @@ def test_engine_large_batch_tiles():
             assert _rel(b, br) < 2e-2, n
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+def test_engine_multi_tile_forward_matches_one_tile(mode):
+    """B=1024: the 64-channel stage convs (1000 M tiles) - and with mode 2 the 128-channel ones - run on the
+    multi-tile forward kernel (several M tiles per workgroup, one BatchNorm partial row per workgroup).  Outputs
+    are computed tile by tile exactly as before; only the BN statistics' summation order changes, so the step
+    agrees with the one-tile plan up to bf16 rounding flips, which a deep random-init net amplifies chaotically
+    towards the stem (the kernel-level equality is pinned by test_conv1d_nlc_stats_multi_tile)."""
+    from crossscale_ecg.ops import conv_mc
+    prev = conv_mc.set_multi_tile(0)
+    try:
+        one = conv_mc.stat_rows(1024 * 125, 64)
+        m0, _, eng0, x, y = _setup(18, B=1024, use_graph=False, seed=5)
+        eng0.forward_backward()
+        torch.cuda.synchronize()
+        conv_mc.set_multi_tile(mode)
+        multi = conv_mc.stat_rows(1024 * 125, 64)
+        assert multi < one == 1000, (multi, one)
+        if mode == 2:
+            assert conv_mc.stat_rows(1024 * 63, 128) < (1024 * 63 + 127) // 128
+        m1, _, eng1, _, _ = _setup(18, B=1024, use_graph=False, seed=5)
+        eng1.set_batch(x, y)
+        eng1.forward_backward()
+        torch.cuda.synchronize()
+    finally:
+        conv_mc.set_multi_tile(prev)
+    assert abs(eng0.avg_loss() - eng1.avg_loss()) < 1e-3
+    errs = {n: _rel(p1.grad, p0.grad) for (n, p0), (_, p1) in zip(m0.named_parameters(), m1.named_parameters())}
+    assert errs["fc.weight"] < 1e-2 and errs["fc.bias"] < 1e-2, errs  # head: a few bf16 flips deep
+    assert max(errs.values()) < 0.3, errs  # round-off amplification (engine vs fp32 torch: up to 0.6 at depth 18)
+    for (n, b0), (_, b1) in zip(m0.named_buffers(), m1.named_buffers()):
+        if b0.is_floating_point():
+            assert _rel(b1, b0) < 1e-3, n
+
+
 @pytest.mark.parametrize("side", ["0", "1"])
 def test_engine_graph_equals_eager_bitwise(side, monkeypatch):
     # side "1": weight gradients on the side stream, the graph is the captured fork-join DAG (forced: by default
