@@ -10,7 +10,8 @@ rounds of ``--local-steps`` steps; EVERY round - including a trailing partial on
 all-reduce (one RCCL ``all_reduce(AVG)`` of the flat weights, reference part3_fedavg_overlap_mpi_gpu.py:
 209-211), so the timed region always contains communication.  W warmup steps (same round plan), then
 every hipGraph the timed plan needs is captured and uploaded, then exactly K timed steps bracketed by
-barrier + synchronize; value = N * B * K / max-over-ranks(elapsed) (whole-job samples/s).  Each round's
+barrier (a shared-memory host barrier when all ranks share the node, parallel/host_barrier.py) + synchronize;
+value = N * B * K / max-over-ranks(elapsed) (whole-job samples/s).  Each round's
 batch indices are drawn while the previous round computes (the first timed round's behind the last warmup
 round) and copied into the step table by the round graph's first node.
 
@@ -268,6 +269,10 @@ def main(argv=None):
         amp = torch.bfloat16 if on_gpu else None
         trainer = TorchLocalTrainer(model, x, y, B, amp_dtype=amp, seed=4321 + ctx.rank)
     runner = FedAvgRunner(trainer, flat, ctx, a.overlap)
+    # timing brackets: a shared-memory host barrier when every rank is on this node (parallel/host_barrier.py),
+    # else the process-group barrier
+    from crossscale_ecg.parallel.host_barrier import HostBarrier
+    tbar = HostBarrier(ctx)
 
     timed_plan = round_plan(a.steps, S)
     if a.warmup > 0:
@@ -276,14 +281,16 @@ def main(argv=None):
         trainer.prepare(sorted(set(timed_plan)))
     runner.syncs = 0
     sync()
-    barrier(ctx)
+    tbar()
     sync()
     t0 = time.perf_counter()
     runner.run(timed_plan)
     sync()
-    barrier(ctx)
+    tbar()
     sync()
     elapsed = time.perf_counter() - t0
+    tbar_kind = tbar.kind
+    tbar.close()
     world_seen, dist_backend = 1, "none"
     if ctx.distributed:
         import torch.distributed as dist
@@ -343,6 +350,7 @@ def main(argv=None):
             "rccl_world_size": world_seen,
             "dist_backend": dist_backend,
             "fedavg_syncs_timed": runner.syncs,
+            "timing_barrier": tbar_kind,
             "timed_round_plan": timed_plan if len(timed_plan) <= 4 else f"{len(timed_plan)} rounds",
             "final_avg_loss": round(loss, 6) if loss == loss else None,
             **extras,

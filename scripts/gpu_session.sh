@@ -46,6 +46,13 @@ for s in $STEPS; do
            run op_profile_mt2 300 env ECG_CONV_MT=2 python scripts/resnet_op_profile.py 34 1024 ;;
     diag_g1) run diag_g1 600 python scripts/diag_g1_overlap.py "$OUT/diag_g1" ;;
     diag_region) run diag_region 300 python scripts/diag_timed_region.py 20 9 ;;
+    timeline)
+      export TMPDIR=/tmp
+      run resnet_tl 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/tl" -o tl -- \
+        python3 scripts/resnet_timeline.py run
+      ;;
+    bench_n2) run bench_n2_gloo 300 env ECG_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 20 --warmup 5 \
+                --no-extras ;;
     op_prof) run op_profile_mt0 300 env ECG_CONV_MT=0 python scripts/resnet_op_profile.py 34 1024
              run op_profile_mt1 300 env ECG_CONV_MT=1 python scripts/resnet_op_profile.py 34 1024 ;;
     mt_tests) run mt_tests 600 python -u -m pytest tests/test_conv_mc_gpu.py -k "stats_multi_tile" \
