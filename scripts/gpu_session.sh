@@ -53,6 +53,13 @@ for s in $STEPS; do
       ;;
     bench_n2) run bench_n2_gloo 300 env ECG_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 20 --warmup 5 \
                 --no-extras ;;
+    knob_ab)
+      for r in a b; do
+        for kv in "X=0" "ECG_CONV_BIG=0" "ECG_CONV_BIG=2" "ECG_CONV_V128=1" "ECG_CONV_V128=2" "ECG_CONV_NST=3" \
+                  "ECG_WGRAD_MAX_SPLITS=48" "ECG_WGRAD_MAX_SPLITS=96" "ECG_CONV_MT=2" "ECG_CONV_NBUF=2"; do
+          run "knob_${kv}_$r" 300 env $kv python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+        done
+      done ;;
     op_prof) run op_profile_mt0 300 env ECG_CONV_MT=0 python scripts/resnet_op_profile.py 34 1024
              run op_profile_mt1 300 env ECG_CONV_MT=1 python scripts/resnet_op_profile.py 34 1024 ;;
     mt_tests) run mt_tests 600 python -u -m pytest tests/test_conv_mc_gpu.py -k "stats_multi_tile" \
