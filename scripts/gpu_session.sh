@@ -60,6 +60,10 @@ for s in $STEPS; do
           run "knob_${kv}_$r" 300 env $kv python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
         done
       done ;;
+    hbm_bench)
+      run bench_resnet34_64gb 600 python bench.py --model resnet1d34 --max-windows 32000000 --steps 60 --warmup 10 \
+        --no-extras
+      run bench_tiny_64gb 600 python bench.py --max-windows 32000000 --steps 500 --warmup 100 --no-extras ;;
     op_prof) run op_profile_mt0 300 env ECG_CONV_MT=0 python scripts/resnet_op_profile.py 34 1024
              run op_profile_mt1 300 env ECG_CONV_MT=1 python scripts/resnet_op_profile.py 34 1024 ;;
     mt_tests) run mt_tests 600 python -u -m pytest tests/test_conv_mc_gpu.py -k "stats_multi_tile" \
