@@ -64,6 +64,7 @@ for s in $STEPS; do
       run bench_resnet34_64gb 600 python bench.py --model resnet1d34 --max-windows 32000000 --steps 60 --warmup 10 \
         --no-extras
       run bench_tiny_64gb 600 python bench.py --max-windows 32000000 --steps 500 --warmup 100 --no-extras ;;
+    conv_stats) run conv_stats 300 python scripts/conv_stats_micro.py ;;
     op_prof) run op_profile_mt0 300 env ECG_CONV_MT=0 python scripts/resnet_op_profile.py 34 1024
              run op_profile_mt1 300 env ECG_CONV_MT=1 python scripts/resnet_op_profile.py 34 1024 ;;
     mt_tests) run mt_tests 600 python -u -m pytest tests/test_conv_mc_gpu.py -k "stats_multi_tile" \
@@ -130,6 +131,11 @@ for s in $STEPS; do
       export TMPDIR=/tmp
       run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
         python3 bench.py --steps 200 --warmup 50 --no-extras
+      ;;
+    prof_resnet)
+      export TMPDIR=/tmp
+      run rocprof_resnet 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_resnet" -o resnet -- \
+        python3 bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
       ;;
     *) echo "unknown step $s" ;;
   esac
