@@ -24,6 +24,7 @@ def test_bench_self_launch_world2_partial_round_syncs():
     rec = _bench("--gpus", "2", "--steps", "7", "--warmup", "3", "--local-steps", "5")
     assert rec["n_gpus"] == 2 and rec["rccl_world_size"] == 2 and rec["dist_backend"] == "gloo"
     assert rec["timed_round_plan"] == [5, 2] and rec["fedavg_syncs_timed"] == 2
+    assert rec["timing_barrier"] == "shm"  # both ranks on this node: shared-memory timing barrier
     assert rec["config"]["global_batch"] == 32 and rec["config"]["parallelism"] == "dp2"
     assert rec["value"] == rec["n_gpus"] * 16 * 7 / (rec["ms_per_step"] * 7 / 1e3) or \
         abs(rec["value"] - 32 / (rec["ms_per_step"] / 1e3)) < 1e-3 * rec["value"]
@@ -37,3 +38,4 @@ def test_bench_overlap_none_world2():
 def test_bench_single_rank():
     rec = _bench("--steps", "3", "--warmup", "1", "--local-steps", "2")
     assert rec["n_gpus"] == 1 and rec["rccl_world_size"] == 1 and rec["fedavg_syncs_timed"] == 2
+    assert rec["timing_barrier"] == "none"
