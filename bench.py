@@ -280,14 +280,17 @@ def main(argv=None):
     if hasattr(trainer, "prepare"):  # capture + upload every graph the timed plan replays, outside the timing
         trainer.prepare(sorted(set(timed_plan)))
     runner.syncs = 0
-    sync()
-    tbar()
-    sync()
+
+    def bracket():  # synchronize + barrier (+ synchronize again only when the barrier itself enqueued GPU work)
+        sync()
+        tbar()
+        if tbar.kind == "dist":
+            sync()
+
+    bracket()
     t0 = time.perf_counter()
     runner.run(timed_plan)
-    sync()
-    tbar()
-    sync()
+    bracket()
     elapsed = time.perf_counter() - t0
     tbar_kind = tbar.kind
     tbar.close()

@@ -113,8 +113,14 @@ def kernels_available() -> bool:
     return _load("libecg_kernels.so") is not None
 
 
+_kernels_lib: Optional[C.CDLL] = None
+
+
 def kernels() -> C.CDLL:
     """The HIP kernel library (raises if it was not built)."""
+    global _kernels_lib
+    if _kernels_lib is not None:  # bound once; no lock on the per-launch path
+        return _kernels_lib
     lib = _load("libecg_kernels.so")
     if lib is None:
         raise NativeError(f"libecg_kernels.so not found in {LIB_DIR}: run `python csrc/build.py` "
@@ -122,6 +128,7 @@ def kernels() -> C.CDLL:
     if not getattr(lib, "_ecg_bound", False):
         _bind_kernels(lib)
         lib._ecg_bound = True
+    _kernels_lib = lib
     return lib
 
 
@@ -170,8 +177,20 @@ def cpu_available() -> bool:
     return _load("libconv1d_cpu.so") is not None
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device=None) -> int:
-    """Raw hipStream_t of torch's current stream on ``device``."""
+    """Raw hipStream_t of torch's current stream on ``device`` (one C++ call: this sits on the launch path of
+    every timed round, where building a torch Stream object first cost microseconds)."""
+    if _raw_stream is not None:
+        if device is None:
+            idx = torch.cuda.current_device()
+        elif isinstance(device, int):
+            idx = device
+        else:
+            idx = device.index if device.index is not None else torch.cuda.current_device()
+        return _raw_stream(idx)
     return torch.cuda.current_stream(device).cuda_stream
 
 

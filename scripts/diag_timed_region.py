@@ -30,10 +30,13 @@ def main(K=20, reps=9):
     tr.prepare([K])
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    rows = {"graph": [], "eager": []}
+    from crossscale_ecg.ops import _lib
+    raw = _lib._raw_stream
+    rows = {"graph": [], "graph_slowstream": [], "eager": []}
     for r in range(reps):
-        for mode in rows:  # interleaved: same box state for both
-            tr.use_graph = mode == "graph"
+        for mode in rows:  # interleaved: same box state for all
+            tr.use_graph = mode != "eager"
+            _lib._raw_stream = None if mode == "graph_slowstream" else raw  # torch Stream object per launch
             tr.prepare_round(K, reset_loss=False)  # batches staged outside the timing (bench: behind the warmup)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -48,11 +51,11 @@ def main(K=20, reps=9):
             span = e0.elapsed_time(e1) * 1e3
             rows[mode].append(((t1 - t0) * 1e6, (t2 - t0) * 1e6, (t3 - t0) * 1e6, span))
             c = rows[mode][-1]
-            print(f"rep {r} {mode:5s}: launch call {c[0]:7.1f} us  sync1 {c[1]:7.1f}  sync2 {c[2]:7.1f}  gpu span "
+            print(f"rep {r} {mode:16s}: launch call {c[0]:7.1f} us  sync1 {c[1]:7.1f}  sync2 {c[2]:7.1f}  gpu span "
                   f"{span:7.1f} us  -> wall/step {c[2] / K:6.2f}  span/step {span / K:6.2f}", flush=True)
     for mode, rr in rows.items():
         med = [statistics.median(c) for c in zip(*rr)]
-        print(f"median {mode:5s}: launch call {med[0]:.1f} us, wall {med[2]:.1f} us, gpu span {med[3]:.1f} us, "
+        print(f"median {mode:16s}: launch call {med[0]:.1f} us, wall {med[2]:.1f} us, gpu span {med[3]:.1f} us, "
               f"fixed {med[2] - med[3]:.1f} us ({(med[2] - med[3]) / K:.2f} us/step at K={K}), "
               f"wall/step {med[2] / K:.2f} us")
     tr.close()

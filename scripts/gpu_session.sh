@@ -65,6 +65,10 @@ for s in $STEPS; do
         --no-extras
       run bench_tiny_64gb 600 python bench.py --max-windows 32000000 --steps 500 --warmup 100 --no-extras ;;
     conv_stats) run conv_stats 300 python scripts/conv_stats_micro.py ;;
+    k20_series)
+      for i in 1 2 3 4; do run k20_$i 300 python bench.py --steps 20 --warmup 5 --no-extras; done
+      sleep 5
+      for i in 5 6; do run k20_$i 300 python bench.py --steps 20 --warmup 5 --no-extras; done ;;
     op_prof) run op_profile_mt0 300 env ECG_CONV_MT=0 python scripts/resnet_op_profile.py 34 1024
              run op_profile_mt1 300 env ECG_CONV_MT=1 python scripts/resnet_op_profile.py 34 1024 ;;
     mt_tests) run mt_tests 600 python -u -m pytest tests/test_conv_mc_gpu.py -k "stats_multi_tile" \
