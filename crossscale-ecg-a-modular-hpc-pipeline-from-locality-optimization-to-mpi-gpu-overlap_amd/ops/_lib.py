@@ -94,6 +94,7 @@ def _bind_kernels(lib: C.CDLL) -> None:
     _sig(lib, "conv1d_batch_hip", [vp, vp, vp, i32, i32, i32, vp])
     _sig(lib, "conv1d_batch_hip_sync", [vp, vp, vp, i32, i32, i32, vp])
     _sig(lib, "conv1d_batch_hip_spin", [vp, vp, vp, i32, i32, i32, vp])
+    _sig(lib, "conv1d_batch_hip_flag", [vp, vp, vp, i32, i32, i32, vp])
     _sig(lib, "conv1d_valid_dgrad_hip", [vp, vp, vp, i32, i32, i32, vp])
     _sig(lib, "conv1d_valid_dgrad_hip_bf16", [vp, vp, vp, i32, i32, i32, vp])
     _sig(lib, "conv1d_valid_wgrad_ws_floats", [i32, i32, i32], i64)

@@ -1,8 +1,9 @@
 """Single-channel valid conv1d (the Module-2 op) on three backends, plus its HIP backward.
 
 * ``hip``   - ``conv1d_batch_hip`` (csrc/kernels/conv1d_valid.hip), fp32 or bf16, async on the torch stream;
-              ``blocking=True`` uses ``conv1d_batch_hip_sync`` (returns when the output is complete, like the
-              reference's CPU kernel) - the single-call path the Module-2 ``time_once`` metric measures.
+              ``blocking=True`` uses ``conv1d_batch_hip_flag`` (returns when the output is complete, like the
+              reference's CPU kernel: the kernel's last workgroup publishes completion to a host-mapped word the
+              caller polls) - the single-call path the Module-2 ``time_once`` metric measures.
               ``conv1d_valid_fn`` is the differentiable version (HIP dgrad + deterministic two-pass wgrad).
 * ``cpu``   - ``conv1d_batch_omp_simd`` (csrc/cpu/conv1d_cpu.cpp), the reference C ABI
               (Module_2/conv1d_openmp_simd.c:21-28) with OpenMP + AVX2/AVX-512.
@@ -50,7 +51,7 @@ def _conv1d_hip_fast(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None,
     if not _HIP_FNS:
         lib = _lib.kernels()  # raises if the HIP library is missing: no silent fallback on a GPU tensor
         _HIP_FNS.update({torch.float32: lib.conv1d_batch_hip, torch.bfloat16: lib.conv1d_batch_hip_bf16,
-                         "sync": lib.conv1d_batch_hip_sync})
+                         "sync": lib.conv1d_batch_hip_flag})
     fn = _HIP_FNS.get("sync" if blocking and x.dtype == torch.float32 else x.dtype)
     if fn is None:
         return None
@@ -73,10 +74,11 @@ def _conv1d_hip_fast(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None,
 class HipConv1dValid:
     """A bound single-channel valid conv1d on the HIP kernel - the op-object counterpart of ``nn.Conv1d(1, 1, K)``
     (taps held by the object, like the module holds its weight).  ``y = op(x, out)`` for x [B, L] / [B, 1, L]
-    fp32 on the taps' device, out [B, L-K+1].  ``blocking``: return when y is complete (launch +
-    hipStreamSynchronize in one native call: the reference CPU kernel's call semantics,
-    Module_2/conv1d_openmp_simd.c:21-61; measured faster than polling hipStreamQuery, profiles/r2/
-    conv1d_single_call_breakdown.txt); else async on the current stream.  Per call it only re-checks the shapes
+    fp32 on the taps' device, out [B, L-K+1].  ``blocking``: return when y is complete (the reference CPU
+    kernel's call semantics, Module_2/conv1d_openmp_simd.c:21-61): one native call that launches the kernel and
+    polls a host-mapped word its last workgroup writes once every output store has drained (9.4-9.6 us at
+    B=256, K=7 vs 14.0 for launch + hipStreamSynchronize, 16.7 polling hipStreamQuery; profiles/r2/
+    conv1d_flag_call_ab.txt); else async on the current stream.  Per call it only re-checks the shapes
     and takes the data pointers."""
 
     def __init__(self, w: torch.Tensor, blocking: bool = True):
@@ -85,7 +87,7 @@ class HipConv1dValid:
         self.w = w.detach().reshape(-1).to(torch.float32).contiguous()
         self.K = self.w.numel()
         lib = _lib.kernels()
-        self._fn = lib.conv1d_batch_hip_sync if blocking else lib.conv1d_batch_hip
+        self._fn = lib.conv1d_batch_hip_flag if blocking else lib.conv1d_batch_hip
         self._wp = self.w.data_ptr()
         self._dev = self.w.device.index
         self._shapes = None

@@ -18,6 +18,10 @@
 //   * wgrad: per-workgroup partial sums [G][K] (fixed order) + a one-workgroup second pass - deterministic.
 #include "../include/ecg_common.h"
 
+#include <chrono>
+#include <cstring>
+#include <mutex>
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -79,6 +83,61 @@ __device__ __forceinline__ void store_quad(TY* __restrict__ yrow, int pos, int l
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if (pos + j < len) store1(yrow + pos + j, acc[j]);
+  }
+}
+
+// ------------------------------------------------------------------------------- forward, completion flag
+// The blocking single call (Module-2's "one call returns a complete output", Module_2/benchmark_part_2.py:61-67):
+// the same per-quad math with kFlagQPT quads per thread (all loads first), then a completion hand-off the host
+// can see without the runtime's kernel-completion path: every wave drains its stores (vmcnt(0)), one lane per
+// workgroup takes an agent-scope ticket, and the last workgroup resets the ticket counter and stores ``epoch``
+// to ONE host-mapped word (system scope) that the calling thread polls.  (Measured: one word per workgroup, all
+// polled by the host, instead of the ticket - 13.4 vs 11.3 us per call at B=256: 31 fabric writes into the
+// polled lines cost more than the ~12 ns-per-arrival ticket.)  Later device work is stream-ordered behind the
+// kernel as usual; the host only stops waiting for the runtime's end-of-kernel signal.
+template <int KC, int kFlagQPT, int kFlagThreads>
+__global__ __launch_bounds__(kFlagThreads) void conv1d_valid_fwd_flag_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ y, int B, int L, int K, int outL,
+    int nquads, int xvec, int yvec, unsigned* __restrict__ counter, unsigned* __restrict__ host_flag,
+    unsigned epoch) {
+  constexpr int NV = (KC + 3 + 3) / 4;
+  const long total = (long)B * nquads;
+  const long base = (long)blockIdx.x * kFlagThreads * kFlagQPT + threadIdx.x;  // quad u: base + u * threads
+  float xv[kFlagQPT][4 * NV];
+  float wr[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) wr[k] = w[k];
+#pragma unroll
+  for (int u = 0; u < kFlagQPT; ++u) {
+    const long gq = base + (long)u * kFlagThreads;
+    if (gq < total) {
+      const int b = (int)(gq / nquads), q = (int)(gq - (long)b * nquads);
+      load_span<NV>(x + (long)b * L, 4 * q, L, xvec != 0, xv[u]);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kFlagQPT; ++u) {
+    const long gq = base + (long)u * kFlagThreads;
+    if (gq < total) {
+      const int b = (int)(gq / nquads), q = (int)(gq - (long)b * nquads);
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < KC; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = fmaf(xv[u][j + k], wr[k], acc[j]);
+      store_quad(y + (long)b * outL, 4 * q, outL, yvec != 0, acc);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's output stores have completed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == gridDim.x - 1) {
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // relaxed: the host learns "done" from this word and never reads y through it (later device work is
+      // stream-ordered behind the kernel), so no L2 write-back (buffer_wbl2) is needed in front of it
+      __hip_atomic_store(host_flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
@@ -315,6 +374,94 @@ ECG_API int conv1d_batch_hip_spin(const float* x, const float* w, float* y, int 
   while ((e = hipStreamQuery(stream)) == hipErrorNotReady) {
   }
   return e == hipSuccess ? ecg::kOk : ecg::kHipError;
+}
+
+// Per-device completion state of the flag call: a zeroed ticket counter (device) and a host-mapped flag word.
+namespace {
+struct FlagState {
+  unsigned* counter = nullptr;
+  unsigned* flag_host = nullptr;
+  unsigned* flag_dev = nullptr;
+  unsigned epoch = 0;
+};
+std::mutex g_flag_mu;
+FlagState g_flag[64];
+}  // namespace
+
+// Blocking forward that returns as soon as the kernel's last workgroup has published completion (see
+// conv1d_valid_fwd_flag_kernel): launch, then poll a host-mapped word.  K must be one of the compile-time tap
+// counts (3, 5, 7, 9, 11, 15, 32) - else the plain launch + hipStreamSynchronize runs.  A poll that outlives
+// ``timeout`` falls back to hipStreamSynchronize (so a fault is reported by the runtime, never hidden).
+ECG_API int conv1d_batch_hip_flag(const float* x, const float* w, float* y, int batch, int L, int K,
+                                  hipStream_t stream) {
+  if (batch <= 0 || L <= 0 || K <= 0 || K > L) return ecg::kBadArg;
+  const bool kc = K == 3 || K == 5 || K == 7 || K == 9 || K == 11 || K == 15 || K == 32;
+  if (!kc) return conv1d_batch_hip_sync(x, w, y, batch, L, K, stream);
+  int dev = 0;
+  ECG_HIP_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return ecg::kBadArg;
+  std::lock_guard<std::mutex> lk(g_flag_mu);
+  FlagState& f = g_flag[dev];
+  const int outL = L - K + 1, nquads = (outL + 3) / 4;
+  const long total = (long)batch * nquads;
+  // ECG_CONV1D_FLAG_CFG (A/B, read once): threads x quads per thread = 0: 512x2, 1: 512x4, 2: 1024x2, 3: 256x1
+  // (default), 4: 128x1, 5: 64x1.  B=256, L=500, K=7 single call (profiles/r2/conv1d_flag_call_ab.txt): 10.6,
+  // 12.4, 12.4, 9.4-9.6, 10.5, 13.4 us - the 124 workgroups of one quad per thread beat fatter threads (less
+  // ticket fan-in) and thinner workgroups (more of it).
+  static const int cfg = [] {
+    const char* e = getenv("ECG_CONV1D_FLAG_CFG");
+    return e ? atoi(e) : 3;
+  }();
+  static const int kNT[6] = {512, 512, 1024, 256, 128, 64}, kQ[6] = {2, 4, 2, 1, 1, 1};
+  const int ci = cfg < 0 || cfg > 5 ? 0 : cfg;
+  const int nt = kNT[ci], qpt = kQ[ci];
+  const long G = (total + (long)nt * qpt - 1) / ((long)nt * qpt);
+  if (G > 0x7fffffffL) return ecg::kBadArg;
+  if (!f.counter) {
+    ECG_HIP_CHECK(hipMalloc(&f.counter, 64));
+    ECG_HIP_CHECK(hipMemset(f.counter, 0, 64));
+    ECG_HIP_CHECK(hipHostMalloc(&f.flag_host, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    ECG_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&f.flag_dev), f.flag_host, 0));
+    __atomic_store_n(f.flag_host, 0u, __ATOMIC_RELEASE);
+    ECG_HIP_CHECK(hipDeviceSynchronize());  // the counter's memset has landed before the first ticket
+  }
+  const unsigned epoch = ++f.epoch == 0 ? ++f.epoch : f.epoch;  // never 0 (the flag's initial value)
+  const dim3 grid((unsigned)G);
+  const int xv = vec_ok(x, L), yv = vec_ok(y, outL);
+#define ECG_FLAG_CFG(KK, Q, T)                                                                                    \
+  hipLaunchKernelGGL((conv1d_valid_fwd_flag_kernel<KK, Q, T>), grid, dim3(T), 0, stream, x, w, y, batch, L, K, outL, \
+                     nquads, xv, yv, f.counter, f.flag_dev, epoch)
+#define ECG_FLAG(KK)                                              \
+  do {                                                            \
+    if (ci == 1) ECG_FLAG_CFG(KK, 4, 512);                        \
+    else if (ci == 2) ECG_FLAG_CFG(KK, 2, 1024);                  \
+    else if (ci == 3) ECG_FLAG_CFG(KK, 1, 256);                   \
+    else if (ci == 4) ECG_FLAG_CFG(KK, 1, 128);                   \
+    else if (ci == 5) ECG_FLAG_CFG(KK, 1, 64);                    \
+    else ECG_FLAG_CFG(KK, 2, 512);                                \
+  } while (0)
+  switch (K) {
+    case 3: ECG_FLAG(3); break;
+    case 5: ECG_FLAG(5); break;
+    case 7: ECG_FLAG(7); break;
+    case 9: ECG_FLAG(9); break;
+    case 11: ECG_FLAG(11); break;
+    case 15: ECG_FLAG(15); break;
+    default: ECG_FLAG(32); break;
+  }
+#undef ECG_FLAG_CFG
+#undef ECG_FLAG
+  ECG_HIP_CHECK(hipGetLastError());
+  const auto t0 = std::chrono::steady_clock::now();
+  for (long it = 0; __atomic_load_n(f.flag_host, __ATOMIC_ACQUIRE) != epoch; ++it) {
+    __builtin_ia32_pause();
+    if ((it & 1023) == 1023 &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2000)) {  // a fault or a stuck queue
+      ECG_HIP_CHECK(hipStreamSynchronize(stream));
+      return __atomic_load_n(f.flag_host, __ATOMIC_ACQUIRE) == epoch ? ecg::kOk : ecg::kHipError;
+    }
+  }
+  return ecg::kOk;
 }
 
 // bf16 activations in/out, fp32 taps and accumulation.

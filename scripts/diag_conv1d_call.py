@@ -62,6 +62,9 @@ def main():
         if hasattr(lib, "conv1d_batch_hip_sync"):
             rows.append(("blocking C call (launch+hipStreamSynchronize)",
                          once(lambda: lib.conv1d_batch_hip_sync(xp, wp, op, B, L, K, raw(0)), sync=False)))
+        rows.append(("flag C call (launch + host-mapped completion word)",
+                     once(lambda: lib.conv1d_batch_hip_flag(xp, wp, op, B, L, K, raw(0)), sync=False)))
+        rows.append(("flag C call + sync", once(lambda: lib.conv1d_batch_hip_flag(xp, wp, op, B, L, K, raw(0)))))
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ks = []
         for _ in range(21):

@@ -69,6 +69,9 @@ for s in $STEPS; do
       for i in 1 2 3 4; do run k20_$i 300 python bench.py --steps 20 --warmup 5 --no-extras; done
       sleep 5
       for i in 5 6; do run k20_$i 300 python bench.py --steps 20 --warmup 5 --no-extras; done ;;
+    flag_tests) run flag_tests 300 python -u -m pytest tests/test_ops_gpu.py -k "flag_call" -x -v -p no:cacheprovider \
+                  --timeout 120 --timeout-method thread ;;
+    flag_ab) for c in 3 4 5 0 3 4 5; do run diag_call_cfg$c 300 env ECG_CONV1D_FLAG_CFG=$c python scripts/diag_conv1d_call.py; done ;;
     op_prof) run op_profile_mt0 300 env ECG_CONV_MT=0 python scripts/resnet_op_profile.py 34 1024
              run op_profile_mt1 300 env ECG_CONV_MT=1 python scripts/resnet_op_profile.py 34 1024 ;;
     mt_tests) run mt_tests 600 python -u -m pytest tests/test_conv_mc_gpu.py -k "stats_multi_tile" \

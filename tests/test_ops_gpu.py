@@ -146,3 +146,25 @@ def test_native_upload_and_prefetch(tmp_path):
     pf.close()
     allx = torch.cat(got).cpu()
     assert torch.equal(allx, torch.from_numpy(data))
+
+
+@pytest.mark.parametrize("B,K", [(64, 3), (256, 7), (512, 5), (300, 15), (33, 4)])
+def test_conv1d_flag_call_matches_torch(B, K):
+    """Blocking single call with the host-mapped completion word (Module-2 time_once path): output equal to
+    F.conv1d after the call returns, over repeated calls (epoch logic) and interleaved with other stream work;
+    K=4 (no compile-time variant) takes the launch + hipStreamSynchronize path."""
+    import torch.nn.functional as F
+    from crossscale_ecg.ops import _lib
+    lib = _lib.kernels()
+    raw = torch._C._cuda_getCurrentRawStream
+    torch.manual_seed(B + K)
+    for rep in range(3):
+        x = torch.randn(B, 500, device="cuda")
+        w = torch.randn(K, device="cuda")
+        y = torch.full((B, 500 - K + 1), float("nan"), device="cuda")
+        junk = torch.randn(1024, 1024, device="cuda") @ torch.randn(1024, 1024, device="cuda")  # work ahead of it
+        st = lib.conv1d_batch_hip_flag(x.data_ptr(), w.data_ptr(), y.data_ptr(), B, 500, K, raw(0))
+        assert st == 0
+        ref = F.conv1d(x.unsqueeze(1), w.view(1, 1, K))[:, 0]
+        torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-4)
+        del junk
