@@ -32,7 +32,7 @@ def main(K=20, reps=9):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     from crossscale_ecg.ops import _lib
     raw = _lib._raw_stream
-    rows = {"graph": [], "graph_slowstream": [], "eager": []}
+    rows = {"graph": [], "graph_slowstream": [], "graph_spin": [], "eager": []}
     for r in range(reps):
         for mode in rows:  # interleaved: same box state for all
             tr.use_graph = mode != "eager"
@@ -44,6 +44,9 @@ def main(K=20, reps=9):
             tr.launch_round(K)
             t1 = time.perf_counter()
             e1.record()
+            if mode == "graph_spin":  # poll the end event (no blocking wait), then the synchronize
+                while not e1.query():
+                    pass
             torch.cuda.synchronize()
             t2 = time.perf_counter()
             torch.cuda.synchronize()
