@@ -295,13 +295,20 @@ class ResNetStepEngine:
                 raise RuntimeError("too many fused BatchNorm finalizes")
             return tails_dev.data_ptr() + 304 * (len(tail_blobs) - 1)
 
+        # data-grad epilogues re-derive the BN1 ReLU mask from z1 and BN1's scale/shift instead of reading the stored
+        # activation a1 (bitwise the same mask: the BN_ACT expression repeated; one activation read less per block).
+        # ECG_DGRAD_MASK_FROM_Z=0: read a1.
+        mask_from_z = os.environ.get("ECG_DGRAD_MASK_FROM_Z", "1") != "0"
+
         def conv(x, Lin, Cin, w_ptr, y, Lout, Cout, K, s, p, dil=1, st=None, add=None, add_mask=None, bnb=None,
-                 tail_ptr=0, lane=0):
-            # bnb = (mask, z, mean, rstd, zd, mean_d, rstd_d): BN-backward statistics fused into the epilogue
+                 tail_ptr=0, lane=0, mbn=None):
+            # bnb = (mask, z, mean, rstd, zd, mean_d, rstd_d): BN-backward statistics fused into the epilogue;
+            # mbn = (scale, shift): the mask is relu(z * scale + shift) > 0 (mask operand not read)
             extra = [P(t) if isinstance(t, torch.Tensor) else int(t or 0) for t in (bnb or ())]
             extra += [0] * (7 - len(extra))
+            m_words = [P(mbn[0]), P(mbn[1])] if (mbn is not None and mask_from_z) else [0, 0]
             op("CONV_FWD", P(x), w_ptr, 0, P(y), P(st), P(add), P(add_mask), B, Lin, Cin, Lout, Cout, K, s, p, dil, 0,
-               *extra, tail_ptr, lane=lane)
+               *extra, tail_ptr, *m_words, lane=lane)
 
         def wgrad(dy, x, Lin, Cin, Lout, Cout, K, s, p, weight):
             S = wsplits(B * Lout, Cout, K, Cin)
@@ -406,7 +413,8 @@ class ResNetStepEngine:
             # dgrad conv2 (stride 1, pad 1) -> ReLU-masked grad wrt a1 + BN1 backward statistics
             T1 = self.lib.ecg_conv1d_nlc_fwd_stat_tiles(R, Co)
             conv(dz2, Lo, Co, self._wb[id(blk.conv2)], ga1, Lo, Co, 3, 1, 1, st=stats,
-                 bnb=(a["a1"], a["z1"], b1.mean, b1.rstd, 0, 0, 0), tail_ptr=tail(T1, Co, [fin_bwd_words(b1, R, 1)]))
+                 bnb=(a["a1"], a["z1"], b1.mean, b1.rstd, 0, 0, 0), tail_ptr=tail(T1, Co, [fin_bwd_words(b1, R, 1)]),
+                 mbn=(b1.scale, b1.shift))
             if not use_tail:
                 fin_bwd(b1, T1, R, 1, stats.data_ptr())
             op("BN_BWD_APPLY", 0, P(ga1), 0, P(a["z1"]), P(b1.mean), P(b1.rstd), P(b1.scale), P(b1.c1),

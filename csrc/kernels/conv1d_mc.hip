@@ -52,6 +52,10 @@ struct FwdArgs {
   const __bf16* szd;
   const float* smean_d;
   const float* srstd_d;
+  // Mask from sz (stat_mode 1): when non-null the ReLU mask is bf16(max(fmaf(sz, mscale, mshift), 0)) > 0 - the
+  // exact values the BN_ACT pass stored as smask (conv -> BN -> ReLU), so smask need not be read
+  const float* mscale;
+  const float* mshift;
   const ecg::BnTail* tail;  // BatchNorm finalize fused into this launch's tail (bn_tail.h), or null
 };
 
@@ -116,11 +120,12 @@ struct EpiLane {
 };
 
 struct EpiConst {
-  float bv[8], mu[8], rsd[8], mud[8], rsdd[8];
+  float bv[8], mu[8], rsd[8], mud[8], rsdd[8], msc[8], msh[8];
   float s1[8], s2[8], s3[8];
   template <bool BWD>
   __device__ __forceinline__ void load(const FwdArgs& a, int n) {
     const bool ds = BWD && a.szd != nullptr;
+    const bool mz = BWD && a.mscale != nullptr;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       bv[e] = a.bias ? a.bias[n + e] : 0.f;
@@ -129,6 +134,8 @@ struct EpiConst {
       rsd[e] = BWD ? a.srstd[n + e] : 0.f;
       mud[e] = ds ? a.smean_d[n + e] : 0.f;
       rsdd[e] = ds ? a.srstd_d[n + e] : 0.f;
+      msc[e] = mz ? a.mscale[n + e] : 0.f;
+      msh[e] = mz ? a.mshift[n + e] : 0.f;
     }
   }
 };
@@ -184,7 +191,15 @@ __device__ __forceinline__ void fwd_epi_tile(const FwdArgs& a, f32x4 (&acc)[BM /
             for (int e = 0; e < 8; ++e) v[e] += (float)ad[e];
           }
         }
-        if (bwd && a.smask != nullptr) {
+        bf16x8 zz;
+        if constexpr (bwd) zz = *reinterpret_cast<const bf16x8*>(a.sz + o);
+        if (bwd && a.mscale != nullptr) {  // the mask the BN_ACT pass stored, recomputed from sz
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const __bf16 act = (__bf16)fmaxf(fmaf((float)zz[e], k.msc[e], k.msh[e]), 0.f);
+            v[e] = (float)act > 0.f ? v[e] : 0.f;
+          }
+        } else if (bwd && a.smask != nullptr) {
           const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.smask + o);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = (float)mk[e] > 0.f ? v[e] : 0.f;
@@ -198,7 +213,6 @@ __device__ __forceinline__ void fwd_epi_tile(const FwdArgs& a, f32x4 (&acc)[BM /
         }
         *reinterpret_cast<bf16x8*>(a.y + o) = outv;
         if constexpr (bwd) {
-          const bf16x8 zz = *reinterpret_cast<const bf16x8*>(a.sz + o);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             k.s1[e] += v[e];
@@ -1255,8 +1269,9 @@ inline bool wgrad_big(int Cout, int Cin) { return conv_big() >= 2 && Cout % 256 
 // in_dil > 1 reads x as zero-inserted with that dilation (used for the data-gradient of strided convs).
 // Extended form used by the ResNet step plan: ``stats`` receives [2][ceil(B*Lout/64)][Cout] BN partials;
 // ``add`` (optionally masked by ``add_mask`` > 0) is added to the output before rounding.
-// ``bnb`` (optional, stat_mode 1): {smask, sz, smean, srstd, szd, smean_d, srstd_d} of the BatchNorm whose
-// backward statistics the data-grad epilogue produces ([2 or 3][M tiles][Cout] into ``stats``).
+// ``bnb`` (optional, stat_mode 1): {smask, sz, smean, srstd, szd, smean_d, srstd_d, mscale, mshift} of the
+// BatchNorm whose backward statistics the data-grad epilogue produces ([2 or 3][M tiles][Cout] into ``stats``);
+// mscale / mshift (both or neither) re-derive the ReLU mask from sz instead of reading smask.
 ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bias, void* y, float* stats,
                                   const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
                                   int Kw, int stride, int pad, int in_dil, int relu, const void* const* bnb,
@@ -1264,12 +1279,15 @@ ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bia
   if (!x || !w || !y || B <= 0 || Lin <= 0 || Lout <= 0 || Kw <= 0 || stride <= 0 || in_dil <= 0 || pad < 0)
     return ecg::kBadArg;
   if (Cin % BK != 0 || Cout % 64 != 0 || (add_mask && !add)) return ecg::kBadArg;
-  if (bnb && (!stats || !bnb[1] || !bnb[2] || !bnb[3] || (bnb[4] && (!bnb[5] || !bnb[6])))) return ecg::kBadArg;
+  if (bnb && (!stats || !bnb[1] || !bnb[2] || !bnb[3] || (bnb[4] && (!bnb[5] || !bnb[6])) || (!bnb[7] != !bnb[8])))
+    return ecg::kBadArg;
   if (tail && !stats) return ecg::kBadArg;
   FwdArgs a{static_cast<const __bf16*>(x), static_cast<const __bf16*>(w), bias, static_cast<__bf16*>(y), stats,
             static_cast<const __bf16*>(add), static_cast<const __bf16*>(add_mask),
             B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil, relu, bnb ? 1 : 0};
   if (bnb) {
+    a.mscale = static_cast<const float*>(bnb[7]);
+    a.mshift = static_cast<const float*>(bnb[8]);
     a.smask = static_cast<const __bf16*>(bnb[0]);
     a.sz = static_cast<const __bf16*>(bnb[1]);
     a.smean = static_cast<const float*>(bnb[2]);

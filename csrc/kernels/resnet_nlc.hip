@@ -473,7 +473,7 @@ __global__ __launch_bounds__(TPB) void bn_act_kernel(const __bf16* __restrict__ 
     ldf8(scale + c0, sc);
     ldf8(shift + c0, sh);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) y[i] = zf[i] * sc[i] + sh[i];
+    for (int i = 0; i < 8; ++i) y[i] = fmaf(zf[i], sc[i], sh[i]);  // (the data-grad epilogue's mask re-derives it)
     if (MODE >= 1) {
       float rf[8];
       ld8(res + o, rf);
@@ -883,9 +883,10 @@ int run_op(const int64_t* o, hipStream_t st) {
   const int kind = (int)o[0];
   switch (kind) {
     case OP_CONV_FWD: {  // words 18..24: BN-backward statistics operands (stat_mode 1 when o[19] != 0);
-                         // word 25: fused BatchNorm finalize (ecg::BnTail in device memory) or 0
-      const void* bnb[7] = {P<void>(o[18]), P<void>(o[19]), P<void>(o[20]), P<void>(o[21]),
-                            P<void>(o[22]), P<void>(o[23]), P<void>(o[24])};
+                         // word 25: fused BatchNorm finalize (ecg::BnTail in device memory) or 0;
+                         // words 26, 27: scale / shift that re-derive the ReLU mask from sz (or 0: load smask)
+      const void* bnb[9] = {P<void>(o[18]), P<void>(o[19]), P<void>(o[20]), P<void>(o[21]), P<void>(o[22]),
+                            P<void>(o[23]), P<void>(o[24]), P<void>(o[26]), P<void>(o[27])};
       return ecg_conv1d_nlc_fwd_ex(P<void>(o[1]), P<void>(o[2]), P<float>(o[3]), P<void>(o[4]), P<float>(o[5]),
                                    P<void>(o[6]), P<void>(o[7]), (int)o[8], (int)o[9], (int)o[10], (int)o[11],
                                    (int)o[12], (int)o[13], (int)o[14], (int)o[15], (int)o[16], (int)o[17],

@@ -108,6 +108,24 @@ def test_engine_multi_tile_forward_matches_one_tile(mode):
             assert _rel(b1, b0) < 1e-3, n
 
 
+def test_dgrad_mask_from_z_bitwise(monkeypatch):
+    """The conv2 data-grad epilogue re-derives the BN1 ReLU mask from z1 (relu(z1*scale+shift) as BN_ACT computes
+    it) instead of reading a1: two SGD steps give bit-for-bit the parameters, momentum and BN statistics of the
+    plan that reads a1."""
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("ECG_DGRAD_MASK_FROM_Z", v)
+        m, ref, eng, x, y = _setup(34, B=64, seed=7)
+        eng.step()
+        eng.step()
+        torch.cuda.synchronize()
+        outs.append((eng.flat.clone(), eng.mom.clone(), [b.clone() for b in m.buffers()]))
+        del eng, m, ref
+    (f0, m0, b0), (f1, m1, b1) = outs
+    assert torch.equal(f0, f1) and torch.equal(m0, m1)
+    assert all(torch.equal(a, b) for a, b in zip(b0, b1))
+
+
 @pytest.mark.parametrize("side", ["0", "1"])
 def test_engine_graph_equals_eager_bitwise(side, monkeypatch):
     # side "1": weight gradients on the side stream, the graph is the captured fork-join DAG (forced: by default
