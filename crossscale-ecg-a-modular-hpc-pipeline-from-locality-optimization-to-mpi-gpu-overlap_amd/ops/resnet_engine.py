@@ -232,7 +232,9 @@ class ResNetStepEngine:
             entries.append(struct.pack("<qqqiiii", self.space.offset_of(c.weight), off, total + off, c.out_channels,
                                        c.in_channels, c.kernel_size[0], block0))
             off += n
-            block0 += (n + 255) // 256
+            if c.out_channels % 64 or c.in_channels % 64 or c.kernel_size[0] > 3:
+                raise ValueError("weight prep tiles need channels % 64 == 0 and k <= 3")
+            block0 += (c.out_channels // 64) * (c.in_channels // 64)  # one 64x64 tile per workgroup
         tab = torch.tensor(list(b"".join(entries)), dtype=torch.uint8).to(dev)
         self._keep.append(tab)
         wprep_blocks = block0

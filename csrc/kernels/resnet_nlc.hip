@@ -805,29 +805,57 @@ struct WEntry {
   long src;  // offset (elements) of the fp32 [Cout][Cin][K] weight in the flat buffer
   long wf;   // offset of the bf16 [Cout][K][Cin] copy
   long wb;   // offset of the bf16 [Cin][K][Cout] flipped copy (data-grad)
-  int Cout, Cin, K, block0;
+  int Cout, Cin, K, block0;  // block0: first 64x64 (Cout x Cin) tile of this conv in the launch
 };
+
+// Both bf16 layouts of every conv weight from the fp32 master copy, one 64 (Cout) x 64 (Cin) tile per workgroup:
+// the tile's source rows (64 x Cin-slice x K floats, contiguous per output channel) are read with 16-byte loads,
+// converted once into an LDS image [k][co][ci], and both destinations are written as whole 16-byte runs -
+// [Cout][K][Cin] along ci and the flipped [Cin][K][Cout] along co (the transpose happens in LDS).  (Was one
+// element per thread with two scattered 2-byte stores and a serial entry scan: 46 us per ResNet1D-34 step.)
+constexpr int WP_LD = 64 + 8;  // bf16 per LDS row (16-byte pad: conflict-free column reads)
 
 __global__ __launch_bounds__(TPB) void weight_prep_kernel(const WEntry* __restrict__ tab, int n,
                                                           const float* __restrict__ flat, __bf16* __restrict__ arena) {
   __shared__ int sel;
-  if (threadIdx.x == 0) {
-    int s = 0;
-    for (int i = 1; i < n; ++i)
-      if ((int)blockIdx.x >= tab[i].block0) s = i;
-    sel = s;
+  __shared__ __attribute__((aligned(16))) __bf16 img[3 * 64 * WP_LD];  // [k][co][ci], K <= 3
+  const int tid = threadIdx.x;
+  if (tid < n) {  // every entry checks its own tile range (one pass, no serial scan)
+    const int b0 = tab[tid].block0, b1 = tid + 1 < n ? tab[tid + 1].block0 : 0x7fffffff;
+    if ((int)blockIdx.x >= b0 && (int)blockIdx.x < b1) sel = tid;
   }
   __syncthreads();
   const WEntry e = tab[sel];
-  const long N = (long)e.Cout * e.Cin * e.K;
-  const long i = ((long)blockIdx.x - e.block0) * TPB + threadIdx.x;
-  if (i >= N) return;
-  const int k = (int)(i % e.K);
-  const long r = i / e.K;
-  const int ci = (int)(r % e.Cin), co = (int)(r / e.Cin);
-  const __bf16 v = (__bf16)flat[e.src + i];
-  arena[e.wf + ((long)co * e.K + k) * e.Cin + ci] = v;
-  arena[e.wb + ((long)ci * e.K + (e.K - 1 - k)) * e.Cout + co] = v;
+  const int K = e.K, tci_n = e.Cin / 64;
+  const int t = (int)blockIdx.x - e.block0;
+  const int co0 = (t / tci_n) * 64, ci0 = (t % tci_n) * 64;
+  // source: row co (64 of them) holds 64*K consecutive floats [ci][k] starting at ci0*K
+  const int row_f = 64 * K, row_v = row_f / 4;  // floats / float4 per row (K=1: 16, K=3: 48)
+  for (int v = tid; v < 64 * row_v; v += TPB) {
+    const int co = v / row_v, q = v - co * row_v;
+    const float4 f = *reinterpret_cast<const float4*>(flat + e.src + ((long)(co0 + co) * e.Cin + ci0) * K + 4 * q);
+    const float fv[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int idx = 4 * q + j, ci = idx / K, k = idx - ci * K;
+      img[(k * 64 + co) * WP_LD + ci] = (__bf16)fv[j];
+    }
+  }
+  __syncthreads();
+  // [Cout][K][Cin]: row (co, k) = 64 consecutive ci = 8 runs of 8 bf16
+  for (int v = tid; v < 64 * K * 8; v += TPB) {
+    const int r = v >> 3, j = v & 7, co = r / K, k = r - co * K;
+    const bf16x8 val = *reinterpret_cast<const bf16x8*>(img + (k * 64 + co) * WP_LD + 8 * j);
+    *reinterpret_cast<bf16x8*>(arena + e.wf + ((long)(co0 + co) * K + k) * e.Cin + ci0 + 8 * j) = val;
+  }
+  // [Cin][K][Cout] flipped taps: row (ci, k') = 64 consecutive co, read down an LDS column
+  for (int v = tid; v < 64 * K * 8; v += TPB) {
+    const int r = v >> 3, j = v & 7, ci = r / K, kp = r - ci * K, k = K - 1 - kp;
+    bf16x8 val;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) val[u] = img[(k * 64 + 8 * j + u) * WP_LD + ci];
+    *reinterpret_cast<bf16x8*>(arena + e.wb + ((long)(ci0 + ci) * K + kp) * e.Cout + co0 + 8 * j) = val;
+  }
 }
 
 inline unsigned grid_for(long n, long per_block = TPB, long cap = 8192) {
@@ -1033,6 +1061,7 @@ int run_op(const int64_t* o, hipStream_t st) {
       break;
     }
     case OP_WEIGHT_PREP:
+      if (o[2] < 1 || o[2] > TPB) return ecg::kBadArg;  // one thread per table entry picks the workgroup's conv
       hipLaunchKernelGGL(weight_prep_kernel, dim3((unsigned)o[3]), dim3(TPB), 0, st, P<const WEntry>(o[1]),
                          (int)o[2], P<const float>(o[4]), P<__bf16>(o[5]));
       break;

@@ -108,6 +108,26 @@ def test_engine_multi_tile_forward_matches_one_tile(mode):
             assert _rel(b1, b0) < 1e-3, n
 
 
+def test_weight_prep_layouts():
+    """WEIGHT_PREP (64x64 tiles transposed through LDS) writes, for every conv, bf16(w) as [Cout][K][Cin] and the
+    tap-flipped [Cin][K][Cout] data-grad layout, exactly."""
+    m, ref, eng, x, y = _setup(34, B=16, use_graph=False)
+    eng.forward_backward()
+    torch.cuda.synchronize()
+    base = eng.warena.data_ptr()
+    n = 0
+    for c in m.modules():
+        if isinstance(c, torch.nn.Conv1d) and id(c) in eng._wf:
+            Co, Ci, K = c.weight.shape
+            wf = eng.warena[(eng._wf[id(c)] - base) // 2:][:Co * K * Ci].view(Co, K, Ci)
+            wb = eng.warena[(eng._wb[id(c)] - base) // 2:][:Co * K * Ci].view(Ci, K, Co)
+            wbf = c.weight.detach().to(torch.bfloat16)
+            assert torch.equal(wf, wbf.permute(0, 2, 1)), c
+            assert torch.equal(wb, wbf.flip(2).permute(1, 2, 0)), c
+            n += 1
+    assert n == 35  # ResNet1D-34: 16 blocks x 2 convs + 3 downsample convs (layers 2-4)
+
+
 def test_dgrad_mask_from_z_bitwise(monkeypatch):
     """The conv2 data-grad epilogue re-derives the BN1 ReLU mask from z1 (relu(z1*scale+shift) as BN_ACT computes
     it) instead of reading a1: two SGD steps give bit-for-bit the parameters, momentum and BN statistics of the
