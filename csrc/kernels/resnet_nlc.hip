@@ -22,6 +22,8 @@
 // All reductions have a fixed order: the step is bitwise deterministic for a given batch.
 #include "../include/ecg_common.h"
 
+#include <type_traits>
+
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -59,34 +61,53 @@ __device__ __forceinline__ void ldf8(const float* p, float* f) {
 
 // ------------------------------------------------------------------------------------------------ stem
 // y[b,t,c] = sum_k w[c,k] x[b, t*s + k - p].  Block = STEM_ROWS rows; thread = 8 channels (16-B stores) of one
-// row per pass (8 channel groups x 32 row lanes); BN partials per block.
+// row per pass (8 channel groups x 32 row lanes); BN partials per block.  The block's input taps are staged in
+// LDS first (thread r loads row r's <= 8 taps, all loads in flight together), so the block pays one global round
+// trip instead of one per pass.
 constexpr int STEM_ROWS = 256;
 __global__ __launch_bounds__(TPB) void stem_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                        __bf16* __restrict__ y, float* __restrict__ stats, int B,
                                                        int L, int Lo, int K, int stride, int pad) {
+  static_assert(STEM_ROWS == TPB, "one staging row per thread");
   __shared__ float red[4][2][64];
+  __shared__ __attribute__((aligned(16))) float xs[STEM_ROWS][8];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int cg = tid & 7, rl = tid >> 3, c0 = cg * 8;
+  const long M = (long)B * Lo;
+  {
+    const long m = (long)blockIdx.x * STEM_ROWS + tid;
+    float xv[8];
+    if (m < M) {
+      const int b = (int)(m / Lo), t = (int)(m % Lo);
+      const float* xb = x + (long)b * L;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int u = t * stride + k - pad;
+        xv[k] = (k < K && u >= 0 && u < L) ? xb[min(max(u, 0), L - 1)] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) xv[k] = 0.f;
+    }
+    *reinterpret_cast<float4*>(&xs[tid][0]) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+    *reinterpret_cast<float4*>(&xs[tid][4]) = make_float4(xv[4], xv[5], xv[6], xv[7]);
+  }
   float wk[8][8];
 #pragma unroll
   for (int e = 0; e < 8; ++e)
 #pragma unroll
     for (int k = 0; k < 8; ++k) wk[e][k] = k < K ? w[(c0 + e) * K + k] : 0.f;
-  const long M = (long)B * Lo;
   float s[8], ss[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s[e] = ss[e] = 0.f;
+  __syncthreads();
+#pragma unroll 2
   for (int i = 0; i < STEM_ROWS / 32; ++i) {
-    const long m = (long)blockIdx.x * STEM_ROWS + rl + 32 * i;
+    const int r = rl + 32 * i;
+    const long m = (long)blockIdx.x * STEM_ROWS + r;
     if (m >= M) break;
-    const int b = (int)(m / Lo), t = (int)(m % Lo);
-    const float* xb = x + (long)b * L;
-    float xv[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int u = t * stride + k - pad;
-      xv[k] = (k < K && u >= 0 && u < L) ? xb[u] : 0.f;
-    }
+    const float4 xa = *reinterpret_cast<const float4*>(&xs[r][0]), xb4 = *reinterpret_cast<const float4*>(&xs[r][4]);
+    const float xv[8] = {xa.x, xa.y, xa.z, xa.w, xb4.x, xb4.y, xb4.z, xb4.w};
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
