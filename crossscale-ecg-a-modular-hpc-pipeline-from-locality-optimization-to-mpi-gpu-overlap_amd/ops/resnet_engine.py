@@ -301,6 +301,10 @@ class ResNetStepEngine:
         # activation a1 (bitwise the same mask: the BN_ACT expression repeated; one activation read less per block).
         # ECG_DGRAD_MASK_FROM_Z=0: read a1.
         mask_from_z = os.environ.get("ECG_DGRAD_MASK_FROM_Z", "1") != "0"
+        # BN-backward apply: ECG_BN_APPLY_RPT=2|4 runs several rows per thread at a fixed channel group (per-channel
+        # coefficients loaded once per thread; bitwise the same output) - measured slower than one 8-channel vector
+        # per thread (B=1024: 3.83-3.87 vs 3.79-3.80 ms/step, profiles/r2/resnet_multi_tile/bn_apply_rpt_ab.txt)
+        apply_rpt = int(os.environ.get("ECG_BN_APPLY_RPT", "0"))
 
         def conv(x, Lin, Cin, w_ptr, y, Lout, Cout, K, s, p, dil=1, st=None, add=None, add_mask=None, bnb=None,
                  tail_ptr=0, lane=0, mbn=None):
@@ -410,7 +414,7 @@ class ResNetStepEngine:
                     fin_bwd(bd, T2, R, 2, base)
             op("BN_BWD_APPLY", 1 if bd is not None else 0, P(dzm), 0, P(a["z2"]), P(b2.mean), P(b2.rstd),
                P(b2.scale), P(b2.c1), P(b2.c2), P(dz2), P(a.get("zd")), P(bd.mean) if bd else 0,
-               P(bd.rstd) if bd else 0, P(bd.scale) if bd else 0, P(bd.c2) if bd else 0, P(dzd), R, Co)
+               P(bd.rstd) if bd else 0, P(bd.scale) if bd else 0, P(bd.c2) if bd else 0, P(dzd), R, Co, apply_rpt)
             wgrad(dz2, a["a1"], Lo, Co, Lo, Co, 3, 1, 1, blk.conv2.weight)
             # dgrad conv2 (stride 1, pad 1) -> ReLU-masked grad wrt a1 + BN1 backward statistics
             T1 = self.lib.ecg_conv1d_nlc_fwd_stat_tiles(R, Co)
@@ -420,7 +424,7 @@ class ResNetStepEngine:
             if not use_tail:
                 fin_bwd(b1, T1, R, 1, stats.data_ptr())
             op("BN_BWD_APPLY", 0, P(ga1), 0, P(a["z1"]), P(b1.mean), P(b1.rstd), P(b1.scale), P(b1.c1),
-               P(b1.c2), P(dz1), 0, 0, 0, 0, 0, 0, R, Co)
+               P(b1.c2), P(dz1), 0, 0, 0, 0, 0, 0, R, Co, apply_rpt)
             wgrad(dz1, a["in"], Li, Ci, Lo, Co, 3, s, 1, blk.conv1.weight)
             add = dzm
             if bd is not None:

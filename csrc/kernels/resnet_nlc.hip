@@ -22,6 +22,7 @@
 // All reductions have a fixed order: the step is bitwise deterministic for a given batch.
 #include "../include/ecg_common.h"
 
+#include <algorithm>
 #include <type_traits>
 
 #include <math.h>
@@ -625,6 +626,69 @@ __global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(
   }
 }
 
+// The same apply with RPT rows per thread at a FIXED channel group (c0 = thread % (C/8)): the five per-channel
+// vectors are loaded once per thread instead of once per 8 elements, and every row's loads are issued before
+// the first store.  Element math identical to bn_bwd_apply_kernel (bitwise the same output).
+template <bool DS, int RPT>
+__global__ __launch_bounds__(TPB) void bn_bwd_apply_rows_kernel(
+    const __bf16* __restrict__ gy, const __bf16* __restrict__ msk, const __bf16* __restrict__ z,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ scale,
+    const float* __restrict__ c1, const float* __restrict__ c2, __bf16* __restrict__ out,
+    const __bf16* __restrict__ zd, const float* __restrict__ mean_d, const float* __restrict__ rstd_d,
+    const float* __restrict__ scale_d, const float* __restrict__ c2_d, __bf16* __restrict__ out_d, long R, int C) {
+  const int cg = C / 8;  // divides TPB (host-checked), so a thread's channel group never changes
+  const long gt = (long)blockIdx.x * TPB + threadIdx.x;
+  const int c0 = (int)(gt % cg) * 8;
+  const long lanes = (long)gridDim.x * TPB / cg;  // row lanes
+  float mu[8], rs[8], sc[8], k1[8], k2[8], mud[8], rsd[8], scd[8], k2d[8];
+  ldf8(mean + c0, mu);
+  ldf8(rstd + c0, rs);
+  ldf8(scale + c0, sc);
+  ldf8(c1 + c0, k1);
+  ldf8(c2 + c0, k2);
+  if (DS) {
+    ldf8(mean_d + c0, mud);
+    ldf8(rstd_d + c0, rsd);
+    ldf8(scale_d + c0, scd);
+    ldf8(c2_d + c0, k2d);
+  }
+  for (long r0 = gt / cg; r0 < R; r0 += lanes * RPT) {
+    float g[RPT][8], zf[RPT][8], zdf[RPT][8];
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const long r = r0 + u * lanes;
+      if (r < R) {
+        const long o = r * C + c0;
+        ld8(gy + o, g[u]);
+        if (msk) {
+          float m[8];
+          ld8(msk + o, m);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) g[u][i] = m[i] > 0.f ? g[u][i] : 0.f;
+        }
+        ld8(z + o, zf[u]);
+        if (DS) ld8(zd + o, zdf[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const long r = r0 + u * lanes;
+      if (r < R) {
+        const long o = r * C + c0;
+        float y[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) y[i] = sc[i] * (g[u][i] - k1[i] - (zf[u][i] - mu[i]) * rs[i] * k2[i]);
+        st8(out + o, y);
+        if (DS) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) y[i] = scd[i] * (g[u][i] - k1[i] - (zdf[u][i] - mud[i]) * rsd[i] * k2d[i]);
+          st8(out_d + o, y);
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ head
 // One block per sample: feat = mean_t h[b,t,:]; logits = W feat + bias; CE loss; g = (softmax - onehot)/B;
 // gh[b,t,c] = (W^T g)[c] / Lf.  Stores g, feat and loss/B for the split reduction.
@@ -1024,6 +1088,26 @@ int run_op(const int64_t* o, hipStream_t st) {
       const bool ds = o[1] != 0;
       const long R = o[17];
       const int C = (int)o[18];
+      // word 19: rows per thread of the fixed-channel variant (ops/resnet_engine.py, ECG_BN_APPLY_RPT; 0 = one
+      // vector per thread, the original kernel)
+      const int rpt = (int)o[19];
+      if (rpt > 0 && C % 8 == 0 && TPB % (C / 8) == 0) {
+        const long lanes_needed = (R + rpt - 1) / rpt;  // row lanes so that each thread gets ~rpt rows
+        const dim3 gr((unsigned)std::max(1L, std::min(8192L, (lanes_needed * (C / 8) + TPB - 1) / TPB)));
+#define ECG_APPLY_ROWS(DSV, RP)                                                                                      \
+  hipLaunchKernelGGL((bn_bwd_apply_rows_kernel<DSV, RP>), gr, dim3(TPB), 0, st, P<const __bf16>(o[2]),               \
+                     P<const __bf16>(o[3]), P<const __bf16>(o[4]), P<const float>(o[5]), P<const float>(o[6]),       \
+                     P<const float>(o[7]), P<const float>(o[8]), P<const float>(o[9]), P<__bf16>(o[10]),            \
+                     P<const __bf16>(o[11]), P<const float>(o[12]), P<const float>(o[13]), P<const float>(o[14]),    \
+                     P<const float>(o[15]), P<__bf16>(o[16]), R, C)
+        if (ds) {
+          if (rpt >= 4) ECG_APPLY_ROWS(true, 4); else if (rpt >= 2) ECG_APPLY_ROWS(true, 2); else ECG_APPLY_ROWS(true, 1);
+        } else {
+          if (rpt >= 4) ECG_APPLY_ROWS(false, 4); else if (rpt >= 2) ECG_APPLY_ROWS(false, 2); else ECG_APPLY_ROWS(false, 1);
+        }
+#undef ECG_APPLY_ROWS
+        break;
+      }
       const dim3 g(grid_for(R * C / 8));
       if (!ds)
         hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]),

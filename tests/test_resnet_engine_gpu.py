@@ -128,13 +128,15 @@ def test_weight_prep_layouts():
     assert n == 35  # ResNet1D-34: 16 blocks x 2 convs + 3 downsample convs (layers 2-4)
 
 
-def test_dgrad_mask_from_z_bitwise(monkeypatch):
-    """The conv2 data-grad epilogue re-derives the BN1 ReLU mask from z1 (relu(z1*scale+shift) as BN_ACT computes
-    it) instead of reading a1: two SGD steps give bit-for-bit the parameters, momentum and BN statistics of the
-    plan that reads a1."""
+@pytest.mark.parametrize("knob,values", [("ECG_DGRAD_MASK_FROM_Z", ("0", "1")), ("ECG_BN_APPLY_RPT", ("0", "4"))])
+def test_plan_variants_bitwise(knob, values, monkeypatch):
+    """Plan variants that must not change a bit: the conv2 data-grad epilogue re-deriving the BN1 ReLU mask from z1
+    (relu(z1*scale+shift) as BN_ACT computes it) instead of reading a1; the BN-backward apply with several rows per
+    thread at a fixed channel group.  Two SGD steps give bit-for-bit the same parameters, momentum and BN
+    statistics either way."""
     outs = []
-    for v in ("0", "1"):
-        monkeypatch.setenv("ECG_DGRAD_MASK_FROM_Z", v)
+    for v in values:
+        monkeypatch.setenv(knob, v)
         m, ref, eng, x, y = _setup(34, B=64, seed=7)
         eng.step()
         eng.step()
