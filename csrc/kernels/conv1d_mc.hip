@@ -528,10 +528,15 @@ __global__ __launch_bounds__(128 * NWR, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_d
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // stage kt landed for every wave; every wave is past mma(kt - 1)
+      // stage kt landed for every wave; every wave is past mma(kt - 1).  A raw barrier: __syncthreads() would
+      // emit vmcnt(0) and drain stage kt+1's DMA, which must stay in flight across it (guide: "Pipelining across
+      // barriers"); the ds_reads of mma(kt - 1) retired with lgkmcnt(0)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
       if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);  // into the buffer mma(kt - 1) read
       mma(kt % 3);
     }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();  // the epilogue reuses the stage buffers
   }
   fwd_epilogue<BM, BN, EPI, NWR>(a, acc, smem, m0, n0, mt, MT, a.Lout, M, 1, 0);
