@@ -188,3 +188,29 @@ def test_host_barrier_shm(world):
         assert kind == "shm"
         assert first_leave >= last_arrival
         assert per_call_us < 5000  # 1000 calls: < 5 ms each even on an oversubscribed CI box
+
+
+def case_host_barrier_timeout(ctx):
+    import time
+    from crossscale_ecg.parallel.host_barrier import HostBarrier
+    os.environ["LOCAL_WORLD_SIZE"] = str(ctx.world_size)
+    b = HostBarrier(ctx, timeout_s=1.0)
+    assert b.kind == "shm"
+    b()  # both meet once
+    err = None
+    if ctx.rank == 0:  # rank 1 never arrives at the second generation: rank 0 must give up, not hang
+        t0 = time.time()
+        try:
+            b()
+        except RuntimeError as e:
+            err = (str(e)[:40], time.time() - t0)
+    dist.barrier()  # (gloo) both ranks done before the segment is closed
+    b.close()
+    return err
+
+
+def test_host_barrier_timeout():
+    out = _run(2, "case_host_barrier_timeout")
+    msg, waited = out[0]
+    assert "host barrier failed" in msg and 0.9 < waited < 30
+    assert out[1] is None
