@@ -185,7 +185,8 @@ class ResNetStepEngine:
         max_T = max((B * Lz + 63) // 64, max((B * a[2] + 63) // 64 for a in shapes))
         stats = self._t(2 * max_T * 512, dtype=torch.float32)
         chunk_for = lambda C: (256 // (C // 8)) * 16  # noqa: E731  rows per reduce block
-        max_Tb = max((B * Lz + chunk_for(64) - 1) // chunk_for(64),
+        stem_chunk_b = 128  # rows per block of the stem backward (more, shorter blocks than chunk_for(64))
+        max_Tb = max((B * Lz + stem_chunk_b - 1) // stem_chunk_b,
                      max((B * a[2] + chunk_for(a[3]) - 1) // chunk_for(a[3]) for a in shapes))
         bpart = self._t(3 * max_Tb * 512, dtype=torch.float32)
         fin_scratch = self._t(1024 * 2 * 512, dtype=torch.float64)
@@ -329,8 +330,10 @@ class ResNetStepEngine:
         op("WEIGHT_PREP", P(tab), len(convs), wprep_blocks, P(self.flat), P(self.warena))
         sr = self.lib.ecg_plan_stem_rows()
         T0 = (B * Lz + sr - 1) // sr
-        op("STEM_FWD", P(self.x), P(c0.weight), P(self.z0), P(stats), B, L, Lz, Ks, Ss, Ps)
-        fin_fwd(bn0, T0, B * Lz)
+        op("STEM_FWD", P(self.x), P(c0.weight), P(self.z0), P(stats), B, L, Lz, Ks, Ss, Ps,
+           tail(T0, 64, [fin_fwd_words(bn0, B * Lz)]))
+        if not use_tail:
+            fin_fwd(bn0, T0, B * Lz)
         op("STEM_POOL", P(self.z0), P(bn0.scale), P(bn0.shift), P(self.h0), B, Lz, Lp, 64)
         xin = self.h0
         # side lane (with fused finalizes): a block's downsample conv runs beside conv1 -> BN_ACT -> conv2, on BN
@@ -403,10 +406,11 @@ class ResNetStepEngine:
             if bn2_src is None:  # last block: gradient from the head
                 ch = chunk_for(Co)
                 Tb = (R + ch - 1) // ch
+                fins = [fin_bwd_words(b2, R, 1)] + ([fin_bwd_words(bd, R, 2)] if bd is not None else [])
                 op("BN_BWD_REDUCE", 3 if bd is not None else 2, P(gcur), P(a["out"]), P(a["z2"]), P(b2.mean),
                    P(b2.rstd), P(a.get("zd")), P(bd.mean) if bd else 0, P(bd.rstd) if bd else 0, P(bpart), R, Co, ch,
-                   P(dzm))
-                bn2_src = (bpart.data_ptr(), Tb, False)
+                   P(dzm), tail(Tb, Co, fins))
+                bn2_src = (bpart.data_ptr(), Tb, use_tail)
             base, T2, fused = bn2_src
             if not fused:  # (fused: the data-grad conv that produced the statistics already finalized them)
                 fin_bwd(b2, T2, R, 1, base)
@@ -453,10 +457,11 @@ class ResNetStepEngine:
                 seg_begin, seg_hi = len(ops), lo
 
         # =============================== stem backward
-        Tb0 = (B * Lz + chunk_for(64) - 1) // chunk_for(64)
+        Tb0 = (B * Lz + stem_chunk_b - 1) // stem_chunk_b
         op("STEM_BWD_REDUCE", P(gcur), P(self.z0), P(bn0.scale), P(bn0.shift), P(bn0.mean), P(bn0.rstd), P(dz0),
-           P(bpart), B, Lz, Lp, 64, chunk_for(64))
-        fin_bwd(bn0, Tb0, B * Lz, 1)
+           P(bpart), B, Lz, Lp, 64, stem_chunk_b, tail(Tb0, 64, [fin_bwd_words(bn0, B * Lz, 1)]))
+        if not use_tail:
+            fin_bwd(bn0, Tb0, B * Lz, 1)
         op("STEM_WGRAD", P(dz0), P(self.z0), P(bn0.mean), P(bn0.rstd), P(bn0.scale), P(bn0.c1), P(bn0.c2),
            P(self.x), P(ws), B, L, Lz, Ks, Ss, Ps, stem_chunk)
         op("REDUCE_SUM", P(ws), stem_blocks, 64 * Ks, self._gptr(c0.weight), 64 * Ks, 0)

@@ -22,6 +22,8 @@
 // All reductions have a fixed order: the step is bitwise deterministic for a given batch.
 #include "../include/ecg_common.h"
 
+#include "../include/bn_tail.h"
+
 #include <algorithm>
 #include <type_traits>
 
@@ -68,7 +70,8 @@ __device__ __forceinline__ void ldf8(const float* p, float* f) {
 constexpr int STEM_ROWS = 256;
 __global__ __launch_bounds__(TPB) void stem_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                        __bf16* __restrict__ y, float* __restrict__ stats, int B,
-                                                       int L, int Lo, int K, int stride, int pad) {
+                                                       int L, int Lo, int K, int stride, int pad,
+                                                       const ecg::BnTail* __restrict__ tail) {  // fused BN finalize
   static_assert(STEM_ROWS == TPB, "one staging row per thread");
   __shared__ float red[4][2][64];
   __shared__ __attribute__((aligned(16))) float xs[STEM_ROWS][8];
@@ -138,8 +141,14 @@ __global__ __launch_bounds__(TPB) void stem_fwd_kernel(const float* __restrict__
   __syncthreads();
   if (tid < 128) {
     const int st = tid >> 6, c = tid & 63;
-    stats[((long)st * gridDim.x + blockIdx.x) * 64 + c] = red[0][st][c] + red[1][st][c] + red[2][st][c] + red[3][st][c];
+    const float v = red[0][st][c] + red[1][st][c] + red[2][st][c] + red[3][st][c];
+    if (tail)
+      ecg::st_sc1(&stats[((long)st * gridDim.x + blockIdx.x) * 64 + c], v);  // handed to the tail's last arriver
+    else
+      stats[((long)st * gridDim.x + blockIdx.x) * 64 + c] = v;
   }
+  if (tail)  // the staging rows are dead: 8 KB of LDS for the tail's scratch
+    ecg::bn_tail<TPB>(tail, stats, 2, gridDim.x, 64, blockIdx.x, 0, 64, reinterpret_cast<unsigned char*>(&xs[0][0]));
 }
 
 // out[b,o,c] = max_{j in {2o-1,2o,2o+1}} relu(z[b,j,c]*scale[c] + shift[c])   (MaxPool1d(3, 2, 1))
@@ -175,8 +184,9 @@ __global__ __launch_bounds__(TPB) void stem_pool_kernel(const __bf16* __restrict
 __global__ __launch_bounds__(TPB) void stem_bwd_reduce_kernel(
     const __bf16* __restrict__ gp, const __bf16* __restrict__ z, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ mean, const float* __restrict__ rstd,
-    __bf16* __restrict__ dz, float* __restrict__ part, int B, int Lz, int Lp, int C, int chunk) {
-  __shared__ float red[TPB * 16];
+    __bf16* __restrict__ dz, float* __restrict__ part, int B, int Lz, int Lp, int C, int chunk,
+    const ecg::BnTail* __restrict__ tail) {  // tail: the stem BatchNorm's backward finalize fused here, or null
+  __shared__ __attribute__((aligned(16))) float red[TPB * 16];
   const int cg = C / 8, tid = threadIdx.x;
   const int rpp = TPB / cg, roff = tid / cg, c0 = (tid % cg) * 8;
   const bool active = roff < rpp;  // C/8 need not divide the block: spare threads idle
@@ -192,34 +202,45 @@ __global__ __launch_bounds__(TPB) void stem_bwd_reduce_kernel(
   for (long r = (long)blockIdx.x * chunk + roff; r < r1; r += rpp) {
     const int b = (int)(r / Lz), j = (int)(r % Lz);
     const __bf16* zb = z + (long)b * Lz * C + c0;
-    float zj[8], g[8];
-    ld8(zb + (long)j * C, zj);
+    // the windows containing j are o0 = j>>1 and o1 = (j+1)>>1 (equal for even j); together they cover the rows
+    // p0 .. p0+4, p0 = 2*o0 - 1.  All seven loads (five z rows, two gradient rows) are issued unconditionally from
+    // clamped addresses, so they are in flight together; validity is applied to the values.
+    const int o0 = j >> 1, o1 = (j + 1) >> 1, p0 = 2 * o0 - 1;
+    const bool has1 = o1 != o0 && o1 < Lp;
+    float zq[5][8], g0[8], g1[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) g[i] = 0.f;
-    const int olo = j >> 1, ohi = min(Lp - 1, (j + 1) >> 1);  // windows containing j
-    for (int o = olo; o <= ohi; ++o) {
-      float best[8];
-      int arg[8];
+    for (int u = 0; u < 5; ++u) ld8(zb + (long)min(max(p0 + u, 0), Lz - 1) * C, zq[u]);
+    ld8(gp + ((long)b * Lp + o0) * C + c0, g0);
+    ld8(gp + ((long)b * Lp + min(o1, Lp - 1)) * C + c0, g1);
+    float g[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) { best[i] = -INFINITY; arg[i] = -1; }
+    for (int i = 0; i < 8; ++i) {
+      // window o0: rows p0, p0+1, p0+2 (first maximum wins, out-of-range rows skipped)
+      float best = -INFINITY;
+      int arg = -1;
 #pragma unroll
-      for (int d = -1; d <= 1; ++d) {
-        const int p = 2 * o + d;
-        if (p < 0 || p >= Lz) continue;
-        float zp[8];
-        ld8(zb + (long)p * C, zp);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float av = fmaxf(zp[i] * sc[i] + sh[i], 0.f);
-          if (av > best[i]) { best[i] = av; arg[i] = p; }
-        }
+      for (int d = 0; d < 3; ++d) {
+        const int p = p0 + d;
+        const float av = fmaxf(zq[d][i] * sc[i] + sh[i], 0.f);
+        if (p >= 0 && p < Lz && av > best) { best = av; arg = p; }
       }
-      float go[8];
-      ld8(gp + ((long)b * Lp + o) * C + c0, go);
+      float gi = arg == j ? g0[i] : 0.f;
+      if (has1) {  // window o1 = o0 + 1: rows p0+2 .. p0+4
+        float best1 = -INFINITY;
+        int arg1 = -1;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (arg[i] == j) g[i] += go[i];
+        for (int d = 2; d < 5; ++d) {
+          const int p = p0 + d;
+          const float av = fmaxf(zq[d][i] * sc[i] + sh[i], 0.f);
+          if (p >= 0 && p < Lz && av > best1) { best1 = av; arg1 = p; }
+        }
+        if (arg1 == j) gi += g1[i];
+      }
+      g[i] = gi;
     }
+    float zj[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) zj[i] = (j & 1) ? zq[2][i] : zq[1][i];  // row j = p0 + 1 + (j & 1)
     float d[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -248,8 +269,12 @@ __global__ __launch_bounds__(TPB) void stem_bwd_reduce_kernel(
     const int st = idx / C, c = idx % C;
     float v = 0.f;
     for (int q = 0; q < rpp; ++q) v += red[(q * 2 + st) * C + c];
-    part[((long)st * T + blockIdx.x) * C + c] = v;
+    if (tail)
+      ecg::st_sc1(&part[((long)st * T + blockIdx.x) * C + c], v);  // handed to the tail's last arriver
+    else
+      part[((long)st * T + blockIdx.x) * C + c] = v;
   }
+  if (tail) ecg::bn_tail<TPB>(tail, part, 2, T, C, blockIdx.x, 0, C, reinterpret_cast<unsigned char*>(red));
 }
 
 // dW[c,k] partials: sum over rows of dzz[b,j,c] * x[b, j*s + k - p], dzz = scale*(dz - c1 - xhat*c2).
@@ -521,8 +546,8 @@ __global__ __launch_bounds__(TPB) void bn_bwd_reduce_kernel(
     const __bf16* __restrict__ gy, const __bf16* __restrict__ msk, const __bf16* __restrict__ z,
     const float* __restrict__ mean, const float* __restrict__ rstd, const __bf16* __restrict__ zd,
     const float* __restrict__ mean_d, const float* __restrict__ rstd_d, float* __restrict__ part, long R, int C,
-    int chunk, __bf16* __restrict__ dzm) {
-  __shared__ float red[TPB * 8 * 3];
+    int chunk, __bf16* __restrict__ dzm, const ecg::BnTail* __restrict__ tail) {  // tail: fused finalize(s) or null
+  __shared__ __attribute__((aligned(16))) float red[TPB * 8 * 3];
   const int cg = C / 8, tid = threadIdx.x;
   const int rpp = TPB / cg, roff = tid / cg, c0 = (tid % cg) * 8;
   const bool active = roff < rpp;
@@ -576,7 +601,16 @@ __global__ __launch_bounds__(TPB) void bn_bwd_reduce_kernel(
     const int st = idx / C, c = idx % C;
     float v = 0.f;
     for (int q = 0; q < rpp; ++q) v += red[(q * NS + st) * C + c];
-    part[((long)st * T + blockIdx.x) * C + c] = v;
+    if (tail)
+      ecg::st_sc1(&part[((long)st * T + blockIdx.x) * C + c], v);  // handed to the tail's last arriver
+    else
+      part[((long)st * T + blockIdx.x) * C + c] = v;
+  }
+  if (tail) {  // every column block of C (64 wide) is finalized by this launch's tail
+    for (int n0 = 0; n0 < C; n0 += 256) {
+      const int bn = C - n0 < 256 ? C - n0 : 256;
+      ecg::bn_tail<TPB>(tail, part, NS, T, C, blockIdx.x, n0, bn, reinterpret_cast<unsigned char*>(red));
+    }
   }
 }
 
@@ -1071,17 +1105,17 @@ int run_op(const int64_t* o, hipStream_t st) {
       const int ns = (int)o[1];
       const long R = o[11];
       const int C = (int)o[12], chunk = (int)o[13];
-      if (C % 8 || C > 8 * TPB || chunk <= 0) return ecg::kBadArg;
+      if (C % 8 || C > 8 * TPB || chunk <= 0 || (o[15] && C % 64)) return ecg::kBadArg;
       const dim3 g((unsigned)((R + chunk - 1) / chunk));
       if (ns == 2)
         hipLaunchKernelGGL(bn_bwd_reduce_kernel<2>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]), P<const __bf16>(o[3]),
                            P<const __bf16>(o[4]), P<const float>(o[5]), P<const float>(o[6]), nullptr, nullptr,
-                           nullptr, P<float>(o[10]), R, C, chunk, P<__bf16>(o[14]));
+                           nullptr, P<float>(o[10]), R, C, chunk, P<__bf16>(o[14]), P<const ecg::BnTail>(o[15]));
       else
         hipLaunchKernelGGL(bn_bwd_reduce_kernel<3>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]), P<const __bf16>(o[3]),
                            P<const __bf16>(o[4]), P<const float>(o[5]), P<const float>(o[6]), P<const __bf16>(o[7]),
                            P<const float>(o[8]), P<const float>(o[9]), P<float>(o[10]), R, C, chunk,
-                           P<__bf16>(o[14]));
+                           P<__bf16>(o[14]), P<const ecg::BnTail>(o[15]));
       break;
     }
     case OP_BN_BWD_APPLY: {
@@ -1128,7 +1162,8 @@ int run_op(const int64_t* o, hipStream_t st) {
       const long M = (long)B * Lo;
       hipLaunchKernelGGL(stem_fwd_kernel, dim3((unsigned)((M + STEM_ROWS - 1) / STEM_ROWS)), dim3(TPB), 0, st,
                          P<const float>(o[1]),
-                         P<const float>(o[2]), P<__bf16>(o[3]), P<float>(o[4]), B, L, Lo, K, (int)o[9], (int)o[10]);
+                         P<const float>(o[2]), P<__bf16>(o[3]), P<float>(o[4]), B, L, Lo, K, (int)o[9], (int)o[10],
+                         P<const ecg::BnTail>(o[11]));
       break;
     }
     case OP_STEM_POOL: {
@@ -1140,12 +1175,12 @@ int run_op(const int64_t* o, hipStream_t st) {
     }
     case OP_STEM_BWD_REDUCE: {
       const int B = (int)o[9], Lz = (int)o[10], Lp = (int)o[11], C = (int)o[12], chunk = (int)o[13];
-      if (C % 8 || 2 * C * (TPB / (C / 8)) > TPB * 16) return ecg::kBadArg;
+      if (C % 8 || 2 * C * (TPB / (C / 8)) > TPB * 16 || (o[14] && (C % 64 || C > 256))) return ecg::kBadArg;
       const long R = (long)B * Lz;
       hipLaunchKernelGGL(stem_bwd_reduce_kernel, dim3((unsigned)((R + chunk - 1) / chunk)), dim3(TPB), 0, st,
                          P<const __bf16>(o[1]), P<const __bf16>(o[2]), P<const float>(o[3]), P<const float>(o[4]),
                          P<const float>(o[5]), P<const float>(o[6]), P<__bf16>(o[7]), P<float>(o[8]), B, Lz, Lp, C,
-                         chunk);
+                         chunk, P<const ecg::BnTail>(o[14]));
       break;
     }
     case OP_STEM_WGRAD: {
