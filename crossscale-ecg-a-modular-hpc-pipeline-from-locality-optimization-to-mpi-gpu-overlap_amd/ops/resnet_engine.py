@@ -52,6 +52,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_tiles", [i32, i32, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_target_wgs", [i32, i32, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles_ex", [i32, i32, i32, i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles_fold", [ctypes.c_long, i32])
     lib._plan_bound = True
     if lib.ecg_plan_op_words() != OP_WORDS or lib.ecg_plan_wentry_bytes() != 40:
         raise _lib.NativeError("resnet plan ABI mismatch (rebuild csrc)")
@@ -307,15 +308,24 @@ class ResNetStepEngine:
         # per thread (B=1024: 3.83-3.87 vs 3.79-3.80 ms/step, profiles/r2/resnet_multi_tile/bn_apply_rpt_ab.txt)
         apply_rpt = int(os.environ.get("ECG_BN_APPLY_RPT", "0"))
 
+        # BN1 + ReLU folded into conv2's A-operand load (register-staged loop): conv2 reads z1 and stages exactly the
+        # a1 values BN_ACT would write; BN_ACT itself moves to the side lane (a1 is read only by the side-lane
+        # weight gradient, the data-grad mask being re-derived from z1).  ECG_BN_FOLD=1: stages with >= 128
+        # channels (the 64-channel stage keeps its multi-tile LDS-DMA conv), 2: every stage, 0 (default): off -
+        # measured slower (B=1024: 3.85 vs 3.755 ms/step, profiles/r2/resnet_multi_tile/bn_fold_ab.txt): the
+        # register-staged loop the fold needs is slower than the LDS-DMA loop by more than the BN_ACT pass costs.
+        bn_fold = int(os.environ.get("ECG_BN_FOLD", "0")) if (mask_from_z and side) else 0
+
         def conv(x, Lin, Cin, w_ptr, y, Lout, Cout, K, s, p, dil=1, st=None, add=None, add_mask=None, bnb=None,
-                 tail_ptr=0, lane=0, mbn=None):
+                 tail_ptr=0, lane=0, mbn=None, afold=None):
             # bnb = (mask, z, mean, rstd, zd, mean_d, rstd_d): BN-backward statistics fused into the epilogue;
             # mbn = (scale, shift): the mask is relu(z * scale + shift) > 0 (mask operand not read)
             extra = [P(t) if isinstance(t, torch.Tensor) else int(t or 0) for t in (bnb or ())]
             extra += [0] * (7 - len(extra))
             m_words = [P(mbn[0]), P(mbn[1])] if (mbn is not None and mask_from_z) else [0, 0]
+            f_words = [P(afold[0]), P(afold[1])] if afold is not None else [0, 0]
             op("CONV_FWD", P(x), w_ptr, 0, P(y), P(st), P(add), P(add_mask), B, Lin, Cin, Lout, Cout, K, s, p, dil, 0,
-               *extra, tail_ptr, *m_words, lane=lane)
+               *extra, tail_ptr, *m_words, *f_words, lane=lane)
 
         def wgrad(dy, x, Lin, Cin, Lout, Cout, K, s, p, weight):
             S = wsplits(B * Lout, Cout, K, Cin)
@@ -349,11 +359,13 @@ class ResNetStepEngine:
                  tail_ptr=tail(T, Co, [fin_fwd_words(b1, B * Lo)]))
             if not use_tail:
                 fin_fwd(b1, T, B * Lo)
-            op("BN_ACT", 0, P(a["z1"]), P(b1.scale), P(b1.shift), 0, 0, 0, P(a["a1"]), B * Lo, Co)
-            conv(a["a1"], Lo, Co, self._wf[id(blk.conv2)], a["z2"], Lo, Co, 3, 1, 1, st=stats,
-                 tail_ptr=tail(T, Co, [fin_fwd_words(b2, B * Lo)]))
+            fold = bn_fold == 2 or (bn_fold == 1 and Co >= 128)
+            op("BN_ACT", 0, P(a["z1"]), P(b1.scale), P(b1.shift), 0, 0, 0, P(a["a1"]), B * Lo, Co, lane=1 if fold else 0)
+            T2 = self.lib.ecg_conv1d_nlc_fwd_stat_tiles_fold(B * Lo, Co) if fold else T
+            conv(a["z1"] if fold else a["a1"], Lo, Co, self._wf[id(blk.conv2)], a["z2"], Lo, Co, 3, 1, 1, st=stats,
+                 tail_ptr=tail(T2, Co, [fin_fwd_words(b2, B * Lo)]), afold=(b1.scale, b1.shift) if fold else None)
             if not use_tail:
-                fin_fwd(b2, T, B * Lo)
+                fin_fwd(b2, T2, B * Lo)
             if bd is not None:
                 if not ds_side:
                     conv(xin, Li, Ci, self._wf[id(blk.downsample[0])], a["zd"], Lo, Co, 1, s, 0, st=stats,

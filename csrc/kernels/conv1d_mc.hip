@@ -56,6 +56,11 @@ struct FwdArgs {
   // exact values the BN_ACT pass stored as smask (conv -> BN -> ReLU), so smask need not be read
   const float* mscale;
   const float* mshift;
+  // A-operand transform (register-staged forward only): when non-null the staged activation is
+  // bf16(max(fmaf(x, ascale[c], ashift[c]), 0)) - a BatchNorm + ReLU folded into the consumer conv's operand load
+  // (padding rows stay zero)
+  const float* ascale;
+  const float* ashift;
   const ecg::BnTail* tail;  // BatchNorm finalize fused into this launch's tail (bn_tail.h), or null
 };
 
@@ -337,10 +342,14 @@ __global__ __launch_bounds__(THREADS, NBUF == 1 ? 3 : 2) void conv1d_nlc_fwd_ker
   }
   const __bf16* wb = a.w + (long)(n0 + (tid >> 3)) * (a.Kw * a.Cin) + (tid & 7) * 8;
   const int Lext = a.in_dil > 1 ? (a.Lin - 1) * a.in_dil + 1 : a.Lin;  // extent of the (dilated) input
+  const bool fold = a.ascale != nullptr;  // block-uniform
+  unsigned aok = 0u;  // rows of the staged A set that are real input rows (fold: padding stays zero)
+  float4 asc0, asc1, ash0, ash1;  // the staged set's 8 channels' BN scale / shift (fold)
   auto ld_set = [&](uint4* ra, uint4* rb, int t) {
     const int tc = t < nk ? t : nk - 1;
     const int k = k0 + (tc / CB) * P, c0 = (tc % CB) * BK;
     const int kk = k * a.Cin + c0;
+    aok = 0u;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       int u = apos[i] + k;
@@ -349,15 +358,37 @@ __global__ __launch_bounds__(THREADS, NBUF == 1 ? 3 : 2) void conv1d_nlc_fwd_ker
         ok = ok && (u % a.in_dil == 0);
         u /= a.in_dil;
       }
+      aok |= (ok ? 1u : 0u) << i;
       ra[i] = ok ? *reinterpret_cast<const uint4*>(a.x + abase[i] + (long)u * a.Cin + c0) : make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (fold) {  // (every A piece of this thread covers channels c0 + (tid & 7) * 8 .. + 8)
+      const float4* sp = reinterpret_cast<const float4*>(a.ascale + c0 + (tid & 7) * 8);
+      const float4* hp = reinterpret_cast<const float4*>(a.ashift + c0 + (tid & 7) * 8);
+      asc0 = sp[0];
+      asc1 = sp[1];
+      ash0 = hp[0];
+      ash1 = hp[1];
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i)
       rb[i] = *reinterpret_cast<const uint4*>(wb + (long)i * (THREADS / 8) * (a.Kw * a.Cin) + kk);
   };
   auto st_set = [&](__bf16* base, const uint4* ra, const uint4* rb) {
+    if (fold) {
+      const float sc[8] = {asc0.x, asc0.y, asc0.z, asc0.w, asc1.x, asc1.y, asc1.z, asc1.w};
+      const float sh[8] = {ash0.x, ash0.y, ash0.z, ash0.w, ash1.x, ash1.y, ash1.z, ash1.w};
 #pragma unroll
-    for (int i = 0; i < NA; ++i) store_one(base, tid + i * THREADS, ra[i]);
+      for (int i = 0; i < NA; ++i) {
+        bf16x8 v = __builtin_bit_cast(bf16x8, ra[i]);
+        const bool ok = (aok >> i) & 1u;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = ok ? (__bf16)fmaxf(fmaf((float)v[e], sc[e], sh[e]), 0.f) : (__bf16)0.f;
+        store_one(base, tid + i * THREADS, __builtin_bit_cast(uint4, v));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) store_one(base, tid + i * THREADS, ra[i]);
+    }
 #pragma unroll
     for (int i = 0; i < NB; ++i) store_one(base + Cfg::A_EL, tid + i * THREADS, rb[i]);
   };
@@ -1277,10 +1308,46 @@ inline bool wgrad_big(int Cout, int Cin) { return conv_big() >= 2 && Cout % 256 
 // ``bnb`` (optional, stat_mode 1): {smask, sz, smean, srstd, szd, smean_d, srstd_d, mscale, mshift} of the
 // BatchNorm whose backward statistics the data-grad epilogue produces ([2 or 3][M tiles][Cout] into ``stats``);
 // mscale / mshift (both or neither) re-derive the ReLU mask from sz instead of reading smask.
+// Register-staged launch for a forward conv with the A-operand BN+ReLU fold (fold_scale/shift): the tile family
+// the picker gives a dilated input (no LDS-DMA, no 256-row tiles, no multi-tile workgroups).
+namespace {
+int launch_fwd_fold(const FwdArgs& a, hipStream_t stream) {
+  int bm, bn;
+  pick_fwd_tile((long)a.B * a.Lout, a.Cout, 2, &bm, &bn);
+  const bool nb2 = conv_nbuf() == 2;
+#define ECG_FOLD(BM_, BN_)                                                                                     \
+  return a.stat_mode == 1 ? (nb2 ? launch_fwd_cfg<BM_, BN_, 1, 2>(a, stream) : launch_fwd_cfg<BM_, BN_, 1, 1>(a, stream)) \
+                          : (nb2 ? launch_fwd_cfg<BM_, BN_, 0, 2>(a, stream) : launch_fwd_cfg<BM_, BN_, 0, 1>(a, stream))
+  if (bm == 128 && bn == 128) ECG_FOLD(128, 128);
+  if (bm == 128) ECG_FOLD(128, 64);
+  ECG_FOLD(64, 64);
+#undef ECG_FOLD
+}
+}  // namespace
+
+ECG_API int ecg_conv1d_nlc_fwd_ex2(const void* x, const void* w, const float* bias, void* y, float* stats,
+                                   const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
+                                   int Kw, int stride, int pad, int in_dil, int relu, const void* const* bnb,
+                                   const void* tail, const float* fold_scale, const float* fold_shift,
+                                   hipStream_t stream);
+
 ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bias, void* y, float* stats,
                                   const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
                                   int Kw, int stride, int pad, int in_dil, int relu, const void* const* bnb,
                                   const void* tail, hipStream_t stream) {
+  return ecg_conv1d_nlc_fwd_ex2(x, w, bias, y, stats, add, add_mask, B, Lin, Cin, Lout, Cout, Kw, stride, pad,
+                                in_dil, relu, bnb, tail, nullptr, nullptr, stream);
+}
+
+// ecg_conv1d_nlc_fwd_ex plus the A-operand fold: with fold_scale / fold_shift (both or neither; in_dil == 1) the
+// conv reads x = z and stages bf16(max(z * fold_scale[c] + fold_shift[c], 0)) - the BN_ACT output it replaces,
+// bitwise - on the register-staged loop.  Its BatchNorm partial rows: ecg_conv1d_nlc_fwd_stat_tiles_fold.
+ECG_API int ecg_conv1d_nlc_fwd_ex2(const void* x, const void* w, const float* bias, void* y, float* stats,
+                                   const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
+                                   int Kw, int stride, int pad, int in_dil, int relu, const void* const* bnb,
+                                   const void* tail, const float* fold_scale, const float* fold_shift,
+                                   hipStream_t stream) {
+  if (!fold_scale != !fold_shift || (fold_scale && in_dil != 1)) return ecg::kBadArg;
   if (!x || !w || !y || B <= 0 || Lin <= 0 || Lout <= 0 || Kw <= 0 || stride <= 0 || in_dil <= 0 || pad < 0)
     return ecg::kBadArg;
   if (Cin % BK != 0 || Cout % 64 != 0 || (add_mask && !add)) return ecg::kBadArg;
@@ -1302,6 +1369,9 @@ ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bia
     a.srstd_d = static_cast<const float*>(bnb[6]);
   }
   a.tail = static_cast<const ecg::BnTail*>(tail);
+  a.ascale = fold_scale;
+  a.ashift = fold_shift;
+  if (fold_scale) return launch_fwd_fold(a, stream);
   int bm, bn;
   pick_fwd_tile((long)B * Lout, Cout, in_dil, &bm, &bn);
   if (bm == 256 && bn == 256) return launch_fwd<256, 256>(a, stream);
@@ -1332,6 +1402,13 @@ ECG_API int ecg_conv1d_nlc_fwd_stat_tiles(long M, int Cout) {
   pick_fwd_tile(M, Cout, 1, &bm, &bn);
   const int gm = fwd_mt_groups(M, Cout, 1, bm, bn);
   return gm > 0 ? gm : (int)((M + bm - 1) / bm);
+}
+
+// Partial rows of a forward with the A-operand fold (register-staged tiles, one per M tile).
+ECG_API int ecg_conv1d_nlc_fwd_stat_tiles_fold(long M, int Cout) {
+  int bm, bn;
+  pick_fwd_tile(M, Cout, 2, &bm, &bn);
+  return (int)((M + bm - 1) / bm);
 }
 
 // Same for a call with batch B, output length Lout and input dilation in_dil (phase-decomposed data-grad).

@@ -128,6 +128,26 @@ def test_weight_prep_layouts():
     assert n == 35  # ResNet1D-34: 16 blocks x 2 convs + 3 downsample convs (layers 2-4)
 
 
+def test_bn_fold_into_conv2(monkeypatch):
+    """ECG_BN_FOLD=2: conv2 reads z1 and stages relu(z1 * scale1 + shift1) itself (BN_ACT moves to the side lane).
+    The first block's conv2 output is bitwise the unfolded one (same operand values, same K order per element);
+    later blocks differ only through the BN partial-sum order of the register-staged tiles."""
+    outs = []
+    for v in ("0", "2"):
+        monkeypatch.setenv("ECG_BN_FOLD", v)
+        m, ref, eng, x, y = _setup(34, B=64, seed=11, use_graph=False)
+        eng.forward_backward()
+        torch.cuda.synchronize()
+        outs.append((eng._acts[0]["z2"].clone(), eng._acts[0]["a1"].clone(), eng.avg_loss(),
+                     {n: p.grad.clone() for n, p in m.named_parameters()}))
+        del eng, m, ref
+    (z0, a0, l0, g0), (z1, a1, l1, g1) = outs
+    assert torch.equal(a0, a1) and torch.equal(z0, z1)
+    assert abs(l0 - l1) < 1e-3
+    errs = {n: _rel(g1[n], g0[n]) for n in g0}
+    assert errs["fc.weight"] < 1e-2 and max(errs.values()) < 0.3, errs
+
+
 @pytest.mark.parametrize("knob,values", [("ECG_DGRAD_MASK_FROM_Z", ("0", "1")), ("ECG_BN_APPLY_RPT", ("0", "4"))])
 def test_plan_variants_bitwise(knob, values, monkeypatch):
     """Plan variants that must not change a bit: the conv2 data-grad epilogue re-deriving the BN1 ReLU mask from z1
