@@ -92,6 +92,10 @@ for s in $STEPS; do
                run fold_${v}_$r 300 env ECG_BN_FOLD=$v python bench.py --model resnet1d34 --steps 60 --warmup 10 \
                  --no-extras
              done; done ;;
+    split_ab) for r in a b c; do for v in 64 48 40; do
+                run split_${v}_$r 300 env ECG_WGRAD_MAX_SPLITS=$v python bench.py --model resnet1d34 --steps 60 \
+                  --warmup 10 --no-extras
+              done; done ;;
     op_prof) run op_profile_mt0 300 env ECG_CONV_MT=0 python scripts/resnet_op_profile.py 34 1024
              run op_profile_mt1 300 env ECG_CONV_MT=1 python scripts/resnet_op_profile.py 34 1024 ;;
     mt_tests) run mt_tests 600 python -u -m pytest tests/test_conv_mc_gpu.py -k "stats_multi_tile" \
