@@ -408,12 +408,14 @@ ECG_API int conv1d_batch_hip_flag(const float* x, const float* w, float* y, int 
   // (default), 4: 128x1, 5: 64x1.  B=256, L=500, K=7 single call (profiles/r2/conv1d_flag_call_ab.txt): 10.6,
   // 12.4, 12.4, 9.4-9.6, 10.5, 13.4 us - the 124 workgroups of one quad per thread beat fatter threads (less
   // ticket fan-in) and thinner workgroups (more of it).
+  // 6: 256x2.  Default (unset): 256x1 up to 160 workgroups, else 256x2 (the ticket fan-in grows with the
+  // workgroup count: B=512 at 256x1 is 248 tickets).
   static const int cfg = [] {
     const char* e = getenv("ECG_CONV1D_FLAG_CFG");
-    return e ? atoi(e) : 3;
+    return e ? atoi(e) : -1;
   }();
-  static const int kNT[6] = {512, 512, 1024, 256, 128, 64}, kQ[6] = {2, 4, 2, 1, 1, 1};
-  const int ci = cfg < 0 || cfg > 5 ? 0 : cfg;
+  static const int kNT[7] = {512, 512, 1024, 256, 128, 64, 256}, kQ[7] = {2, 4, 2, 1, 1, 1, 2};
+  const int ci = cfg < 0 ? ((total + 255) / 256 <= 160 ? 3 : 6) : (cfg > 6 ? 0 : cfg);
   const int nt = kNT[ci], qpt = kQ[ci];
   const long G = (total + (long)nt * qpt - 1) / ((long)nt * qpt);
   if (G > 0x7fffffffL) return ecg::kBadArg;
@@ -438,6 +440,7 @@ ECG_API int conv1d_batch_hip_flag(const float* x, const float* w, float* y, int 
     else if (ci == 3) ECG_FLAG_CFG(KK, 1, 256);                   \
     else if (ci == 4) ECG_FLAG_CFG(KK, 1, 128);                   \
     else if (ci == 5) ECG_FLAG_CFG(KK, 1, 64);                    \
+    else if (ci == 6) ECG_FLAG_CFG(KK, 2, 256);                   \
     else ECG_FLAG_CFG(KK, 2, 512);                                \
   } while (0)
   switch (K) {
@@ -452,13 +455,26 @@ ECG_API int conv1d_batch_hip_flag(const float* x, const float* w, float* y, int 
 #undef ECG_FLAG_CFG
 #undef ECG_FLAG
   ECG_HIP_CHECK(hipGetLastError());
+  // Poll the word; from 8 us on (a typical call is done by ~9.5 us) also ask the runtime every 3 us
+  // (hipStreamQuery costs ~1 us of host time per call), so a call whose completion word is slow to reach host
+  // memory (seen in some Module-2 grid cells: 28 us against 9-11 typical) returns no later than the runtime's
+  // own completion signal would let it.
   const auto t0 = std::chrono::steady_clock::now();
+  auto next_q = t0 + std::chrono::microseconds(8);
   for (long it = 0; __atomic_load_n(f.flag_host, __ATOMIC_ACQUIRE) != epoch; ++it) {
     __builtin_ia32_pause();
-    if ((it & 1023) == 1023 &&
-        std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2000)) {  // a fault or a stuck queue
-      ECG_HIP_CHECK(hipStreamSynchronize(stream));
-      return __atomic_load_n(f.flag_host, __ATOMIC_ACQUIRE) == epoch ? ecg::kOk : ecg::kHipError;
+    if ((it & 31) == 31) {
+      const auto now = std::chrono::steady_clock::now();
+      if (now >= next_q) {
+        const hipError_t q = hipStreamQuery(stream);
+        if (q == hipSuccess) return ecg::kOk;  // the kernel (and everything before it) completed
+        if (q != hipErrorNotReady) return ecg::kHipError;
+        next_q = now + std::chrono::microseconds(3);
+      }
+      if (now - t0 > std::chrono::milliseconds(2000)) {  // a fault or a stuck queue
+        ECG_HIP_CHECK(hipStreamSynchronize(stream));
+        return __atomic_load_n(f.flag_host, __ATOMIC_ACQUIRE) == epoch ? ecg::kOk : ecg::kHipError;
+      }
     }
   }
   return ecg::kOk;
