@@ -28,7 +28,7 @@ def run_prep(dataset: str = "synthetic", win_len: int = 500, stride: int = 250, 
     load_end = time.perf_counter()
     n, l = windows.shape
     if verbose:
-        print(f"[prep] total windows: {n}, L={l}")
+        print(f"shard_prep: {n} windows of {l} samples to split")
     os.makedirs(out_dir, exist_ok=True)
     i = sid = 0
     while i < n:
@@ -36,7 +36,7 @@ def run_prep(dataset: str = "synthetic", win_len: int = 500, stride: int = 250, 
         out = os.path.join(out_dir, shard_name(sid))
         write_shard(out, windows[i:j])
         if verbose:
-            print(f"[prep] wrote {out} with {j - i} windows")
+            print(f"shard_prep: shard {sid}: {j - i} windows -> {out}")
         i, sid = j, sid + 1
     end = time.perf_counter()
     metrics = {
@@ -54,7 +54,7 @@ def run_prep(dataset: str = "synthetic", win_len: int = 500, stride: int = 250, 
     with open(os.path.join(results_dir, "shard_prep_metrics.json"), "w") as f:
         json.dump(metrics, f, indent=2)
     if verbose:
-        print(f"[prep] done: {sid} shards in {out_dir}; load {metrics['load_time_s']:.2f}s "
+        print(f"shard_prep: finished, {sid} shards in {out_dir}; load {metrics['load_time_s']:.2f}s "
               f"write {metrics['write_time_s']:.2f}s; metrics -> {results_dir}/shard_prep_metrics.json")
     return metrics
 
