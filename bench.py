@@ -77,15 +77,37 @@ def _free_port() -> int:
     return port
 
 
+def count_gpus_kfd(root: str = "/sys/class/kfd/kfd/topology/nodes") -> int:
+    """GPUs visible to this process, counted WITHOUT the HIP runtime: KFD topology nodes with a non-zero
+    ``gpu_id`` (CPU nodes have 0), limited by ``HIP_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES`` /
+    ``CUDA_VISIBLE_DEVICES`` when set.  -1 when the topology is not readable (no KFD)."""
+    try:
+        nodes = os.listdir(root)
+    except OSError:
+        return -1
+    n = 0
+    for node in nodes:
+        try:
+            with open(os.path.join(root, node, "gpu_id")) as f:
+                n += int(f.read().strip() or 0) != 0
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([t for t in v.split(",") if t.strip()]))
+    return n
+
+
 def self_launch(a, argv) -> int:
     """Start ``a.gpus`` ranks (one per GPU) as a ``torch.distributed.run`` child; return its exit code.
 
-    Nothing here initialises HIP: ``torch.cuda.device_count()`` only counts devices on this image."""
+    The parent never touches the GPU runtime: it neither imports torch nor calls HIP; GPUs are counted from
+    the KFD sysfs topology (``count_gpus_kfd``)."""
     backend = os.environ.get("ECG_DIST_BACKEND", "nccl")
     if a.device == "gpu" and backend == "nccl":
-        import torch
-        n_dev = torch.cuda.device_count()
-        if n_dev < a.gpus:
+        n_dev = count_gpus_kfd()
+        if 0 <= n_dev < a.gpus:
             print(f"bench.py: --gpus {a.gpus} needs {a.gpus} GPUs for RCCL (one rank per GPU), found {n_dev}",
                   file=sys.stderr)
             return 2
@@ -104,12 +126,18 @@ def round_plan(steps: int, local_steps: int):
 
 
 class FedAvgRunner:
-    """Runs a round plan on a trainer: each round = local steps then the FedAvg all-reduce (AVG)."""
+    """Runs a round plan on a trainer: each round = local steps then the FedAvg all-reduce (AVG).
 
-    def __init__(self, trainer, flat, ctx, overlap: str):
-        from crossscale_ecg.parallel.fedavg import allreduce_mean_
+    Per round, in enqueue order: launch the round's steps -> issue the all-reduce -> stage the NEXT round's
+    batches (weight-independent) -> [next round] wait for the all-reduce -> launch.  With ``tail`` the
+    collective is issued async, so RCCL's stream waits only for the round's steps and the staging kernels run
+    on the compute stream beside it; with ``none`` the host blocks on the collective before staging."""
+
+    def __init__(self, trainer, flat, ctx, overlap: str, allreduce=None):
+        if allreduce is None:
+            from crossscale_ecg.parallel.fedavg import allreduce_mean_ as allreduce
         self.trainer, self.flat, self.ctx = trainer, flat, ctx
-        self.allreduce = allreduce_mean_
+        self.allreduce = allreduce
         self.overlap = overlap if ctx.distributed else "none"
         self.syncs = 0
         self._pending = None
@@ -119,15 +147,17 @@ class FedAvgRunner:
         for i, n in enumerate(plan):
             next_n = plan[i + 1] if i + 1 < len(plan) else then
             self.trainer.prepare_round(n, reset_loss=False)  # no-op when the previous round staged it
-            if self._pending is not None:  # tail: the next batches were prepared while the all-reduce ran
+            if self._pending is not None:  # tail: the next batches were staged while the all-reduce ran
                 self._pending.wait()
                 self._pending = None
-            self.trainer.launch_round(n, next_n)
+            self.trainer.launch_round(n)
             if self.overlap == "tail":
                 self._pending = self.allreduce(self.flat, self.ctx, async_op=True)
             else:
                 self.allreduce(self.flat, self.ctx)
             self.syncs += 1
+            if next_n is not None and hasattr(self.trainer, "stage"):
+                self.trainer.stage(next_n)
         self.drain()
 
     def drain(self):
@@ -287,20 +317,31 @@ def main(argv=None):
         if tbar.kind == "dist":
             sync()
 
+    # device-side span of the timed work: hipEvents on the compute stream right after the opening bracket and
+    # right after the last round was enqueued (the runner's drain made the compute stream wait for RCCL), so an
+    # outlier can be attributed: gpu_ms ~ wall -> the GPU (or a starved queue) was slow; gpu_ms << wall -> host
+    ev0 = ev1 = None
+    if on_gpu:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     bracket()
+    if ev0 is not None:  # recorded on the idle stream just before the clock starts (its host cost stays outside)
+        ev0.record()
     t0 = time.perf_counter()
     runner.run(timed_plan)
+    if ev1 is not None:
+        ev1.record()
     bracket()
     elapsed = time.perf_counter() - t0
+    gpu_s = ev0.elapsed_time(ev1) / 1e3 if ev0 is not None else float("nan")
     tbar_kind = tbar.kind
     tbar.close()
     world_seen, dist_backend = 1, "none"
     if ctx.distributed:
         import torch.distributed as dist
         world_seen, dist_backend = dist.get_world_size(), dist.get_backend()
-        t = torch.tensor([elapsed], device=dev if dist_backend == "nccl" else "cpu", dtype=torch.float64)
+        t = torch.tensor([elapsed, gpu_s], device=dev if dist_backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, gpu_s = float(t[0].item()), float(t[1].item())
     total = a.gpus * B * a.steps
     value = total / elapsed
     loss = trainer.avg_loss() if hasattr(trainer, "avg_loss") else float("nan")
@@ -335,6 +376,7 @@ def main(argv=None):
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(elapsed * 1e3 / a.steps, 5),
+            "gpu_ms_per_step": round(gpu_s * 1e3 / a.steps, 5) if gpu_s == gpu_s else None,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

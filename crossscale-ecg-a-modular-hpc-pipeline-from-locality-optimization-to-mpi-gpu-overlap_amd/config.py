@@ -30,6 +30,10 @@ class FedAvgConfig:
     momentum: float = 0.9
     seed: int = 1234
     drop_prob: float = 0.0  # FL client dropout injection (weighted FedAvg, zero-weight skip)
+    # latency injection: host sleep inside each round's weight-independent batch preparation (the work that
+    # --overlap tail places under the in-flight all-reduce); lets the overlap tests prove exposure < comm
+    inject_prep_delay_ms: float = 0.0
+    bucket_mb: float = 4.0  # ResNet1D tail / DDP gradient-bucket size (~1-4 MB per collective)
     ckpt_every: int = 0
     ckpt_dir: str = "checkpoints"
     resume: bool = False

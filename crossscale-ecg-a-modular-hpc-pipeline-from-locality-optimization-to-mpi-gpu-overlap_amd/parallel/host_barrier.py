@@ -28,6 +28,7 @@ def _bind(lib) -> None:
     _lib._sig(lib, "ecg_host_barrier_open", [C.c_char_p, _lib.i32, _lib.i32, C.POINTER(_lib.vp)])
     _lib._sig(lib, "ecg_host_barrier_wait", [_lib.vp, _lib.i32])
     _lib._sig(lib, "ecg_host_barrier_close", [_lib.vp])
+    _lib._sig(lib, "ecg_host_barrier_unlink", [_lib.vp])
     lib._host_barrier_bound = True
 
 
@@ -58,6 +59,8 @@ class HostBarrier:
         dist.all_gather_object(oks, bool(ok))
         if all(oks):
             self.kind = "shm"
+            if ctx.rank == 0:  # every rank holds its mapping: drop the name now, so a crash leaks nothing
+                self._lib.ecg_host_barrier_unlink(self._h)
         else:  # every rank falls back together
             self._close_handle()
 

@@ -20,6 +20,7 @@ On CPU (gloo) the same API uses host clocks: ``comm_ms`` = issue -> completion o
 """
 from __future__ import annotations
 
+import contextlib
 import time
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -202,6 +203,24 @@ class FedAvgRound:
         self.comm.wait(self._pending, self._rec)
         self._pending, self._rec = [], None
         self.flat.add_(self.snap).sub_(self.base)  # w <- w + (avg_r - w_r)
+
+    @contextlib.contextmanager
+    def averaged_in_place(self):
+        """Inside the block ``flat`` holds the last all-reduced average (``delayed``: avg_r, after a stream wait on
+        the in-flight collective, which stays pending - the stale correction is still applied at the next
+        boundary); on exit ``flat`` is restored.  Other modes: ``flat`` is already the average, nothing changes."""
+        if self.mode != "delayed" or not self._pending:
+            yield
+            return
+        self.comm.wait(self._pending, self._rec)  # marks them waited; _finish_delayed later only applies
+        keep = self.flat.clone()
+        with torch.no_grad():
+            self.flat.copy_(self.snap)
+        try:
+            yield
+        finally:
+            with torch.no_grad():
+                self.flat.copy_(keep)
 
     def finalize(self) -> None:
         """Drain an in-flight collective (end of training)."""

@@ -164,9 +164,23 @@ def _resume(cfg: FedAvgConfig, cname: str, ctx: DistContext, comm: Communicator,
     if rnd < 0:
         return 0
     own = rank_state_path(cfg.ckpt_dir, rnd, cname, ctx.rank)
+    independent = cfg.sync not in ("fedavg", "ddp") or not ctx.distributed
     if os.path.exists(own):
-        load_trainer_local_state(trainer, load_checkpoint(own))
+        st = load_checkpoint(own)
+        load_trainer_local_state(trainer, st)
+        if st.get("client_weights") is not None:  # --sync none: every client continues from its OWN weights
+            flat = model_flat(model)
+            if st["client_weights"].shape != flat.shape:
+                raise ValueError(f"client weights {tuple(st['client_weights'].shape)} != {tuple(flat.shape)}")
+            with torch.no_grad():
+                flat.copy_(st["client_weights"].to(flat.device))
+        elif independent and ctx.rank != 0:
+            raise RuntimeError(f"{own} holds no client weights: cannot resume an independent (--sync "
+                               f"{cfg.sync}) client without them")
         log.info(f"[fedavg] rank {ctx.rank}: client state restored from {own}")
+    elif independent and ctx.rank != 0:
+        raise RuntimeError(f"--resume with --sync {cfg.sync}: {own} is missing; an independent client cannot be "
+                           "restored from rank 0's model")
     else:
         log.info(f"[fedavg] rank {ctx.rank}: no {own}; momentum restarts at zero, sampler from its seed")
     if ctx.rank == 0:
@@ -213,11 +227,11 @@ def run_fedavg(cfg: FedAvgConfig, ctx: DistContext) -> List[Dict]:
             t_round0 = time.perf_counter()
             rec = CommRecord()
             # ---- broadcast the global model (round 0 / resume / every round for reference parity) ----------
-            # (--overlap tail skips the per-round re-broadcast: it would serialise the overlap away, and the RCCL
-            # AVG already leaves identical weights on every client)
+            # (--overlap tail / delayed skip the per-round re-broadcast: it would drain the in-flight all-reduce
+            # and serialise the overlap away, and the RCCL AVG already leaves identical weights on every client)
             if ctx.distributed and cfg.sync in ("fedavg", "ddp") and (
-                    r == start_round or (fedavg and cfg.bcast_every_round and mode != "tail")):
-                fround.finalize()  # an in-flight tail all-reduce must land before the weights are overwritten
+                    r == start_round or (fedavg and cfg.bcast_every_round and mode == "none")):
+                fround.finalize()  # nothing is in flight here except at a resume boundary
                 with profiling.range("bcast"):
                     fcomm.blocking(lambda: broadcast_model(comm, model), rec)
             # ---- local steps (the previous round's tail all-reduce overlaps this round's batch preparation) --
@@ -225,8 +239,14 @@ def run_fedavg(cfg: FedAvgConfig, ctx: DistContext) -> List[Dict]:
             m_l0 = fcomm.mark()
             stalls0 = len(fround._rec.stalls) if fround._rec is not None else 0
             prev_rec = fround._rec
+
+            def prep(n=n):
+                trainer.prepare_round(n)
+                if cfg.inject_prep_delay_ms > 0:  # latency injection (weight-independent host work)
+                    time.sleep(cfg.inject_prep_delay_ms / 1e3)
+
             with profiling.range("local_round"):
-                fround.begin_round(prep=lambda: trainer.prepare_round(n))
+                fround.begin_round(prep=prep)
                 if cfg.sync == "ddp" and backend == "fused" and ctx.distributed:
                     _ddp_fused_round(trainer, ctx, n)
                 else:
@@ -247,14 +267,16 @@ def run_fedavg(cfg: FedAvgConfig, ctx: DistContext) -> List[Dict]:
                     elif not seg_tail:
                         fround.end_round(rec)
             due = bool(cfg.ckpt_every) and (r + 1) % cfg.ckpt_every == 0
-            if due:
-                fround.finalize()  # checkpoints hold averaged weights (drains an in-flight all-reduce)
+            if due and mode != "delayed":
+                fround.finalize()  # checkpoints hold averaged weights (drains an in-flight tail all-reduce)
             avg_loss = trainer.avg_loss()
             if due:
+                own = model_flat(model) if cfg.sync not in ("fedavg", "ddp") else None  # independent clients
                 if ctx.rank == 0:
                     mom = getattr(trainer, "mom", None)
-                    save_checkpoint(ckpt_path(cfg.ckpt_dir, r, cname), r, model, mom, cname, asdict(cfg))
-                save_rank_state(cfg.ckpt_dir, r, cname, ctx.rank, trainer)
+                    with fround.averaged_in_place():  # delayed: avg_r saved, the stale correction stays pending
+                        save_checkpoint(ckpt_path(cfg.ckpt_dir, r, cname), r, model, mom, cname, asdict(cfg))
+                save_rank_state(cfg.ckpt_dir, r, cname, ctx.rank, trainer, client_weights=own)
             recs.append((r, rec, m_l0, m_l1, inner, avg_loss, (time.perf_counter() - t_round0) * 1e3))
         fround.finalize()
         _sync(dev)

@@ -63,15 +63,23 @@ class ResNetEngineTrainer:
             self.engine.apply_update()
         self.steps_done += 1
 
+    def stage(self, n: Optional[int] = None) -> None:
+        """Draw the NEXT round's batches into the index table, enqueued behind the rounds already launched (which
+        have consumed it); no weights read, so it runs beside an in-flight all-reduce."""
+        # the whole round's batches are drawn up front (a round ended by ``tail_fedavg`` uses the last row)
+        self.sampler.fill(self.table)
+        self._staged = True
+
     def prepare_round(self, n: Optional[int] = None, reset_loss: bool = True) -> None:
-        """Draw the round's batches into the index table (no weights read: may overlap an all-reduce)."""
+        """Draw the round's batches into the index table unless ``stage`` already did."""
         n = self.S if n is None else n
         if n > self.S:
             raise ValueError(f"round of {n} steps > steps_per_round={self.S}")
         if reset_loss:
             self.engine.reset_loss()
-        # the whole round's batches are drawn up front (a round ended by ``tail_fedavg`` uses the last row)
-        self.sampler.fill(self.table)
+        if not getattr(self, "_staged", False):
+            self.sampler.fill(self.table)
+        self._staged = False
         self.engine.reset_counter()
 
     def launch_round(self, n: Optional[int] = None, next_n: Optional[int] = None) -> None:

@@ -7,7 +7,10 @@ Layout (plain ``torch.save``, loaded with ``weights_only=True`` - no pickle exec
   its ``"model"`` entry anywhere.
 * ``checkpoints/fedavg_{cfg}_round{r:05d}.rank{k}.pt`` - written by EVERY rank into its own ``ckpt_dir``: the
   client-local state FedAvg never averages (SGD momentum, the batch sampler's generator / epoch block / cursor,
-  the CPU RNG).
+  the CPU RNG) and, for ``--sync none`` (independent clients), the client's own flat weights.
+* ``--overlap delayed``: a checkpoint of round r holds avg_r (the all-reduce of round r's weights, waited for on
+  the device); the run itself keeps its one-round-stale correction pending, so its trajectory does not depend
+  on ``--ckpt-every``.  A resume starts from avg_r with nothing in flight: resuming ends the staleness once.
 
 Resume (``train.fedavg.run_fedavg``): rank 0 alone resolves the latest round (its directory is the only one
 guaranteed to hold the model file - no shared filesystem is assumed), broadcasts the round index, loads the
@@ -90,8 +93,14 @@ def load_trainer_local_state(trainer, st: Dict[str, Any]) -> None:
         torch.set_rng_state(st["rng_cpu"])
 
 
-def save_rank_state(ckpt_dir: str, round_idx: int, config: str, rank: int, trainer) -> str:
-    return _atomic_save(trainer_local_state(trainer), rank_state_path(ckpt_dir, round_idx, config, rank))
+def save_rank_state(ckpt_dir: str, round_idx: int, config: str, rank: int, trainer,
+                    client_weights: Optional[torch.Tensor] = None) -> str:
+    """``client_weights``: the client's own flat weights, for runs whose clients are never averaged
+    (``--sync none``): a resumed independent client continues from them, not from rank 0's model."""
+    st = trainer_local_state(trainer)
+    if client_weights is not None:
+        st["client_weights"] = client_weights.detach().cpu().clone()
+    return _atomic_save(st, rank_state_path(ckpt_dir, round_idx, config, rank))
 
 
 def load_checkpoint(path: str) -> Dict[str, Any]:

@@ -11,7 +11,8 @@
 // write-through (agent-scope relaxed atomic stores = global_store ... sc1) by every wave, drained with
 // s_waitcnt vmcnt(0) before a workgroup barrier, then ONE lane takes an agent-scope ticket; the workgroup whose
 // ticket is last reads the partials only with sc1 loads after its ticket returned (the other waves after a
-// barrier).  No fences.  Level 1: the last arriver of each group of ``gs`` M tiles sums the group's rows (fp64)
+// barrier).  No fences: valid for gfx950's sc1 lowering of relaxed agent-scope atomics (ecg_common.h refuses
+// any other device target), measured as the guide's hand-off row 1 under load.  Level 1: the last arriver of each group of ``gs`` M tiles sums the group's rows (fp64)
 // into ``gpart``; level 2: the last group reducer of the column block sums the group rows in group order and
 // finalizes.  The summation order never depends on arrival order: bitwise reproducible.  The final reducer
 // zeroes the block's counters for the next launch.

@@ -6,6 +6,14 @@
 
 #define ECG_API extern "C" __attribute__((visibility("default")))
 
+// The inter-workgroup hand-offs of these kernels (bn_tail.h tickets, the split-K / slab last-arriver reducers,
+// the conv1d flag call) rely on gfx950 code generation: relaxed agent-scope atomic stores/loads lower to
+// global_* ... sc1 (write-through / L1-bypassing), which is row 1 of the MI355X guide's sc1 hand-off table and
+// needs no release/acquire fence.  Another target may lower them differently, so refuse to build for it.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "CrossScale-ECG kernels are written for gfx950 (MI355X) only: the sc1 hand-offs are not valid elsewhere"
+#endif
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));

@@ -115,7 +115,17 @@ ECG_API int ecg_host_barrier_wait(void* handle, int timeout_ms) {
   }
 }
 
-// Unmap; the creator also unlinks the name (peers that still map it keep their mapping until they close).
+// Remove the segment's name once every rank holds its mapping (the creator calls this right after the ranks
+// agreed they all opened it): the page then lives exactly as long as the mappings, so a rank that crashes or
+// times out never leaves /dev/shm/ecg_bar_* behind.  Idempotent; a no-op for non-creators.
+ECG_API int ecg_host_barrier_unlink(void* handle) {
+  Barrier* b = static_cast<Barrier*>(handle);
+  if (!b || !b->creator) return 0;
+  b->creator = false;
+  return shm_unlink(b->name) == 0 ? 0 : kErrSys;
+}
+
+// Unmap; a creator that has not unlinked yet also unlinks the name (peers keep their mapping until they close).
 ECG_API int ecg_host_barrier_close(void* handle) {
   Barrier* b = static_cast<Barrier*>(handle);
   if (!b) return 0;

@@ -141,6 +141,67 @@ def test_tail_overlap_equals_none_and_measures_exposure(tmp_path):
     assert any(float(r["comm_ms"]) != float(r["comm_exposed_ms"]) for r in rows)
 
 
+def _rows(path):
+    return list(csv.DictReader(open(path)))
+
+
+def test_overlap_modes_expose_what_they_should(tmp_path):
+    """Each round's weight-independent batch preparation sleeps DELAY ms (--inject-prep-delay-ms).
+    none: the compute side waits right after issuing -> exposed ~= comm;
+    tail: the next round's preparation runs between issue and wait -> exposed <= comm - DELAY;
+    delayed (default flags, i.e. --bcast-every-round on): the collective runs under the next round's steps ->
+    exposed well below comm while comm > 0 (the per-round broadcast must not drain it)."""
+    delay = 40.0
+    res = {}
+    for mode in ("none", "tail", "delayed"):
+        _fedavg_world2(tmp_path, ["--overlap", mode, "--inject-prep-delay-ms", str(delay)], 4, f"ov_{mode}.csv")
+        res[mode] = _rows(tmp_path / f"ov_{mode}.csv")
+        assert {r["overlap"] for r in res[mode]} == {mode}
+    for r in res["none"]:
+        comm, exposed = float(r["comm_ms"]), float(r["comm_exposed_ms"])
+        assert comm > 0 and exposed >= 0.8 * comm - 0.5, r
+    # tail: the all-reduce of round k is waited for inside round k+1's begin (after the delayed preparation);
+    # the last round's collective is drained by finalize() without a preparation in between
+    for r in res["tail"]:
+        if int(r["round_idx"]) < 3:
+            comm, exposed = float(r["comm_ms"]), float(r["comm_exposed_ms"])
+            assert comm >= 0.9 * delay and exposed <= comm - 0.9 * delay, r
+    dl = [r for r in res["delayed"] if int(r["round_idx"]) < 3]
+    comm = sum(float(r["comm_ms"]) for r in dl)
+    exposed = sum(float(r["comm_exposed_ms"]) for r in dl)
+    assert comm > 0 and exposed < 0.5 * comm, (comm, exposed)
+
+
+def test_delayed_trajectory_independent_of_ckpt_every(tmp_path):
+    """A checkpoint no longer ends the delayed mode's staleness: the run's weights after round 3 are the same
+    with a checkpoint every round and with one at the end (the checkpoint holds avg_r)."""
+    import torch
+    import crossscale_ecg  # noqa: F401
+    for every in (1, 4):
+        _fedavg_world2(tmp_path, ["--overlap", "delayed", "--ckpt-every", str(every), "--ckpt-dir",
+                                  str(tmp_path / f"ck{every}")], 4, f"d{every}.csv")
+    assert torch.equal(_final_weights(tmp_path / "ck1", 3), _final_weights(tmp_path / "ck4", 3))
+
+
+def test_resume_sync_none_restores_each_clients_weights(tmp_path):
+    """--sync none: every client's own weights go into its rank file, so a resumed run continues each
+    independent client bit for bit (rank 1 included)."""
+    import torch
+    import crossscale_ecg  # noqa: F401
+    from crossscale_ecg.utils.ckpt import load_checkpoint
+    base = ["--sync", "none", "--ckpt-every", "1"]
+    _fedavg_world2(tmp_path, base + ["--ckpt-dir", str(tmp_path / "full")], 4, "nf.csv")
+    _fedavg_world2(tmp_path, base + ["--ckpt-dir", str(tmp_path / "part")], 2, "np.csv")
+    _fedavg_world2(tmp_path, base + ["--ckpt-dir", str(tmp_path / "part"), "--resume"], 4, "np.csv")
+    for k in (0, 1):
+        a = load_checkpoint(str(tmp_path / "full" / f"fedavg_G1_round00003.rank{k}.pt"))["client_weights"]
+        b = load_checkpoint(str(tmp_path / "part" / f"fedavg_G1_round00003.rank{k}.pt"))["client_weights"]
+        assert torch.equal(a, b), k
+    r0 = load_checkpoint(str(tmp_path / "full" / "fedavg_G1_round00003.rank0.pt"))["client_weights"]
+    r1 = load_checkpoint(str(tmp_path / "full" / "fedavg_G1_round00003.rank1.pt"))["client_weights"]
+    assert not torch.equal(r0, r1)  # independent clients really diverged
+
+
 def test_resume_only_rank0_has_checkpoint(tmp_path):
     """Node-local checkpoint dirs: rank 0 resolves the round and broadcasts it; a rank whose directory is empty
     resumes at the same round (momentum from zero) instead of desynchronising the collectives."""
