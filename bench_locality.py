@@ -29,11 +29,15 @@ def main(argv=None):
     ap.add_argument("--no-normalize", action="store_true")
     ap.add_argument("--results-dir", default="results")
     ap.add_argument("--plots", action="store_true")
+    ap.add_argument("--reps", type=int, default=1, help="interleaved repetitions per (config, batch): median + IQR")
+    ap.add_argument("--pin-thread", action="store_true",
+                    help="pinned configs: DataLoader pin-memory thread on a CPU of its own, apart from the main thread")
     a = ap.parse_args(argv)
     if a.dataset == "mitbih":
         print("[WARN] MIT-BIH needs wfdb + network; falling back to synthetic shards.")
     rows = run_locality(a.shard_dir, a.batch_sizes, a.iters, a.num_workers, a.device, a.compute, a.results_dir,
-                        a.n_windows, labl=not a.no_labl, normalize=not a.no_normalize)
+                        a.n_windows, labl=not a.no_labl, normalize=not a.no_normalize, reps=a.reps,
+                        pin_thread=a.pin_thread)
     if a.plots:
         from crossscale_ecg.report.plots import plot_locality
         plot_locality(os.path.join(a.results_dir, "part1_locality_results.csv"), a.results_dir)

@@ -89,13 +89,45 @@ class _Compute:
         self.opt.zero_grad(set_to_none=True)
 
 
-def measure_step(dl: DataLoader, device, non_blocking: bool, iters: int = 50, compute: str = "torch") -> Dict:
-    """Reference ``measure_step`` (bench_locality.py:23-76): 5 warm-up steps, then timed data/H2D/compute."""
+def split_cpus(cpus: Optional[Sequence[int]] = None):
+    """(main-thread cpu, pin-thread cpu): two distinct CPUs of this process's affinity set (None if < 2)."""
+    cpus = sorted(cpus if cpus is not None else os.sched_getaffinity(0))
+    if len(cpus) < 2:
+        return None
+    return cpus[0], cpus[len(cpus) // 2]
+
+
+def _pin_threads(it, pin_cpus) -> Optional[tuple]:
+    """Put the DataLoader iterator's pin-memory thread and the calling (training) thread on two different CPUs so
+    the pinning copy no longer competes with the launch-bound step for one core.  Returns the calling thread's
+    previous affinity (to restore), or None when not applicable."""
+    th = getattr(it, "_pin_memory_thread", None)
+    if pin_cpus is None or th is None or getattr(th, "native_id", None) is None:
+        return None
+    prev = os.sched_getaffinity(0)
+    os.sched_setaffinity(th.native_id, {pin_cpus[1]})
+    os.sched_setaffinity(0, {pin_cpus[0]})  # (Linux: pid 0 = the calling thread)
+    return prev
+
+
+def measure_step(dl: DataLoader, device, non_blocking: bool, iters: int = 50, compute: str = "torch",
+                 pin_cpus: Optional[tuple] = None) -> Dict:
+    """Reference ``measure_step`` (bench_locality.py:23-76): 5 warm-up steps, then timed data/H2D/compute.
+    ``pin_cpus=(main, pin)``: the pin-memory thread and this thread on distinct CPUs (``split_cpus``)."""
     dev = torch.device(device)
     B = dl.batch_size
     L = dl.dataset.x.shape[1]
     step = _Compute(dev, compute, B, L)
     it = iter(dl)
+    prev_aff = _pin_threads(it, pin_cpus)
+    try:
+        return _measure(dl, dev, non_blocking, iters, step, it, pin_cpus)
+    finally:
+        if prev_aff is not None:
+            os.sched_setaffinity(0, prev_aff)
+
+
+def _measure(dl, dev, non_blocking, iters, step, it, pin_cpus):
 
     def nxt():
         nonlocal it
@@ -113,6 +145,7 @@ def measure_step(dl: DataLoader, device, non_blocking: bool, iters: int = 50, co
     data_ms = h2d_ms = comp_ms = 0.0
     total = 0
     it = iter(dl)
+    _pin_threads(it, pin_cpus)  # the new iterator's pin thread
     t_all = time.perf_counter()
     for _ in range(iters):
         t0 = time.perf_counter()
@@ -248,42 +281,70 @@ def bench_gpu_resident(shard_paths, batch_size, iters, device, compute="torch") 
     return dict(step_ms=wall, samples_per_s=batch_size / (wall / 1e3), data_ms=0.0, h2d_ms=0.0, compute_ms=wall)
 
 
+SPREAD_COLUMNS = ["samples_per_s_q1", "samples_per_s_q3", "reps"]
+
+
+def _median_row(cells: List[Dict]) -> Dict:
+    """Median of every timing column over the repetitions of one (config, batch) cell, plus the interquartile
+    range of samples/s."""
+    out = dict(cells[0])
+    for k in ("data_ms", "h2d_ms", "compute_ms", "step_ms", "samples_per_s"):
+        out[k] = float(np.median([c[k] for c in cells]))
+    sps = [c["samples_per_s"] for c in cells]
+    out["samples_per_s_q1"], out["samples_per_s_q3"] = (float(v) for v in np.percentile(sps, [25, 75]))
+    out["reps"] = len(cells)
+    return out
+
+
 def run_locality(shard_dir: str, batch_sizes: List[int], iters: int = 100, num_workers: int = 4,
                  device: Optional[str] = None, compute: str = "torch", results_dir: str = "results",
-                 n_windows: int = 20000, labl: bool = True, normalize: bool = True) -> List[Dict]:
+                 n_windows: int = 20000, labl: bool = True, normalize: bool = True, reps: int = 1,
+                 pin_thread: bool = False) -> List[Dict]:
+    """A0-A5 per batch size.  ``reps`` > 1: every (config, batch) cell is measured ``reps`` times, the
+    configurations interleaved within each repetition (A0 A1 A2 A3 A4 A5, A0 A1 ...), and the CSV holds the
+    median of each column plus the samples/s interquartile range (``samples_per_s_q1/q3``, ``reps``).
+    ``pin_thread``: the pinned configurations run with the pin-memory thread on its own CPU."""
     dev = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
     paths = ensure_synthetic_shards(shard_dir, n_windows, shard_size=8192) if not list_shards(shard_dir) \
         else list_shards(shard_dir)
     ds = ShardDataset(paths)
+    pin_cpus = split_cpus() if pin_thread else None
     rows, labl_rows = [], []
     for bs in batch_sizes:
-        for name, contiguous, pin, nb in CONFIGS:
-            sampler = SequentialSampler(ds) if contiguous else RandomSampler(ds)
-            dl = DataLoader(ds, batch_size=bs, sampler=sampler, num_workers=num_workers,
-                            pin_memory=pin and dev.type == "cuda", drop_last=True,
-                            persistent_workers=num_workers > 0)
-            st = measure_step(dl, dev, non_blocking=nb, iters=iters, compute=compute)
-            # retire this loader's persistent worker processes (and its pin-memory thread) before the next
-            # config is timed: left alive they prefetch beside it (the A4 B=256 outlier of round 1)
-            del dl
-            gc.collect()
-            row = dict(config=name, batch_size=bs, pin_memory=pin, contiguous=contiguous, non_blocking=nb, **st)
-            print(row, flush=True)
+        cells: Dict[str, List[Dict]] = {}
+        for rep in range(max(1, reps)):
+            for name, contiguous, pin, nb in CONFIGS:
+                sampler = SequentialSampler(ds) if contiguous else RandomSampler(ds)
+                dl = DataLoader(ds, batch_size=bs, sampler=sampler, num_workers=num_workers,
+                                pin_memory=pin and dev.type == "cuda", drop_last=True,
+                                persistent_workers=num_workers > 0)
+                st = measure_step(dl, dev, non_blocking=nb, iters=iters, compute=compute,
+                                  pin_cpus=pin_cpus if pin else None)
+                # retire this loader's persistent worker processes (and its pin-memory thread) before the next
+                # config is timed: left alive they prefetch beside it (the A4 B=256 outlier of round 1)
+                del dl
+                gc.collect()
+                row = dict(config=name, batch_size=bs, pin_memory=pin, contiguous=contiguous, non_blocking=nb, **st)
+                print(dict(rep=rep, **row), flush=True)
+                cells.setdefault(name, []).append(row)
+            if labl:
+                st = bench_labl(paths, bs, iters, normalize, dev, compute=compute)
+                r = dict(config="A4_LABL", batch_size=bs, pin_memory=True, contiguous=True, non_blocking=True, **st)
+                print(dict(rep=rep, **r), flush=True)
+                cells.setdefault("A4_LABL", []).append(r)
+            if dev.type == "cuda":
+                st = bench_gpu_resident(paths, bs, iters, dev, compute=compute)
+                r = dict(config="A5_GPU_RESIDENT", batch_size=bs, pin_memory=False, contiguous=False,
+                         non_blocking=False, **st)
+                print(dict(rep=rep, **r), flush=True)
+                cells.setdefault("A5_GPU_RESIDENT", []).append(r)
+        for name, cl in cells.items():
+            row = _median_row(cl)
             rows.append(row)
-        if labl:
-            st = bench_labl(paths, bs, iters, normalize, dev, compute=compute)
-            r = dict(config="A4_LABL", batch_size=bs, **st)
-            print(r, flush=True)
-            labl_rows.append(r)
-            rows.append(dict(config="A4_LABL", batch_size=bs, pin_memory=True, contiguous=True, non_blocking=True,
-                             **st))
-        if dev.type == "cuda":
-            st = bench_gpu_resident(paths, bs, iters, dev, compute=compute)
-            rows.append(dict(config="A5_GPU_RESIDENT", batch_size=bs, pin_memory=False, contiguous=False,
-                             non_blocking=False, **st))
-            print(rows[-1], flush=True)
+            if name == "A4_LABL":
+                labl_rows.append(row)
     os.makedirs(results_dir, exist_ok=True)
-    write_csv(os.path.join(results_dir, "part1_locality_results.csv"), rows, LOCALITY_COLUMNS)
+    write_csv(os.path.join(results_dir, "part1_locality_results.csv"), rows, LOCALITY_COLUMNS + SPREAD_COLUMNS)
     if labl_rows:
-        write_csv(os.path.join(results_dir, "part1_labl_results.csv"), labl_rows, LABL_COLUMNS)
+        write_csv(os.path.join(results_dir, "part1_labl_results.csv"), labl_rows, LABL_COLUMNS + SPREAD_COLUMNS)
     return rows

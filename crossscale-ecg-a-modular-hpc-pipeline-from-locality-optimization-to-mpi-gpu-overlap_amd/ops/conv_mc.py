@@ -33,6 +33,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad", [vp, vp, vp] + [i32] * 9 + [vp])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_tiles", [i32, i32, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_target_wgs", [i32, i32, i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_wgrad_splits", [i32] * 8)
     _lib._sig(lib, "ecg_conv1d_nlc_set_big", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_set_mt", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_ex", [vp] * 7 + [i32] * 10 + [vp, vp, vp])
@@ -111,7 +112,9 @@ def wgrad_raw(dy: torch.Tensor, x: torch.Tensor, K: int, stride: int, pad: int,
     chunks = (R + 63) // 64
     lib = _lib_k()
     tiles = lib.ecg_conv1d_nlc_wgrad_tiles(Cout, K, Cin)
-    if splits is None:  # target workgroup count, >= 8 row chunks per workgroup, <= 256 partial slices
+    if splits is None:  # the tap-shared kernel's plan, else: target workgroups, >= 8 chunks each, <= 256 slices
+        splits = lib.ecg_conv1d_nlc_wgrad_splits(B, Lin, Cin, Lout, Cout, K, stride, pad)
+    if not splits:
         target = lib.ecg_conv1d_nlc_wgrad_target_wgs(Cout, K, Cin)
         splits = max(1, min(256, max(1, chunks // 8), max(1, target // max(1, tiles))))
     part = torch.empty((splits, Cout, K * Cin), dtype=torch.float32, device=dy.device)

@@ -51,6 +51,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles", [ctypes.c_long, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_tiles", [i32, i32, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_target_wgs", [i32, i32, i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_wgrad_splits", [i32] * 8)
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles_ex", [i32, i32, i32, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles_fold", [ctypes.c_long, i32])
     lib._plan_bound = True
@@ -195,7 +196,12 @@ class ResNetStepEngine:
         self._keep.append(tickets)
 
         # ---- wgrad split plan + workspace
-        def wsplits(R, Cout, K, Cin):
+        def wsplits(R, Cout, K, Cin, s=1, Lin=None, Lout=None):
+            # stride-1 3-tap convs: the tap-shared kernel's own plan (conv1d_mc.hip, ecg_conv1d_nlc_wgrad_splits)
+            if Lout is not None:
+                ts = self.lib.ecg_conv1d_nlc_wgrad_splits(B, Lin, Cin, Lout, Cout, K, s, 1 if K == 3 else 0)
+                if ts > 0:
+                    return ts
             # the kernel's target workgroup count, >= 8 row chunks each, <= 256 partial slices (the reduce reads
             # S x |dW|)
             chunks = (R + 63) // 64
@@ -209,7 +215,8 @@ class ResNetStepEngine:
         ws_need = 0
         for (Li, Ci, Lo, Co, s), blk in zip(shapes, blocks):
             R = B * Lo
-            ws_need = max(ws_need, wsplits(R, Co, 3, Ci) * Co * 3 * Ci, wsplits(R, Co, 3, Co) * Co * 3 * Co)
+            ws_need = max(ws_need, wsplits(R, Co, 3, Ci, s, Li, Lo) * Co * 3 * Ci,
+                          wsplits(R, Co, 3, Co, 1, Lo, Lo) * Co * 3 * Co)
             if blk.downsample is not None:
                 ws_need = max(ws_need, wsplits(R, Co, 1, Ci) * Co * Ci)
         stem_chunk = max(256, -(-(B * Lz) // 1024))  # <= ~1024 partial slices
@@ -328,7 +335,7 @@ class ResNetStepEngine:
                *extra, tail_ptr, *m_words, *f_words, lane=lane)
 
         def wgrad(dy, x, Lin, Cin, Lout, Cout, K, s, p, weight):
-            S = wsplits(B * Lout, Cout, K, Cin)
+            S = wsplits(B * Lout, Cout, K, Cin, s, Lin, Lout)
             op("CONV_WGRAD", P(dy), P(x), P(ws_w), S, B, Lin, Cin, Lout, Cout, K, s, p, lane=1)
             op("REDUCE_WGRAD", P(ws_w), S, Cout, K, Cin, self._gptr(weight), lane=1)
 

@@ -1246,6 +1246,250 @@ __global__ __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) void conv1d_nlc_wgrad_
   wgrad_epilogue<BM, BN, NWR>(a, acc, smem, split, co0, n0);
 }
 
+// ------------------------------------------------------------------------------ tap-shared weight gradient
+// Stride-1, pad-1, 3-tap convs (Lin == Lout = L, every 3-tap conv of a ResNet stage except its first):
+//   dw[co][k][ci] = sum_r dy[r][co] * x[r + k - 1][ci]   over rows r = (b, t), the shifted row inside sample b.
+// One workgroup owns a 64 (co) x 64 (ci) x 3 (taps) block of dw and a range of 64-row chunks of r.  Per chunk it
+// stages dy[r0, r0 + 64) and x[r0 - 1, r0 + 65) ONCE into LDS (LDS-DMA): the three taps read the x image at row
+// offsets 0, 1, 2.  Against the one-tap kernel (a 128 x 128 tile of one tap per workgroup) that moves 17 KB instead
+// of 32 KB per 0.8 M MACs ... per CU: 46 vs 32 MAC per staged byte, 3 x the MFMAs per barrier, and a 12 K-element
+// output block instead of 16 K, so the split-K partial slabs (S x |dw|) shrink at equal workgroup counts.
+// Sample boundaries: where t = 0 (tap 0) or t = L - 1 (tap 2) the shifted x row belongs to the neighbouring sample,
+// so the dy operand of that tap is zeroed at those rows (a per-lane dword mask on the MFMA fragment).
+// LDS images: [row][64] bf16 (128-B rows); 16-B chunk c of row j lives at chunk c ^ tsw(j), tsw(j) =
+// 2 * (((j >> 1) & 1) | ((j >> 3) & 1) << 1): the 8 rows x 32 B one 32-lane ds_read_b64_tr_b16 group reads (rows
+// {0..3, 8..11} + any shift) hit all 64 banks once.  The DMA writes lane-linear, so the XOR goes on the SOURCE chunk.
+// Waves: wave w owns ci columns [16w, 16w + 16) for all 64 co and 3 taps (acc[4 co frags][3 taps]).
+__device__ __forceinline__ int tsw(int j) { return 2 * (((j >> 1) & 1) | (((j >> 3) & 1) << 1)); }
+
+// LDS-DMA through inline asm: hipcc (ROCm 7.2) cannot tell a ring buffer's stages apart, so after a builtin
+// buffer_load ... lds it waits vmcnt(0) before the next ds_read of ANY stage - draining the chunks the ring keeps in
+// flight.  Issued from asm the loads are invisible to its wait-count pass; the loop's counted vmcnt waits (the only
+// vector-memory loads in flight there) order them.  M0 = the wave's LDS destination; s_nop covers the M0 -> LDS-DMA
+// hazard.
+typedef int srd_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ srd_t make_srd(const void* p, long bytes) {
+  const unsigned long a = reinterpret_cast<unsigned long>(p);
+  srd_t r;
+  r[0] = (int)(unsigned)(a & 0xffffffffu);
+  r[1] = (int)(unsigned)((a >> 32) & 0xffffu);
+  r[2] = (int)(bytes < 0x7fff0000L ? bytes : 0x7fff0000L);
+  r[3] = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ unsigned lds_addr(const unsigned char* p) {
+  return (unsigned)reinterpret_cast<unsigned long>((__attribute__((address_space(3))) const unsigned char*)p);
+}
+__device__ __forceinline__ void dma16_asm(srd_t srd, unsigned voff, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(srd), "s"(lds)
+               : "memory", "m0");
+}
+
+constexpr int TSW_DY = 64 * 128;              // dy image bytes per stage
+constexpr int TSW_STAGE = TSW_DY + 72 * 128;  // + x image rows r0-1 .. r0+70 (66 used)
+
+template <int NST>
+__global__ __launch_bounds__(256, 2) void conv1d_nlc_wgrad_ts_kernel(WgradArgs a, int TM, int TN, int splits) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR): the DMA destinations are scalar
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int tiles = TM * TN;
+  const int split = wgid / tiles, tile = wgid % tiles;  // the tiles of one split (same rows) share an XCD
+  const int co0 = (tile / TN) * 64, ci0 = (tile % TN) * 64;
+  const int L = a.Lout;
+  const int R = a.B * L;
+  const int nchunks = (R + 63) / 64;
+  const int ch0 = split * a.chunks_per_split;
+  const int ch1 = min(nchunks, ch0 + a.chunks_per_split);
+  f32x4 acc[4][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (ch0 < ch1) {  // block-uniform
+    const srd_t dyr = make_srd(a.dy, (long)R * a.Cout * 2);
+    const srd_t xr = make_srd(a.x, (long)R * a.Cin * 2);
+    const unsigned lds0 = lds_addr(smem);
+    const int prow = lane >> 3;  // row inside an 8-row DMA piece
+    // issue: dy pieces wv, wv + 4; x pieces wv, wv + 4, and x piece 8 split over the waves (16 lanes = 2 rows each)
+    auto issue = [&](int ch, int st) {
+      const unsigned dimg = lds0 + st * TSW_STAGE;
+      const unsigned ximg = dimg + TSW_DY;
+      const int r0 = ch * 64;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int p = wv + 4 * u, row = 8 * p + prow, r = r0 + row;
+        const int src = (lane & 7) ^ tsw(row);
+        dma16_asm(dyr, r < R ? (unsigned)(((long)r * a.Cout + co0 + src * 8) * 2) : 0x7ffffff0u, dimg + p * 1024);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int p = wv + 4 * u, row = 8 * p + prow, r = r0 - 1 + row;
+        const int src = (lane & 7) ^ tsw(row);
+        dma16_asm(xr, (r >= 0 && r < R) ? (unsigned)(((long)r * a.Cin + ci0 + src * 8) * 2) : 0x7ffffff0u,
+              ximg + p * 1024);
+      }
+      {  // piece 8 (rows 64..71): lanes 16w .. 16w + 15 of wave w write rows 64 + 2w, 65 + 2w
+        const int row = 64 + prow, r = r0 - 1 + row;
+        const int src = (lane & 7) ^ tsw(row);
+        if ((lane >> 4) == wv)
+          dma16_asm(xr, (r >= 0 && r < R) ? (unsigned)(((long)r * a.Cin + ci0 + src * 8) * 2) : 0x7ffffff0u,
+                ximg + 8 * 1024);
+      }
+    };
+    const int h = lane >> 4, q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
+    auto tr_img = [&](const unsigned char* img, int row, int col) -> s16x4 {
+      return tr16(reinterpret_cast<const __bf16*>(img + row * 128 + (((col >> 3) ^ tsw(row)) << 4) + ((col & 7) << 1)));
+    };
+    auto mma = [&](int st, int ch) {
+      const unsigned char* dimg = smem + st * TSW_STAGE;
+      const unsigned char* ximg = dimg + TSW_DY;
+      const int r0 = ch * 64;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        typedef short s16x8v __attribute__((ext_vector_type(8)));
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const int rr = ks * 32 + 8 * h + q;
+        // this lane's 8 reduction rows r0 + ks*32 + 8h + j: tap 0 drops t == 0, tap 2 drops t == L - 1 (L >= 8:
+        // one wrap at most)
+        const int rb = r0 + ks * 32 + 8 * h;
+        const int tb = rb - fdiv(rb, a.lout) * L;
+        u32x4 m0, m2;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          unsigned v0 = 0u, v2 = 0u;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            int t = tb + 2 * d + e;
+            t -= t >= L ? L : 0;
+            v0 |= (t != 0 ? 0xffffu : 0u) << (16 * e);
+            v2 |= (t != L - 1 ? 0xffffu : 0u) << (16 * e);
+          }
+          m0[d] = v0;
+          m2[d] = v2;
+        }
+        bf16x8 bx[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const s16x4 lo = tr_img(ximg, rr + k, 16 * wv + p4), hi = tr_img(ximg, rr + k + 4, 16 * wv + p4);
+          s16x8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          bx[k] = __builtin_bit_cast(bf16x8, v);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const s16x4 lo = tr_img(dimg, rr, 16 * i + p4), hi = tr_img(dimg, rr + 4, 16 * i + p4);
+          s16x8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const u32x4 ad = __builtin_bit_cast(u32x4, v);
+          acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ad), bx[1], acc[i][1], 0, 0, 0);
+          acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ad & m0), bx[0], acc[i][0], 0,
+                                                              0, 0);
+          acc[i][2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ad & m2), bx[2], acc[i][2], 0,
+                                                              0, 0);
+        }
+      }
+    };
+    // NST-stage ring: chunks ch+1 .. ch+NST-2 stay in flight while chunk ch's MFMAs run.  Every wave issues exactly
+    // 5 DMA instructions per chunk, so "chunk ch landed" = at most 5 x (younger chunks issued) outstanding; raw
+    // s_barrier (a __syncthreads() would emit vmcnt(0) and drain the younger chunks: guide, "Pipelining across
+    // barriers"); lgkmcnt(0) before it retires this wave's ds_reads of the buffer the next issue overwrites.
+    const int n = ch1 - ch0;
+#pragma unroll
+    for (int i = 0; i < NST - 1; ++i)
+      if (i < n) issue(ch0 + i, i);
+    for (int i = 0; i < n; ++i) {
+      const int ahead = min(NST - 2, n - 1 - i);  // younger chunks already issued
+      if constexpr (NST >= 4) {
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if constexpr (NST == 3) {
+        if (ahead >= 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (i + NST - 1 < n) issue(ch0 + i + NST - 1, (i + NST - 1) % NST);  // into the buffer mma(i - 1) read
+      mma(i % NST, ch0 + i);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  }
+  // partial[split][co][k * Cin + ci]: lane holds co = 16i + 4h + e, ci = 16 wv + (lane & 15) -> 64-B row segments
+  const long N = 3L * a.Cin;
+  float* out = a.part + (long)split * a.Cout * N + (long)co0 * N + ci0 + 16 * wv + (lane & 15);
+  const int hq = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[(long)(16 * i + hq + e) * N + (long)k * a.Cin] = acc[i][k][e];
+}
+
+// The tap-shared kernel applies (stride 1, pad 1, 3 taps, same length, whole tensors addressable with 32-bit
+// offsets); ECG_WGRAD_TS=0 keeps the one-tap kernels (read once).
+inline bool wgrad_ts_ok(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ECG_WGRAD_TS");
+    v = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  const long R = (long)B * Lout;
+  return v == 1 && Kw == 3 && stride == 1 && pad == 1 && Lin == Lout && Lout >= 8 && Cin % 64 == 0 && Cout % 64 == 0 &&
+         R * Cout * 2 < 0x7fff0000L && R * Cin * 2 < 0x7fff0000L;
+}
+
+// Workgroups the tap-shared launch aims for (ECG_WGRAD_TS_WGS, default 256: one per CU; the split-K partials are
+// workgroups x 48 KB).
+inline int wgrad_ts_target() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ECG_WGRAD_TS_WGS");
+    v = e ? atoi(e) : 256;
+    if (v < 8) v = 8;
+  }
+  return v;
+}
+
+// ECG_WGRAD_TS_NST = LDS stages of the tap-shared loop (2..4, default 4: two chunks in flight); read once.
+inline int wgrad_ts_nst() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ECG_WGRAD_TS_NST");
+    v = e ? atoi(e) : 4;
+    if (v < 2 || v > 4) v = 4;
+  }
+  return v;
+}
+
+template <int NST>
+int launch_wgrad_ts_n(const WgradArgs& a, int splits, hipStream_t stream) {
+  constexpr int SMEM = NST * TSW_STAGE;
+  static bool attr = false;
+  if (!attr) {
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_wgrad_ts_kernel<NST>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
+    attr = true;
+  }
+  const int TM = a.Cout / 64, TN = a.Cin / 64;
+  hipLaunchKernelGGL(conv1d_nlc_wgrad_ts_kernel<NST>, dim3((unsigned)(TM * TN * splits)), dim3(256), SMEM, stream, a,
+                     TM, TN, splits);
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
+}
+
+int launch_wgrad_ts(const WgradArgs& a, int splits, hipStream_t stream) {
+  switch (wgrad_ts_nst()) {
+    case 2: return launch_wgrad_ts_n<2>(a, splits, stream);
+    case 3: return launch_wgrad_ts_n<3>(a, splits, stream);
+    default: return launch_wgrad_ts_n<4>(a, splits, stream);
+  }
+}
+
 template <int BM, int BN>
 int launch_wgrad(const WgradArgs& a, int splits, hipStream_t stream) {
   constexpr int NWR = BM >= 256 ? 4 : 2;
@@ -1438,6 +1682,7 @@ ECG_API int ecg_conv1d_nlc_wgrad(const void* dy, const void* x, float* part, int
   const int cps = (nchunks + splits - 1) / splits;
   WgradArgs a{static_cast<const __bf16*>(dy), static_cast<const __bf16*>(x), part, B, Lin, Cin, Lout, Cout, Kw,
               stride, pad, cps, make_fastdiv(Lout)};
+  if (wgrad_ts_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad)) return launch_wgrad_ts(a, splits, stream);
   const bool bm128 = Cout % 128 == 0, bn128 = Cin % 128 == 0;
   // LDS-DMA loops: 32-bit buffer offsets from the split's first row / sample
   const long rows = (long)cps * 64;
@@ -1457,6 +1702,17 @@ ECG_API int ecg_conv1d_nlc_wgrad_tiles(int Cout, int Kw, int Cin) {
   const bool big = wgrad_big(Cout, Cin);
   const int bm = big ? 256 : (Cout % 128 == 0 ? 128 : 64), bn = big ? 256 : (Cin % 128 == 0 ? 128 : 64);
   return (Cout / bm) * (Kw * Cin / bn);
+}
+
+// Split count for the tap-shared weight-gradient kernel (64 x 64 x 3 output blocks, ~ECG_WGRAD_TS_WGS workgroups,
+// >= 4 row chunks each), or 0 when this conv takes the one-tap kernels (the caller then sizes its own splits).
+ECG_API int ecg_conv1d_nlc_wgrad_splits(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad) {
+  if (!wgrad_ts_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad)) return 0;
+  const long chunks = ((long)B * Lout + 63) / 64;
+  const int tiles = (Cout / 64) * (Cin / 64);
+  long s = (wgrad_ts_target() + tiles - 1) / tiles;
+  s = s < chunks / 4 ? s : chunks / 4;
+  return (int)(s < 1 ? 1 : (s > 1024 ? 1024 : s));
 }
 
 // Workgroups the weight-gradient launch should aim for (tiles x splits): ~4 resident per CU for the 4-wave

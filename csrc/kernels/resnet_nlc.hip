@@ -906,6 +906,62 @@ __global__ __launch_bounds__(TPB) void reduce_wgrad_kernel(const float* __restri
   }
 }
 
+// Same sum, for the tap-shared weight gradient's many-split partials (S up to 256 x 48 KB slabs): block = 16 float4
+// columns x 16 split groups, each thread's loads of a 16-split batch in flight together (one memory round trip per
+// 256 splits), fixed summation order (bitwise reproducible); 16x the blocks of reduce_wgrad_kernel for a small |dW|.
+__global__ __launch_bounds__(TPB) void reduce_wgrad_wide_kernel(const float* __restrict__ part, int S, int Cout, int K,
+                                                                int Cin, float* __restrict__ grad) {
+  __shared__ float4 red[16][17];
+  const long N = (long)Cout * K * Cin, N4 = N / 4;
+  const int tid = threadIdx.x, col = tid & 15, sg = tid >> 4;
+  const long i4 = (long)blockIdx.x * 16 + col;
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i4 < N4) {
+    int s = sg;
+    for (; s + 16 * 15 < S; s += 256) {
+      float4 t[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) t[u] = p4[(long)(s + 16 * u) * N4 + i4];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        acc.x += t[u].x; acc.y += t[u].y; acc.z += t[u].z; acc.w += t[u].w;
+      }
+    }
+    for (; s + 16 * 3 < S; s += 64) {
+      float4 t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[u] = p4[(long)(s + 16 * u) * N4 + i4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc.x += t[u].x; acc.y += t[u].y; acc.z += t[u].z; acc.w += t[u].w;
+      }
+    }
+    for (; s < S; s += 16) {
+      const float4 t = p4[(long)s * N4 + i4];
+      acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+    }
+  }
+  red[sg][col] = acc;
+  __syncthreads();
+  if (tid < 64) {  // 16 columns x 4 elements: one output element per thread
+    const int c = tid >> 2, e = tid & 3;
+    const long i = ((long)blockIdx.x * 16 + c) * 4 + e;  // = co*K*Cin + k*Cin + ci
+    if (i < N) {
+      float v = 0.f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const float4 r = red[g][c];
+        v += e == 0 ? r.x : e == 1 ? r.y : e == 2 ? r.z : r.w;
+      }
+      const int ci = (int)(i % Cin);
+      const long rk = i / Cin;
+      const int k = (int)(rk % K), co = (int)(rk / K);
+      grad[((long)co * Cin + ci) * K + k] = v;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ data
 // Batch staging inside the step graph: the step index comes from a device counter, so one captured step is
 // replayed for every batch of a round; the index table [S][B] is refilled in place between rounds.
@@ -1020,6 +1076,16 @@ inline float F(int64_t v) {
   return (float)d;
 }
 
+// ECG_REDUCE_WIDE=0 keeps the 4-split-group weight-gradient reduce (read once; default: the 16-group wide one).
+inline bool reduce_wide() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ECG_REDUCE_WIDE");
+    v = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return v == 1;
+}
+
 // ECG_BN_FIN=ticket selects the single-launch ticketed finalize (fence + last-block reduction); default: two
 // launches.  Read once.
 inline int fin_mode() {
@@ -1051,8 +1117,12 @@ int run_op(const int64_t* o, hipStream_t st) {
     case OP_REDUCE_WGRAD: {
       const long N = o[3] * o[4] * o[5];
       if (N % 256) return ecg::kBadArg;
-      hipLaunchKernelGGL(reduce_wgrad_kernel, dim3((unsigned)(N / 256)), dim3(TPB), 0, st, P<const float>(o[1]), (int)o[2],
-                         (int)o[3], (int)o[4], (int)o[5], P<float>(o[6]));
+      if (reduce_wide())
+        hipLaunchKernelGGL(reduce_wgrad_wide_kernel, dim3((unsigned)(N / 64)), dim3(TPB), 0, st, P<const float>(o[1]),
+                           (int)o[2], (int)o[3], (int)o[4], (int)o[5], P<float>(o[6]));
+      else
+        hipLaunchKernelGGL(reduce_wgrad_kernel, dim3((unsigned)(N / 256)), dim3(TPB), 0, st, P<const float>(o[1]),
+                           (int)o[2], (int)o[3], (int)o[4], (int)o[5], P<float>(o[6]));
       break;
     }
     case OP_BN_FIN: {

@@ -168,6 +168,18 @@ for s in $STEPS; do
       run rocprof_resnet 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_resnet" -o resnet -- \
         python3 bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
       ;;
+    wgrad_ab) run wgrad_ts0 120 env ECG_WGRAD_TS=0 python scripts/wgrad_micro.py
+              for kv in "ECG_WGRAD_TS_NST=4 ECG_WGRAD_TS_WGS=256" "ECG_WGRAD_TS_NST=4 ECG_WGRAD_TS_WGS=512" \
+                        "ECG_WGRAD_TS_NST=3 ECG_WGRAD_TS_WGS=512" "ECG_WGRAD_TS_NST=2 ECG_WGRAD_TS_WGS=512" \
+                        "ECG_WGRAD_TS_NST=4 ECG_WGRAD_TS_WGS=1024"; do
+                run "wgrad_${kv// /_}" 120 env $kv python scripts/wgrad_micro.py
+              done ;;
+    conv_tests) run conv_tests 600 python -u -m pytest tests/test_conv_mc_gpu.py -x -v -p no:cacheprovider --timeout 300 \
+                  --timeout-method thread ;;
+    resnet_ab) for r in a b; do
+                 run resnet_ts1_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+                 run resnet_ts0_$r 300 env ECG_WGRAD_TS=0 ECG_REDUCE_WIDE=0 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+               done ;;
     *) echo "unknown step $s" ;;
   esac
 done

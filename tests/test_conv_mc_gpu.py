@@ -70,6 +70,36 @@ def test_conv1d_nlc_big_tiles(B, L, Cin, Cout, K, s, p):
         set_tile_family(prev)
 
 
+TS_CASES = [  # stride-1 3-tap shapes of the tap-shared weight gradient: chunks spanning samples, ragged last chunk
+    (3, 37, 64, 128),
+    (5, 8, 128, 64),  # L = 8: a sample boundary in every 8-row group
+    (2, 16, 512, 512),
+    (1024, 125, 64, 64),
+    (256, 32, 256, 256),
+]
+
+
+@pytest.mark.parametrize("B,L,Cin,Cout", TS_CASES)
+def test_wgrad_tap_shared_matches_fp64(B, L, Cin, Cout):
+    """The tap-shared weight gradient (one 64x64x3 block per workgroup, taps 0/2 masked at sample boundaries) is
+    an fp32 sum of exact bf16 products: within 1e-4 relative of an fp64 reference on the same bf16 inputs."""
+    from crossscale_ecg.ops import conv_mc
+    lib = conv_mc._lib_k()
+    assert lib.ecg_conv1d_nlc_wgrad_splits(B, L, Cin, L, Cout, 3, 1, 1) > 0, "tap-shared path not selected"
+    torch.manual_seed(3)
+    x = torch.randn(B, L, Cin, device=DEV).bfloat16()
+    dy = torch.randn(B, L, Cout, device=DEV).bfloat16()
+    dw = conv_mc.wgrad_raw(dy, x, 3, 1, 1)  # [Cout][Cin][K] or [Cout][K][Cin] per wgrad_raw's contract
+    xr = x.double().transpose(1, 2)
+    ref = torch.nn.grad.conv1d_weight(xr, (Cout, Cin, 3), dy.double().transpose(1, 2), stride=1, padding=1)
+    got = dw.double()
+    if got.shape != ref.shape:
+        got = got.permute(0, 2, 1)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape
+    assert (got - ref).norm().item() / ref.norm().item() < 1e-4
+
+
 def _grads(m, x, y, amp=False):
     m.zero_grad(set_to_none=True)
     with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
