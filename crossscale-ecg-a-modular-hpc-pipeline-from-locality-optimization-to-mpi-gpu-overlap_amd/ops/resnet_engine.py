@@ -9,9 +9,10 @@ BASELINE.json config 5 (ResNet1D-34 stress, bf16, large batch).  Design (MI355X-
   transposes, no MIOpen), all shapes fixed at construction so every pointer is baked into the plan;
 * every conv is an MFMA implicit GEMM (conv1d_mc.hip) whose epilogue also emits the BatchNorm statistics;
   BN apply / backward passes are fused with ReLU and the residual;
-* backward is laid out in ``segments`` (head+layer4, layer3, layer2, layer1+stem).  The gradients of a
-  segment form one contiguous range of the flat grad buffer, so with ``grad_sync`` each range is all-reduced
-  on a side stream while the next segment's graph runs (the DDP overlap of SURVEY §2 C29 / §7 step 8).
+* backward is laid out in ``segments`` = gradient buckets of ~``bucket_mb`` (default 4 MB, closed at block
+  boundaries; layer1 joins the stem's).  The gradients of a segment form one contiguous range of the flat grad
+  buffer, so each range is all-reduced on a comm stream while the next segment runs (``run_segments``: the DDP
+  overlap of SURVEY §2.4 M5 / §7 step 8).
 
 The reference has no ResNet; parity is against PyTorch's own fp32 ResNet1D (tests/test_resnet_engine_gpu.py).
 """
@@ -42,6 +43,8 @@ def _bind(lib):
         return
     vp, i32 = _lib.vp, _lib.i32
     _lib._sig(lib, "ecg_plan_run", [vp, i32, ctypes.POINTER(ctypes.c_int), vp])
+    _lib._sig(lib, "ecg_plan_run_ex", [vp, i32, ctypes.POINTER(ctypes.c_int), vp, i32, ctypes.POINTER(ctypes.c_void_p)])
+    _lib._sig(lib, "ecg_plan_join", [vp])
     _lib._sig(lib, "ecg_plan_graph_create", [ctypes.POINTER(ctypes.c_void_p), vp, i32, ctypes.POINTER(ctypes.c_int)])
     _lib._sig(lib, "ecg_plan_graph_launch", [vp, vp])
     _lib._sig(lib, "ecg_plan_graph_destroy", [vp])
@@ -87,7 +90,8 @@ class ResNetStepEngine:
     def __init__(self, model: ResNet1D, batch_size: int, seq_len: int = 500, lr: float = 1e-2,
                  momentum: float = 0.9, weight_decay: float = 0.0, nesterov: bool = False, use_graph: bool = True,
                  grad_sync: Optional[Callable[[torch.Tensor], None]] = None,
-                 source: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None):
+                 source: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None,
+                 bucket_mb: Optional[float] = None):
         dev = next(model.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("ResNetStepEngine needs a GPU (HIP kernels)")
@@ -116,6 +120,12 @@ class ResNetStepEngine:
         self._keep: List[torch.Tensor] = []
         self._graphs: Dict[str, int] = {}
         self._range_ops: Dict[Tuple[int, int], torch.Tensor] = {}
+        # gradient buckets: the backward closes a segment after the first block at which the
+        # segment's gradients reach bucket_mb (fp32 bytes), so the first collective starts after layer4's first
+        # block instead of after the whole stage; 0 = one segment per stage (round 2's plan)
+        if bucket_mb is None:
+            bucket_mb = float(os.environ.get("ECG_RESNET_BUCKET_MB", "4"))
+        self.bucket_bytes = int(float(bucket_mb) * (1 << 20))
         self._build()
 
     # ------------------------------------------------------------------------------------------ allocation
@@ -468,10 +478,15 @@ class ResNetStepEngine:
             # BN_BWD_REDUCE) and write din (ReLU-masked for block bi-1; the stem's unmasked pooled gradient at bi=0)
             self._bwd_marks.append((bi, blk_begin, len(ops), dzm, din))
             gcur, nxt = din, dzm
-            if bi == 0 or stage_of[bi - 1] != stage_of[bi]:  # stage boundary: close a grad segment
-                if stage_of[bi] == 0:
-                    break  # layer1 joins the stem segment
-                lo = min(self.space.offset_of(p) for p in blocks[bi].parameters())
+            # close a grad segment: at a stage boundary (bucket_mb = 0), or once the open segment's gradients
+            # reach the bucket size; layer1's blocks join the stem segment either way
+            boundary = bi == 0 or stage_of[bi - 1] != stage_of[bi]
+            if stage_of[bi] == 0:
+                if boundary:
+                    break
+                continue
+            lo = min(self.space.offset_of(p) for p in blocks[bi].parameters())
+            if (boundary and self.bucket_bytes <= 0) or (self.bucket_bytes > 0 and 4 * (seg_hi - lo) >= self.bucket_bytes):
                 self._segments.append((seg_begin, len(ops), lo, seg_hi))
                 seg_begin, seg_hi = len(ops), lo
 
@@ -539,6 +554,43 @@ class ResNetStepEngine:
         self.x.copy_(x.reshape(self.B, self.L), non_blocking=True)
         self.y.copy_(y.reshape(self.B), non_blocking=True)
 
+    def _run_nojoin(self, begin: int, end: int):
+        """Enqueue ops [begin, end) without joining the side lane at the end; returns the side stream (a torch
+        ExternalStream) when the range put work on it, else None."""
+        bad = ctypes.c_int(-1)
+        side = ctypes.c_void_p()
+        st = self.lib.ecg_plan_run_ex(self._ops_ptr(begin), end - begin, ctypes.byref(bad), _lib.stream_ptr(self.dev),
+                                      0, ctypes.byref(side))
+        if st:
+            raise _lib.NativeError(f"resnet plan op {begin + bad.value} failed with status {st}")
+        if not side.value:
+            return None
+        if getattr(self, "_side_ext", None) is None or self._side_ext.cuda_stream != side.value:
+            self._side_ext = torch.cuda.ExternalStream(side.value, device=self.dev)
+        return self._side_ext
+
+    def run_segments(self, on_segment: Callable[[int, int, int, Optional[torch.cuda.Stream]], None]) -> None:
+        """Forward, then the backward one gradient bucket (segment) at a time: ``on_segment(i, lo, hi, side)`` is
+        called once segment i's ops are enqueued, with the flat range [lo, hi) whose gradients they complete.  With
+        the side lane the weight-gradient ops of the segment may still be running on ``side``: the callback orders
+        its consumer (the bucket's all-reduce) after BOTH the current stream and ``side`` - the main stream itself
+        never waits, so the data-gradient chain runs on beside the weight gradients and the collectives.  Ends
+        with the side lane joined into the current stream (before the optimizer)."""
+        first = self._segments[0][0]
+        eager = not (self.use_graph and (not self.side_lane or os.environ.get("ECG_RESNET_SIDE_GRAPH") == "1"))
+        self._exec("fwd", 0, first)
+        for i, (b, e, lo, hi) in enumerate(self._segments):
+            if eager:
+                side = self._run_nojoin(b, e)
+            else:
+                self._exec(f"seg{i}", b, e)
+                side = None
+            on_segment(i, lo, hi, side)
+        if eager and self.side_lane:
+            _lib.check(self.lib.ecg_plan_join(_lib.stream_ptr(self.dev)), "ecg_plan_join")
+        self._loss_steps += 1
+        self._steps_since_sync += 1
+
     def forward_backward(self) -> None:
         """Forward + backward into the flat grad buffer (``grad_sync`` per segment if set)."""
         if self.grad_sync is None:
@@ -568,8 +620,9 @@ class ResNetStepEngine:
     def reset_counter(self) -> None:
         self.counter.zero_()
 
-    def sgd_range(self, lo: int, hi: int) -> None:
-        """SGD on the flat parameter range [lo, hi) only (the per-segment update of ``--overlap tail``)."""
+    def sgd_range(self, lo: int, hi: int, stream=None) -> None:
+        """SGD on the flat parameter range [lo, hi) only (the per-segment update of ``--overlap tail``), on the
+        current stream or ``stream``."""
         key = (lo, hi)
         ops = self._range_ops.get(key)
         if ops is None:
@@ -577,7 +630,8 @@ class ResNetStepEngine:
                  hi - lo, _f(self.lr), _f(self.momentum), _f(self.wd), int(self.nesterov)]
             ops = self._range_ops[key] = torch.tensor([w + [0] * (OP_WORDS - len(w))], dtype=torch.int64)
         bad = ctypes.c_int(-1)
-        st = self.lib.ecg_plan_run(ops.data_ptr(), 1, ctypes.byref(bad), _lib.stream_ptr(self.dev))
+        sp = stream.cuda_stream if stream is not None else _lib.stream_ptr(self.dev)
+        st = self.lib.ecg_plan_run(ops.data_ptr(), 1, ctypes.byref(bad), sp)
         _lib.check(st, "ecg_plan_run(sgd_range)")
 
     def avg_loss(self) -> float:

@@ -95,12 +95,12 @@ def make_trainer(cfg: FedAvgConfig, config_name: str, model, x, y, ctx: DistCont
     if backend == "hip":  # ResNet1D on the native step engine
         from .resnet_trainer import ResNetEngineTrainer
         return ResNetEngineTrainer(model, x, y, cfg.batch_size, cfg.local_steps, lr=cfg.lr, momentum=cfg.momentum,
-                                   seed=seed, ctx=ctx, sync=cfg.sync)
+                                   seed=seed, ctx=ctx, sync=cfg.sync, bucket_mb=cfg.bucket_mb)
     amp = None if config_name == "G0" else _amp(cfg)
     net = model
     if cfg.sync == "ddp" and ctx.distributed:
         from torch.nn.parallel import DistributedDataParallel as DDP
-        net = DDP(model, device_ids=[dev_index(ctx)] if ctx.device.type == "cuda" else None, bucket_cap_mb=4)
+        net = DDP(model, device_ids=[dev_index(ctx)] if ctx.device.type == "cuda" else None, bucket_cap_mb=cfg.bucket_mb)
     return TorchLocalTrainer(net, x, y, cfg.batch_size, lr=cfg.lr, momentum=cfg.momentum, amp_dtype=amp, seed=seed)
 
 

@@ -5,12 +5,15 @@ Same interface as ``TorchLocalTrainer`` / ``FusedTinyTrainer`` (``run_round`` / 
 
 * per round: one ``randperm`` fill of the [S, B] index table, a counter reset, then S replays of the captured
   step graph (batch gather -> forward -> backward -> SGD, all on device; no host work per step);
-* ``sync="ddp"``: synchronous data parallel - each backward segment's gradient range is all-reduced (RCCL AVG,
-  async) as soon as the segment's graph is enqueued, so the reduction of layer4's gradients overlaps the
-  backward of layer3..stem; the SGD op waits on the collectives on the GPU (no host sync);
+* ``sync="ddp"``: synchronous data parallel - the backward runs in gradient buckets of ~``bucket_mb`` (4 MB;
+  ``ResNetStepEngine.run_segments``) and each bucket's gradient range is all-reduced (RCCL AVG, async) from a
+  comm stream ordered after the bucket's ops on BOTH the main stream and the weight-gradient side lane - the
+  main stream never waits, so layer4's first bucket reduces while the rest of the backward runs; the SGD op
+  waits on the collectives on the GPU (no host sync);
 * ``tail_fedavg()``: the ``--overlap tail`` round ending (SURVEY §5.8 mode 2) - the last step's SGD is applied
-  per segment and each segment's updated weights are all-reduced while earlier segments still run backward;
-  the result equals ``none`` FedAvg (all-reduce of the final weights) up to fp32 summation order.
+  per bucket (on the comm stream, after the bucket's gradients are final) and each bucket's updated weights are
+  all-reduced while earlier buckets still run backward; the result equals ``none`` FedAvg (all-reduce of the
+  final weights) up to fp32 summation order.
 """
 from __future__ import annotations
 
@@ -28,7 +31,8 @@ from ..parallel.fedavg import allreduce_mean_
 class ResNetEngineTrainer:
     def __init__(self, model, x: torch.Tensor, y: torch.Tensor, batch_size: int, steps_per_round: int,
                  lr: float = 1e-2, momentum: float = 0.9, weight_decay: float = 0.0, seed: Optional[int] = None,
-                 use_graph: bool = True, ctx: Optional[DistContext] = None, sync: str = "fedavg"):
+                 use_graph: bool = True, ctx: Optional[DistContext] = None, sync: str = "fedavg",
+                 bucket_mb: Optional[float] = None):
         self.model, self.B, self.S = model, batch_size, steps_per_round
         self.ctx = ctx
         self.device = x.device
@@ -40,25 +44,37 @@ class ResNetEngineTrainer:
         ddp = sync == "ddp" and ctx is not None and ctx.distributed
         self.engine = ResNetStepEngine(model, batch_size, x.shape[1], lr=lr, momentum=momentum,
                                        weight_decay=weight_decay, use_graph=use_graph,
-                                       grad_sync=self._grad_sync if ddp else None,
-                                       source=(self.x, self.y32, self.table))
+                                       source=(self.x, self.y32, self.table), bucket_mb=bucket_mb)
+        self.ddp = ddp
+        self._comm = torch.cuda.Stream(device=self.device, priority=-1) if ctx is not None and ctx.distributed \
+            else None
+        self.issue_log: List = []  # (segment, lo, hi) in issue order (tests / timeline)
         self.mom = self.engine.mom
         self.steps_done = 0
 
-    def _grad_sync(self, seg: torch.Tensor) -> None:
-        self._works.append(allreduce_mean_(seg, self.ctx, async_op=True))
+    def _after(self, side) -> torch.cuda.Stream:
+        """The comm stream, ordered after everything enqueued so far on the current stream and on ``side``."""
+        self._comm.wait_stream(torch.cuda.current_stream(self.device))
+        if side is not None:
+            self._comm.wait_stream(side)
+        return self._comm
 
     def _wait(self) -> None:
         for w in self._works:
             if w is not None:
-                w.wait()
+                w.wait()  # the current (main) stream waits for the collective
         self._works.clear()
+        torch.cuda.current_stream(self.device).wait_stream(self._comm)
 
     def _step(self) -> None:
-        if self.engine.grad_sync is None:
+        if not self.ddp:
             self.engine.step()
         else:
-            self.engine.forward_backward()
+            def bucket(i, lo, hi, side):
+                with torch.cuda.stream(self._after(side)):
+                    self.issue_log.append((i, lo, hi))
+                    self._works.append(allreduce_mean_(self.engine.grad[lo:hi], self.ctx, async_op=True))
+            self.engine.run_segments(bucket)
             self._wait()  # stream-side wait on the RCCL collectives, then SGD
             self.engine.apply_update()
         self.steps_done += 1
@@ -94,8 +110,8 @@ class ResNetEngineTrainer:
     run_steps = run_round
 
     def tail_fedavg(self, comm=None, rec=None) -> None:
-        """Run one more local step whose update is applied and all-reduced segment by segment (exact FedAvg of
-        the post-step weights, communication overlapped with the remaining backward).
+        """Run one more local step whose update is applied and all-reduced bucket by bucket (exact FedAvg of the
+        post-step weights, communication overlapped with the remaining backward).
 
         ``comm``/``rec`` (``parallel.overlap.FedAvgComm`` / ``CommRecord``): issue the collectives from the
         timed comm stream so the round records the collectives' span and the compute stream's actual stall."""
@@ -106,20 +122,27 @@ class ResNetEngineTrainer:
         if comm is None:
             from ..parallel.overlap import CommRecord, FedAvgComm
             comm, rec = FedAvgComm(self.ctx), CommRecord()
-        first = eng._segments[0][0]
-        eng._exec("fwd", 0, first)
         pend = []
-        for i, (b, e, lo, hi) in enumerate(eng._segments):
-            eng._exec(f"seg{i}", b, e)
-            eng.sgd_range(lo, hi)
-            pend.append(comm.issue(eng.flat[lo:hi], rec))
-        eng._loss_steps += 1
-        eng._steps_since_sync += 1
+        upd = self._comm if comm.stream is None else comm.stream
+
+        def bucket(i, lo, hi, side):
+            # the bucket's SGD runs on the comm stream once its gradients are final on both lanes; FedAvgComm.issue
+            # orders the all-reduce after the current stream, so issue it from the comm stream itself
+            upd.wait_stream(torch.cuda.current_stream(self.device))
+            if side is not None:
+                upd.wait_stream(side)
+            with torch.cuda.stream(upd):
+                eng.sgd_range(lo, hi, stream=upd)
+                self.issue_log.append((i, lo, hi))
+                pend.append(comm.issue(eng.flat[lo:hi], rec))
+
+        eng.run_segments(bucket)
         # BN running statistics (not touched by SGD) are averaged too, like the flat all-reduce of ``none``
         buf = eng.flat[eng.space.param_numel:]
         if buf.numel():
             pend.append(comm.issue(buf, rec))
         comm.wait(pend, rec)
+        torch.cuda.current_stream(self.device).wait_stream(upd)
         self.steps_done += 1
 
     def avg_loss(self) -> float:

@@ -1374,7 +1374,40 @@ int side_lane(SideLane** out) {
 // Run ``nops`` encoded ops back to back on ``stream`` (side-lane ops on the device's side stream, joined back
 // before LANE_JOIN ops and before returning).  Returns the first failing op's status (ops before it have been
 // enqueued).  ``first_bad`` (optional) receives its index.
+ECG_API int ecg_plan_run_ex(const int64_t* ops, int nops, int* first_bad, hipStream_t stream, int join_end,
+                            hipStream_t* side_out);
+
 ECG_API int ecg_plan_run(const int64_t* ops, int nops, int* first_bad, hipStream_t stream) {
+  return ecg_plan_run_ex(ops, nops, first_bad, stream, 1, nullptr);
+}
+
+// The device's side-lane stream (created on first use): callers that run a plan range with join_end = 0 order
+// their own work (a gradient bucket's all-reduce) after it instead of making the main stream wait.
+ECG_API int ecg_plan_side_stream(hipStream_t* out) {
+  if (!out) return ecg::kBadArg;
+  SideLane* lane = nullptr;
+  const int st = side_lane(&lane);
+  if (st) return st;
+  *out = lane->side;
+  return ecg::kOk;
+}
+
+// Make ``stream`` wait for everything enqueued on the device's side lane so far.
+ECG_API int ecg_plan_join(hipStream_t stream) {
+  SideLane* lane = nullptr;
+  const int st = side_lane(&lane);
+  if (st) return st;
+  ECG_HIP_CHECK(hipEventRecord(lane->join, lane->side));
+  ECG_HIP_CHECK(hipStreamWaitEvent(stream, lane->join, 0));
+  return ecg::kOk;
+}
+
+// ecg_plan_run with the end-of-run join optional: join_end = 0 leaves the range's side-lane work running (the
+// caller joins later with ecg_plan_join, or orders a consumer after the side stream); *side_out (optional) receives
+// the side stream when the range put work on it, else null.  LANE_JOIN ops still join.
+ECG_API int ecg_plan_run_ex(const int64_t* ops, int nops, int* first_bad, hipStream_t stream, int join_end,
+                            hipStream_t* side_out) {
+  if (side_out) *side_out = nullptr;
   if (!ops || nops < 0) return ecg::kBadArg;
   SideLane* lane = nullptr;
   bool side_busy = false, main_ahead = true;  // side has unjoined work / main has work the side has not waited for
@@ -1412,6 +1445,10 @@ ECG_API int ecg_plan_run(const int64_t* ops, int nops, int* first_bad, hipStream
     if (first_bad) *first_bad = bad;
     (void)join();  // leave no side work unjoined (a capture must end with every stream joined)
     return st;
+  }
+  if (!join_end) {
+    if (side_out && side_busy) *side_out = lane->side;
+    return ecg::kOk;
   }
   return join();
 }

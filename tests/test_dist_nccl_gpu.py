@@ -110,14 +110,23 @@ def _tiny_client(ctx, steps):
     return m, FusedTinyTrainer(m, x, y, 64, steps, seed=7 + ctx.rank)
 
 
-def _tiny_fedavg(ctx, mode):
+SPIN = 2_000_000  # GPU cycles (~1 ms) of weight-independent work in each round's preparation
+
+
+def _tiny_fedavg(ctx, mode, spin=0):
     from crossscale_ecg.parallel.overlap import CommRecord, FedAvgComm, FedAvgRound
     m, tr = _tiny_client(ctx, 5)
     comm = FedAvgComm(ctx)
     fr = FedAvgRound(m.flat, comm, mode)
     recs = []
+
+    def prep():
+        tr.prepare_round(5)
+        if spin:
+            torch.cuda._sleep(spin)  # compute-stream work that reads no weights
+
     for _ in range(3):
-        fr.begin_round(prep=lambda: tr.prepare_round(5))
+        fr.begin_round(prep=prep)
         tr.launch_round(5)
         rec = CommRecord()
         fr.end_round(rec)
@@ -134,6 +143,30 @@ def case_tiny_tail_vs_none(ctx):
     a, ta = _tiny_fedavg(ctx, "none")
     b, tb = _tiny_fedavg(ctx, "tail")
     return torch.cat([a, b]), torch.cat([ta, tb])
+
+
+def case_tiny_exposure(ctx):
+    """[comm_ms, exposed_ms] per round for none / tail / delayed with a ~1 ms weight-independent preparation."""
+    return [_tiny_fedavg(ctx, mode, SPIN)[1] for mode in ("none", "tail", "delayed")]
+
+
+def case_resnet_tail_exposure(ctx):
+    """The ResNet per-bucket tail: [comm_ms, exposed_ms] of the tail step's collectives."""
+    from crossscale_ecg.models.resnet1d import resnet1d18
+    from crossscale_ecg.parallel.overlap import CommRecord, FedAvgComm
+    from crossscale_ecg.train.resnet_trainer import ResNetEngineTrainer
+    torch.manual_seed(0)
+    m = resnet1d18().to(ctx.device)
+    x = torch.randn(512, 500, device=ctx.device)
+    y = (x.mean(1) > 0).long()
+    tr = ResNetEngineTrainer(m, x, y, 128, 3, seed=ctx.rank, ctx=ctx, bucket_mb=1.0)
+    tr.run_round(2)
+    comm, rec = FedAvgComm(ctx), CommRecord()
+    tr.tail_fedavg(comm, rec)
+    torch.cuda.synchronize()
+    out = torch.tensor([rec.comm_ms(), rec.exposed_ms(), float(len(tr.issue_log))])
+    tr.close()
+    return out
 
 
 def case_tiny_ddp_round(ctx):
@@ -200,6 +233,25 @@ def test_rccl_tiny_tail_equals_none(world, tmp_path):
         assert torch.equal(w[:P], w[P:])  # tail == none, bit for bit
         assert torch.equal(w[:P], outs[0][0][:P])  # every client holds the averaged model
         assert bool((t >= 0).all())
+
+
+@need2
+def test_rccl_overlap_exposure(tmp_path):
+    """none: the compute stream stalls for the whole collective; tail: the collective runs under the next round's
+    ~1 ms preparation, so the stall is below comm - 0.5 ms; delayed: it runs under a whole local round (~0 stall)."""
+    for none, tail, delayed in _run(2, "case_tiny_exposure", tmp_path):
+        for comm, exposed in none.tolist():
+            assert exposed >= 0.8 * comm - 0.05, (comm, exposed)
+        for comm, exposed in tail[:-1].tolist():  # the last round's collective is drained by finalize()
+            assert exposed <= comm - 0.5, (comm, exposed)
+        for comm, exposed in delayed[1:].tolist():
+            assert comm > 0 and exposed < 0.5 * comm, (comm, exposed)
+
+
+@need2
+def test_rccl_resnet_bucket_tail_exposure(tmp_path):
+    for comm, exposed, buckets in (t.tolist() for t in _run(2, "case_resnet_tail_exposure", tmp_path)):
+        assert buckets > 4 and comm > 0 and exposed < comm, (comm, exposed, buckets)
 
 
 @need2

@@ -364,3 +364,30 @@ def test_engine_bn_tail_matches_separate_finalize(monkeypatch):
     for (n, b), (_, b0) in zip(m.named_buffers(), ref.named_buffers()):
         if b.is_floating_point():
             assert _rel(b, b0) < 1e-5, n
+
+
+@pytest.mark.parametrize("bucket_mb", [0.0, 4.0])
+def test_engine_gradient_buckets(bucket_mb):
+    """Segments (gradient buckets) tile the flat gradient back to front; 4 MB buckets close inside layer4, so the
+    first bucket's all-reduce can start before layer4's backward is over; 0 = one segment per stage."""
+    from crossscale_ecg.models.resnet1d import resnet1d34
+    from crossscale_ecg.ops.resnet_engine import ResNetStepEngine
+    torch.manual_seed(0)
+    m = resnet1d34().to("cuda:0")
+    eng = ResNetStepEngine(m, 16, 500, bucket_mb=bucket_mb)
+    segs = eng._segments
+    hi = eng.space.param_numel
+    for (b, e, lo, h) in segs:
+        assert h == hi and lo < h and b < e
+        hi = lo
+    assert hi == 0
+    ends = {bi: end for (bi, _, end, _, _) in eng._bwd_marks}
+    layer4_end = ends[13]  # ResNet-34 blocks 13..15 form layer4; the backward visits block 13 last
+    if bucket_mb == 0:
+        assert len(segs) == 4
+        assert segs[0][1] == layer4_end
+    else:
+        assert len(segs) > 4
+        assert segs[0][1] < layer4_end  # the first bucket closes before layer4's backward ends
+        assert all(4 * (h - lo) >= bucket_mb * (1 << 20) for (_, _, lo, h) in segs[:-1])
+    eng.close()

@@ -40,7 +40,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, mode, out_dir):
+def _worker(rank, world, port, mode, out_dir, bucket_mb=4.0, tag=""):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")
     import crossscale_ecg  # noqa: F401
@@ -56,7 +56,8 @@ def _worker(rank, world, port, mode, out_dir):
     g.manual_seed(100 + rank)
     x = torch.randn(128, 500, generator=g, device=dev)
     y = (x.mean(1) > 0).long()
-    tr = ResNetEngineTrainer(m, x, y, 16, 3, lr=0.05, seed=rank, ctx=ctx, sync="ddp" if mode == "ddp" else "fedavg")
+    tr = ResNetEngineTrainer(m, x, y, 16, 3, lr=0.05, seed=rank, ctx=ctx, sync="ddp" if mode == "ddp" else "fedavg",
+                             bucket_mb=bucket_mb)
     if mode == "ddp":
         tr.run_round(3)
     elif mode == "tail":
@@ -68,7 +69,9 @@ def _worker(rank, world, port, mode, out_dir):
     torch.cuda.synchronize()
     # DDP keeps BN running statistics per client (like torch DDP without SyncBN): compare parameters only
     keep = m._space.param_numel if mode == "ddp" else m.flat.numel()
-    torch.save(m.flat[:keep].detach().cpu(), os.path.join(out_dir, f"{mode}_{rank}.pt"))
+    torch.save(m.flat[:keep].detach().cpu(), os.path.join(out_dir, f"{mode}{tag}_{rank}.pt"))
+    if rank == 0 and tr.issue_log:
+        torch.save(torch.tensor([list(t) for t in tr.issue_log]), os.path.join(out_dir, f"{mode}{tag}_log.pt"))
     tr.close()
     shutdown_distributed()
 
@@ -89,3 +92,18 @@ def test_tail_equals_none(tmp_path):
     a = torch.load(tmp_path / "tail_0.pt", weights_only=True)
     b = torch.load(tmp_path / "none_0.pt", weights_only=True)
     assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_ddp_buckets_equal_single_allreduce(tmp_path):
+    """Bucketed DDP (~1 MB buckets: many collectives, issued while the backward runs) gives bitwise the weights of
+    one all-reduce of the whole gradient (a bucket larger than the model)."""
+    for tag, mb in (("_b1", 1.0), ("_all", 1e6)):
+        port = _free_port()
+        mp.start_processes(_worker, args=(2, port, "ddp", str(tmp_path), mb, tag), nprocs=2, join=True,
+                           start_method="spawn")
+    a = torch.load(tmp_path / "ddp_b1_0.pt", weights_only=True)
+    b = torch.load(tmp_path / "ddp_all_0.pt", weights_only=True)
+    assert torch.equal(a, b)
+    log_b = torch.load(tmp_path / "ddp_b1_log.pt", weights_only=True)
+    log_all = torch.load(tmp_path / "ddp_all_log.pt", weights_only=True)
+    assert log_all.shape[0] == 3 and log_b.shape[0] > log_all.shape[0]  # 3 steps x 1 bucket vs many
