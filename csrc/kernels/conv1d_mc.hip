@@ -442,12 +442,32 @@ __global__ __launch_bounds__(THREADS, NBUF == 1 ? 3 : 2) void conv1d_nlc_fwd_ker
 // distinct 16-byte slots of the 256-byte bank row.  The DMA writes lane-linear (lane l -> row l/8, chunk l%8 of
 // its 8-row piece), so the XOR is applied to the SOURCE chunk (MI355X guide rule 21).  Padding rows and the M
 // tail use an out-of-range buffer offset: the range check lands zeros.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, long bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+// The LDS-DMA goes through inline asm (buffer_load_dwordx4 ... offen lds, M0 = the wave's LDS destination):
+// after a builtin LDS-DMA hipcc (ROCm 7.2) cannot tell a ring buffer's stages apart and waits vmcnt(0) before the
+// next ds_read of ANY stage, draining every stage kept in flight (it defeated the 3-stage loops below).  From asm
+// the loads are invisible to its wait-count pass: every loop here orders them with explicit (counted) vmcnt
+// waits; compiler-placed waits for its own loads can only over-wait behind them (vmcnt retires in order).
+typedef int srd_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ srd_t make_rsrc(const void* p, long bytes) {
+  const unsigned long a = reinterpret_cast<unsigned long>(p);
+  srd_t r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)(a & 0xffffffffu));
+  r[1] = __builtin_amdgcn_readfirstlane((int)(unsigned)((a >> 32) & 0xffffu));  // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane((int)(bytes < 0x7fff0000L ? bytes : 0x7fff0000L));  // num_records
+  r[3] = 0x00020000;
+  return r;
 }
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned char* lds_piece) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_piece, 16, (int)voff, 0, 0,
-                                           0);
+__device__ __forceinline__ unsigned lds_addr(const unsigned char* p) {
+  return (unsigned)reinterpret_cast<unsigned long>((__attribute__((address_space(3))) const unsigned char*)p);
+}
+// one 16-B piece per lane into LDS at (wave-uniform) lds + 16 * lane; s_nop covers the M0 -> LDS-DMA hazard
+__device__ __forceinline__ void dma16_at(srd_t r, unsigned voff, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r),
+               "s"(__builtin_amdgcn_readfirstlane(lds))
+               : "memory");
+}
+__device__ __forceinline__ void dma16(srd_t r, unsigned voff, unsigned char* lds_piece) {
+  dma16_at(r, voff, lds_addr(lds_piece));
 }
 
 // NWR = waves along M: 2 -> 4 waves (2x2), 4 -> 8 waves (4x2, 2 per SIMD at one workgroup per CU).  256-row
@@ -474,8 +494,8 @@ __global__ __launch_bounds__(128 * NWR, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_d
   // checks that one tile's sample span fits); records are capped below the out-of-range padding offset.
   const int b0 = m0 / a.Lout;
   const long xrem = (long)(a.B - b0) * a.Lin * a.Cin * 2;
-  const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + (long)b0 * a.Lin * a.Cin, xrem < 0x7fff0000L ? xrem : 0x7fff0000L);
-  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, (long)a.Cout * K * 2);
+  const srd_t xr = make_rsrc(a.x + (long)b0 * a.Lin * a.Cin, xrem < 0x7fff0000L ? xrem : 0x7fff0000L);
+  const srd_t wrs = make_rsrc(a.w, (long)a.Cout * K * 2);
   // this lane's rows: piece p = wv + 4*i covers tile rows 8p..8p+7; lane -> row 8p + lane/8, LDS chunk lane%8
   unsigned abase[AP];
   int apos[AP];
@@ -601,7 +621,7 @@ __global__ __launch_bounds__(128 * NWR, 2) void conv1d_nlc_fwd_dma_mt_kernel(Fwd
   const int M = a.B * a.Lout;
   const int ntiles = gm < MT ? (MT - gm + GM - 1) / GM : 0;
   const int total = ntiles * nk;
-  const __amdgpu_buffer_rsrc_t wrs = make_rsrc(a.w, (long)a.Cout * K * 2);
+  const srd_t wrs = make_rsrc(a.w, (long)a.Cout * K * 2);
   unsigned wbase[BP];
 #pragma unroll
   for (int i = 0; i < BP; ++i) {
@@ -611,7 +631,7 @@ __global__ __launch_bounds__(128 * NWR, 2) void conv1d_nlc_fwd_dma_mt_kernel(Fwd
   }
   // addressing of the tile being loaded (rebuilt when the K-step stream crosses into the next tile)
   int lt = -1;
-  __amdgpu_buffer_rsrc_t xr = wrs;
+  srd_t xr = wrs;
   unsigned abase[AP];
   int apos[AP];
   auto setup = [&](int j) {
@@ -1166,8 +1186,8 @@ __global__ __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) void conv1d_nlc_wgrad_
   if (ch0 < ch1) {  // block-uniform
     const int r0 = ch0 * 64, b0 = r0 / a.Lout;
     const long dyrem = (long)(R - r0) * a.Cout * 2, xrem = (long)(a.B - b0) * a.Lin * a.Cin * 2;
-    const __amdgpu_buffer_rsrc_t dyr = make_rsrc(a.dy + (long)r0 * a.Cout, dyrem < 0x7fff0000L ? dyrem : 0x7fff0000L);
-    const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x + (long)b0 * a.Lin * a.Cin, xrem < 0x7fff0000L ? xrem : 0x7fff0000L);
+    const srd_t dyr = make_rsrc(a.dy + (long)r0 * a.Cout, dyrem < 0x7fff0000L ? dyrem : 0x7fff0000L);
+    const srd_t xr = make_rsrc(a.x + (long)b0 * a.Lin * a.Cin, xrem < 0x7fff0000L ? xrem : 0x7fff0000L);
     // this lane's image rows and source chunks (piece p = wv + 4*i covers rows RPP*p .. RPP*p + RPP-1)
     int arow[AP], asrc[BP > AP ? BP : AP], brow[BP];
 #pragma unroll
@@ -1262,29 +1282,6 @@ __global__ __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) void conv1d_nlc_wgrad_
 // Waves: wave w owns ci columns [16w, 16w + 16) for all 64 co and 3 taps (acc[4 co frags][3 taps]).
 __device__ __forceinline__ int tsw(int j) { return 2 * (((j >> 1) & 1) | (((j >> 3) & 1) << 1)); }
 
-// LDS-DMA through inline asm: hipcc (ROCm 7.2) cannot tell a ring buffer's stages apart, so after a builtin
-// buffer_load ... lds it waits vmcnt(0) before the next ds_read of ANY stage - draining the chunks the ring keeps in
-// flight.  Issued from asm the loads are invisible to its wait-count pass; the loop's counted vmcnt waits (the only
-// vector-memory loads in flight there) order them.  M0 = the wave's LDS destination; s_nop covers the M0 -> LDS-DMA
-// hazard.
-typedef int srd_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ srd_t make_srd(const void* p, long bytes) {
-  const unsigned long a = reinterpret_cast<unsigned long>(p);
-  srd_t r;
-  r[0] = (int)(unsigned)(a & 0xffffffffu);
-  r[1] = (int)(unsigned)((a >> 32) & 0xffffu);
-  r[2] = (int)(bytes < 0x7fff0000L ? bytes : 0x7fff0000L);
-  r[3] = 0x00020000;
-  return r;
-}
-__device__ __forceinline__ unsigned lds_addr(const unsigned char* p) {
-  return (unsigned)reinterpret_cast<unsigned long>((__attribute__((address_space(3))) const unsigned char*)p);
-}
-__device__ __forceinline__ void dma16_asm(srd_t srd, unsigned voff, unsigned lds) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(srd), "s"(lds)
-               : "memory", "m0");
-}
-
 constexpr int TSW_DY = 64 * 128;              // dy image bytes per stage
 constexpr int TSW_STAGE = TSW_DY + 72 * 128;  // + x image rows r0-1 .. r0+70 (66 used)
 
@@ -1310,8 +1307,8 @@ __global__ __launch_bounds__(256, 2) void conv1d_nlc_wgrad_ts_kernel(WgradArgs a
 #pragma unroll
     for (int k = 0; k < 3; ++k) acc[i][k] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (ch0 < ch1) {  // block-uniform
-    const srd_t dyr = make_srd(a.dy, (long)R * a.Cout * 2);
-    const srd_t xr = make_srd(a.x, (long)R * a.Cin * 2);
+    const srd_t dyr = make_rsrc(a.dy, (long)R * a.Cout * 2);
+    const srd_t xr = make_rsrc(a.x, (long)R * a.Cin * 2);
     const unsigned lds0 = lds_addr(smem);
     const int prow = lane >> 3;  // row inside an 8-row DMA piece
     // issue: dy pieces wv, wv + 4; x pieces wv, wv + 4, and x piece 8 split over the waves (16 lanes = 2 rows each)
@@ -1323,20 +1320,20 @@ __global__ __launch_bounds__(256, 2) void conv1d_nlc_wgrad_ts_kernel(WgradArgs a
       for (int u = 0; u < 2; ++u) {
         const int p = wv + 4 * u, row = 8 * p + prow, r = r0 + row;
         const int src = (lane & 7) ^ tsw(row);
-        dma16_asm(dyr, r < R ? (unsigned)(((long)r * a.Cout + co0 + src * 8) * 2) : 0x7ffffff0u, dimg + p * 1024);
+        dma16_at(dyr, r < R ? (unsigned)(((long)r * a.Cout + co0 + src * 8) * 2) : 0x7ffffff0u, dimg + p * 1024);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int p = wv + 4 * u, row = 8 * p + prow, r = r0 - 1 + row;
         const int src = (lane & 7) ^ tsw(row);
-        dma16_asm(xr, (r >= 0 && r < R) ? (unsigned)(((long)r * a.Cin + ci0 + src * 8) * 2) : 0x7ffffff0u,
+        dma16_at(xr, (r >= 0 && r < R) ? (unsigned)(((long)r * a.Cin + ci0 + src * 8) * 2) : 0x7ffffff0u,
               ximg + p * 1024);
       }
       {  // piece 8 (rows 64..71): lanes 16w .. 16w + 15 of wave w write rows 64 + 2w, 65 + 2w
         const int row = 64 + prow, r = r0 - 1 + row;
         const int src = (lane & 7) ^ tsw(row);
         if ((lane >> 4) == wv)
-          dma16_asm(xr, (r >= 0 && r < R) ? (unsigned)(((long)r * a.Cin + ci0 + src * 8) * 2) : 0x7ffffff0u,
+          dma16_at(xr, (r >= 0 && r < R) ? (unsigned)(((long)r * a.Cin + ci0 + src * 8) * 2) : 0x7ffffff0u,
                 ximg + 8 * 1024);
       }
     };
@@ -1431,15 +1428,18 @@ __global__ __launch_bounds__(256, 2) void conv1d_nlc_wgrad_ts_kernel(WgradArgs a
 }
 
 // The tap-shared kernel applies (stride 1, pad 1, 3 taps, same length, whole tensors addressable with 32-bit
-// offsets); ECG_WGRAD_TS=0 keeps the one-tap kernels (read once).
+// offsets) up to ECG_WGRAD_TS channels (read once; default 64: measured on MI355X, B=1024 ResNet1D-34 shapes,
+// scripts/wgrad_micro.py, profiles/r3/wgrad_ts_ab.txt - 14.1 vs 21.6 us at 64 channels, where the one-tap path
+// is the register-staged 64x64 kernel; slower than the one-tap 128x128 LDS-DMA kernel at 128-512 channels).
+// 0 disables it.
 inline bool wgrad_ts_ok(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad) {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("ECG_WGRAD_TS");
-    v = (e && atoi(e) == 0) ? 0 : 1;
+    v = e ? atoi(e) : 64;
   }
   const long R = (long)B * Lout;
-  return v == 1 && Kw == 3 && stride == 1 && pad == 1 && Lin == Lout && Lout >= 8 && Cin % 64 == 0 && Cout % 64 == 0 &&
+  return Cin <= v && Cout <= v && Kw == 3 && stride == 1 && pad == 1 && Lin == Lout && Lout >= 8 && Cin % 64 == 0 && Cout % 64 == 0 &&
          R * Cout * 2 < 0x7fff0000L && R * Cin * 2 < 0x7fff0000L;
 }
 

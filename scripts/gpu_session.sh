@@ -180,6 +180,11 @@ for s in $STEPS; do
                  run resnet_ts1_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
                  run resnet_ts0_$r 300 env ECG_WGRAD_TS=0 ECG_REDUCE_WIDE=0 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
                done ;;
+    conv3_ab) for v in 0 1 3; do run conv3_v128_$v 120 env ECG_CONV_V128=$v python scripts/conv_micro.py; done
+              run conv3_nst3 120 env ECG_CONV_NST=3 python scripts/conv_micro.py
+              for kv in "X=0" "ECG_CONV_V128=1" "ECG_CONV_NST=3" "ECG_CONV_V128=1 ECG_CONV_NST=3"; do
+                run "r34_${kv// /_}" 300 env $kv python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+              done ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -233,7 +233,7 @@ def test_engine_ddp_segments_cover_grads():
     eng.forward_backward()
     torch.cuda.synchronize()
     total = sum(n for _, n in calls)
-    assert total == eng.space.param_numel and len(calls) == 4
+    assert total == eng.space.param_numel and len(calls) == len(eng._segments) >= 3
     g_seg = eng.grad.clone()
     eng.grad_sync = None
     eng.forward_backward()
