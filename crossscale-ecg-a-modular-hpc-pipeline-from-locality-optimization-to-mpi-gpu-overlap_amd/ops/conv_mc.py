@@ -38,6 +38,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_set_mt", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_ex", [vp] * 7 + [i32] * 10 + [vp, vp, vp])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles", [_lib.C.c_long, i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_rows", [i32] * 9)
     lib._conv_mc_bound = True
 
 
@@ -74,7 +75,7 @@ def fwd_stats_raw(x: torch.Tensor, w_t: torch.Tensor, stride: int, pad: int, L_o
     Cout, K, _ = w_t.shape
     if not (x.dtype == w_t.dtype == torch.bfloat16 and x.is_contiguous() and w_t.is_contiguous()):
         raise ValueError("conv1d_nlc: contiguous bf16 operands required")
-    rows = stat_rows(B * L_out, Cout)
+    rows = _lib_k().ecg_conv1d_nlc_fwd_stat_rows(B, Lin, Cin, L_out, Cout, K, stride, pad, 1)
     y = torch.empty((B, L_out, Cout), dtype=torch.bfloat16, device=x.device)
     stats = torch.empty((2, rows, Cout), dtype=torch.float32, device=x.device)
     st = _lib_k().ecg_conv1d_nlc_fwd_ex(x.data_ptr(), w_t.data_ptr(), None, y.data_ptr(), stats.data_ptr(), None,

@@ -57,6 +57,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_splits", [i32] * 8)
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles_ex", [i32, i32, i32, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles_fold", [ctypes.c_long, i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_rows", [i32] * 9)
     lib._plan_bound = True
     if lib.ecg_plan_op_words() != OP_WORDS or lib.ecg_plan_wentry_bytes() != 40:
         raise _lib.NativeError("resnet plan ABI mismatch (rebuild csrc)")
@@ -367,18 +368,20 @@ class ResNetStepEngine:
         # partials of its own; the BN_ACT that adds it joins the lanes
         ds_side = side and use_tail
         stats_d = self._t(2 * max_T * 512, dtype=torch.float32) if ds_side else stats
+        rows = lambda Lin, Cin, Lout, Cout, K, s, p, dil=1: self.lib.ecg_conv1d_nlc_fwd_stat_rows(  # noqa: E731
+            B, Lin, Cin, Lout, Cout, K, s, p, dil)  # rows of the epilogue's BN partials for that exact conv
         for (Li, Ci, Lo, Co, s), blk, a, (b1, b2, bd) in zip(shapes, blocks, acts, bns):
-            T = self.lib.ecg_conv1d_nlc_fwd_stat_tiles(B * Lo, Co)  # rows of the epilogue's BN partials
+            Td, T = rows(Li, Ci, Lo, Co, 1, s, 0), rows(Li, Ci, Lo, Co, 3, s, 1)
             if bd is not None and ds_side:
                 conv(xin, Li, Ci, self._wf[id(blk.downsample[0])], a["zd"], Lo, Co, 1, s, 0, st=stats_d,
-                     tail_ptr=tail(T, Co, [fin_fwd_words(bd, B * Lo)]), lane=1)
+                     tail_ptr=tail(Td, Co, [fin_fwd_words(bd, B * Lo)]), lane=1)
             conv(xin, Li, Ci, self._wf[id(blk.conv1)], a["z1"], Lo, Co, 3, s, 1, st=stats,
                  tail_ptr=tail(T, Co, [fin_fwd_words(b1, B * Lo)]))
             if not use_tail:
                 fin_fwd(b1, T, B * Lo)
             fold = bn_fold == 2 or (bn_fold == 1 and Co >= 128)
             op("BN_ACT", 0, P(a["z1"]), P(b1.scale), P(b1.shift), 0, 0, 0, P(a["a1"]), B * Lo, Co, lane=1 if fold else 0)
-            T2 = self.lib.ecg_conv1d_nlc_fwd_stat_tiles_fold(B * Lo, Co) if fold else T
+            T2 = self.lib.ecg_conv1d_nlc_fwd_stat_tiles_fold(B * Lo, Co) if fold else rows(Lo, Co, Lo, Co, 3, 1, 1)
             conv(a["z1"] if fold else a["a1"], Lo, Co, self._wf[id(blk.conv2)], a["z2"], Lo, Co, 3, 1, 1, st=stats,
                  tail_ptr=tail(T2, Co, [fin_fwd_words(b2, B * Lo)]), afold=(b1.scale, b1.shift) if fold else None)
             if not use_tail:
@@ -386,9 +389,9 @@ class ResNetStepEngine:
             if bd is not None:
                 if not ds_side:
                     conv(xin, Li, Ci, self._wf[id(blk.downsample[0])], a["zd"], Lo, Co, 1, s, 0, st=stats,
-                         tail_ptr=tail(T, Co, [fin_fwd_words(bd, B * Lo)]))
+                         tail_ptr=tail(Td, Co, [fin_fwd_words(bd, B * Lo)]))
                 if not use_tail:
-                    fin_fwd(bd, T, B * Lo)
+                    fin_fwd(bd, Td, B * Lo)
                 op("BN_ACT", 2, P(a["z2"]), P(b2.scale), P(b2.shift), P(a["zd"]), P(bd.scale), P(bd.shift),
                    P(a["out"]), B * Lo, Co, lane=2)
             else:
@@ -450,7 +453,7 @@ class ResNetStepEngine:
                P(bd.rstd) if bd else 0, P(bd.scale) if bd else 0, P(bd.c2) if bd else 0, P(dzd), R, Co, apply_rpt)
             wgrad(dz2, a["a1"], Lo, Co, Lo, Co, 3, 1, 1, blk.conv2.weight)
             # dgrad conv2 (stride 1, pad 1) -> ReLU-masked grad wrt a1 + BN1 backward statistics
-            T1 = self.lib.ecg_conv1d_nlc_fwd_stat_tiles(R, Co)
+            T1 = rows(Lo, Co, Lo, Co, 3, 1, 1)
             conv(dz2, Lo, Co, self._wb[id(blk.conv2)], ga1, Lo, Co, 3, 1, 1, st=stats,
                  bnb=(a["a1"], a["z1"], b1.mean, b1.rstd, 0, 0, 0), tail_ptr=tail(T1, Co, [fin_bwd_words(b1, R, 1)]),
                  mbn=(b1.scale, b1.shift))
@@ -466,7 +469,7 @@ class ResNetStepEngine:
                 add = tmp
             if bi > 0:  # din is the previous block's output gradient: mask it and emit that block's BN2 stats
                 pa, (_, pb2, pbd) = acts[bi - 1], bns[bi - 1]
-                Tn = self.lib.ecg_conv1d_nlc_fwd_stat_tiles_ex(B, Li, Ci, s)  # phase-decomposed when s > 1
+                Tn = rows(Lo, Co, Li, Ci, 3, 1, 1, s)  # phase-decomposed when s > 1
                 fins = [fin_bwd_words(pb2, B * Li, 1)] + ([fin_bwd_words(pbd, B * Li, 2)] if pbd else [])
                 conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=add, st=stats_b,
                      bnb=(pa["out"], pa["z2"], pb2.mean, pb2.rstd, pa.get("zd") if pbd else 0,

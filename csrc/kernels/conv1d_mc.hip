@@ -1266,6 +1266,347 @@ __global__ __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) void conv1d_nlc_wgrad_
   wgrad_epilogue<BM, BN, NWR>(a, acc, smem, split, co0, n0);
 }
 
+// ------------------------------------------------------------------ weight-resident tap-shared forward (WR)
+// Stride-1, pad-1, 3-tap convs with C_in in {64, 128, 256} (the forward and the data-grad of every 3-tap conv of a
+// ResNet stage except its strided first one: in_dil 1, Lin == Lout).  One workgroup per CU (4 waves):
+//   * the weights of its BN output channels, all 3 taps x C_in, stay resident in LDS for the workgroup's life
+//     (loaded once; the one-tap kernels restream a weight tile per 64-deep K step of every M tile);
+//   * per 128-row M tile and 64-channel chunk it stages x[m0 - 1, m0 + 135) ONCE (LDS-DMA, 3-stage ring, counted
+//     vmcnt, raw barriers); the 3 taps read that image at row offsets 0, 1, 2.
+// So a CU moves ~17 KB of activations per 128 x BN x 192 MACs instead of 32 KB per 128 x 128 x 64.
+// Orientation out^T[co][m] = W[co][kk] x X^T[kk][m] (A = weights, B = activations): a lane's accumulator holds 4
+// consecutive channels of ONE output row, so the epilogue is 8-byte loads / stores straight from registers and
+// the BatchNorm partials reduce over rows with DPP - the LDS holds only the weights and the activation ring.
+// Sample boundaries: a lane's B fragment is one output row; it is zeroed for tap 0 at t == 0 and for tap 2 at
+// t == L - 1 (the shifted row belongs to the neighbouring sample).
+// Work split: workgroup (gm, nt) of a GM x NT grid owns channels [nt * BN, + BN) and M tiles gm, gm + GM, ...; its
+// statistics accumulate over those tiles into partial row gm of GM (the rows the BatchNorm tail reduces).
+// Weight image: row co = 3 * C_in bf16 (tap-major), padded to a multiple of 256 B; 16-B chunk ch of row co is
+// stored at (ch & ~15) | ((ch & 15) ^ (co & 15)), so the 16 rows x 2 chunk offsets of a ds_read_b128 lane group
+// land on 16 distinct slots.  Activation image: [136 rows][64] bf16, chunk cc of row r at cc ^ ((r >> 1) & 7).
+__device__ __forceinline__ float wr_row16_sum(float v) {  // lane 15 of each 16-lane DPP row ends with the row sum
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
+  return v;
+}
+
+constexpr int WR_BM = 128;
+constexpr int WR_XSTAGE = 136 * 128;  // activation image bytes per stage (rows m0-1 .. m0+134, 130 used)
+
+template <int BN, int NCH>
+struct WrCfg {
+  static constexpr int CIN = 64 * NCH;
+  static constexpr int WROW = (3 * CIN * 2 + 255) / 256 * 256;  // weight-image row bytes
+  static constexpr int W_BYTES = BN * WROW;
+  static constexpr int FI = BN / 16;                             // co fragments per wave
+  static constexpr int SRED_BYTES = 4 * 3 * BN * 4;              // [wave][stat][BN] partials
+  static constexpr int smem(int nst) { return W_BYTES + nst * WR_XSTAGE + SRED_BYTES; }
+};
+
+template <int BN, int NCH, int EPI, int NST>
+__global__ __launch_bounds__(256, 1) void conv1d_nlc_fwd_wr_kernel(FwdArgs a, int MT, int NT, int GM) {
+  using Cfg = WrCfg<BN, NCH>;
+  constexpr int CIN = Cfg::CIN, WROW = Cfg::WROW, FI = Cfg::FI;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* const wimg = smem;
+  unsigned char* const xring = smem + Cfg::W_BYTES;
+  float* const sred = reinterpret_cast<float*>(smem + Cfg::W_BYTES + NST * WR_XSTAGE);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 4, ml = lane & 15;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int gm = wgid / NT, nt = wgid % NT;  // the NT workgroups of one gm (same activation rows) share an XCD
+  const int n0 = nt * BN;
+  const int L = a.Lout;
+  const int M = a.B * L;
+  const int ntiles = gm < MT ? (MT - gm + GM - 1) / GM : 0;
+  const int total = ntiles * NCH;
+  const srd_t xr = make_rsrc(a.x, (long)M * CIN * 2);
+  const unsigned ring0 = lds_addr(xring);
+  const int prow = lane >> 3;
+  // stage s = (tile j, chunk c): rows m0 - 1 + [0, 136) of channels [64c, 64c + 64); 5 DMA instructions per wave
+  auto issue = [&](int s, int st) {
+    const int j = s / NCH, c = s - j * NCH;
+    const int m0 = (gm + j * GM) * WR_BM;
+    const unsigned base = ring0 + st * WR_XSTAGE;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = wv + 4 * u, row = 8 * p + prow, r = m0 - 1 + row;
+      const int src = (lane & 7) ^ ((row >> 1) & 7);
+      dma16_at(xr, (r >= 0 && r < M) ? (unsigned)((r * CIN + c * 64 + src * 8) * 2) : 0x7ffffff0u, base + p * 1024);
+    }
+    {  // piece 16 (rows 128..135): lanes 16w .. 16w + 15 of wave w write rows 128 + 2w, 129 + 2w
+      const int row = 128 + prow, r = m0 - 1 + row;
+      const int src = (lane & 7) ^ ((row >> 1) & 7);
+      if ((lane >> 4) == wv)
+        dma16_at(xr, (r >= 0 && r < M) ? (unsigned)((r * CIN + c * 64 + src * 8) * 2) : 0x7ffffff0u,
+                 base + 16 * 1024);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < NST - 1; ++i)
+    if (i < total) issue(i, i);
+  // resident weights (plain 16-B loads -> swizzled ds_write_b128; once per workgroup)
+  {
+    constexpr int RCH = 3 * CIN / 8;  // 16-B chunks per weight row
+    constexpr int LPT = BN * RCH / 256;
+    static_assert(LPT * 256 == BN * RCH, "weight image must split evenly over the threads");
+    uint4 wv4[LPT];
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int q = tid + 256 * u, co = q / RCH, ch = q - co * RCH;
+      wv4[u] = *reinterpret_cast<const uint4*>(a.w + (long)(n0 + co) * (3 * CIN) + ch * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int q = tid + 256 * u, co = q / RCH, ch = q - co * RCH;
+      const int phys = (ch & ~15) | ((ch & 15) ^ (co & 15));
+      *reinterpret_cast<uint4*>(wimg + co * WROW + phys * 16) = wv4[u];
+    }
+  }
+  __syncthreads();
+  f32x4 acc[FI][2];
+#pragma unroll
+  for (int i = 0; i < FI; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float st1[FI][4], st2[FI][4], st3[FI][4];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) st1[i][q] = st2[i][q] = st3[i][q] = 0.f;
+  const bool ds = EPI == 1 && a.szd != nullptr;
+  bool v0[2] = {true, true}, v2[2] = {true, true};  // this lane's rows: tap 0 / tap 2 inside the sample
+  for (int s = 0; s < total; ++s) {
+    const int ahead = min(NST - 2, total - 1 - s);
+    if constexpr (NST >= 4) {
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (NST == 3) {
+      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + NST - 1 < total) issue(s + NST - 1, (s + NST - 1) % NST);  // into the stage read at s - 1
+    const int j = s / NCH, c = s - j * NCH;
+    const int m0 = (gm + j * GM) * WR_BM;
+    if (c == 0) {
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int m = m0 + 32 * wv + 16 * jj + ml;
+        const int t = m - (m / L) * L;
+        v0[jj] = t != 0;
+        v2[jj] = t != L - 1;
+      }
+    }
+    const unsigned char* ximg = xring + (s % NST) * WR_XSTAGE;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 wf[FI], xf[2];
+        const int ch = k * 8 * NCH + c * 8 + ks * 4 + h;
+#pragma unroll
+        for (int i = 0; i < FI; ++i) {
+          const int co = 16 * i + ml;
+          const int phys = (ch & ~15) | ((ch & 15) ^ (co & 15));
+          wf[i] = *reinterpret_cast<const bf16x8*>(wimg + co * WROW + phys * 16);
+        }
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int row = 32 * wv + 16 * jj + ml + k;
+          const int cc = (ks * 4 + h) ^ ((row >> 1) & 7);
+          uint4 v = *reinterpret_cast<const uint4*>(ximg + row * 128 + cc * 16);
+          const bool ok = k == 1 || (k == 0 ? v0[jj] : v2[jj]);
+          if (!ok) v = make_uint4(0u, 0u, 0u, 0u);
+          xf[jj] = __builtin_bit_cast(bf16x8, v);
+        }
+#pragma unroll
+        for (int i = 0; i < FI; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[jj], acc[i][jj], 0, 0, 0);
+      }
+    }
+    if (c == NCH - 1) {  // tile j complete: epilogue from registers (rows m, 4 channels per lane and fragment)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int m = m0 + 32 * wv + 16 * jj + ml;
+        if (m < M) {
+#pragma unroll
+          for (int i = 0; i < FI; ++i) {
+            const int co = n0 + 16 * i + 4 * h;
+            const long o = (long)m * a.Cout + co;
+            float v[4] = {acc[i][jj][0], acc[i][jj][1], acc[i][jj][2], acc[i][jj][3]};
+            if (a.bias) {
+              const float4 b4 = *reinterpret_cast<const float4*>(a.bias + co);
+              v[0] += b4.x; v[1] += b4.y; v[2] += b4.z; v[3] += b4.w;
+            }
+            if (a.add) {
+              const bf16x4 ad = *reinterpret_cast<const bf16x4*>(a.add + o);
+              if (a.add_mask) {
+                const bf16x4 mk = *reinterpret_cast<const bf16x4*>(a.add_mask + o);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] += (float)mk[e] > 0.f ? (float)ad[e] : 0.f;
+              } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] += (float)ad[e];
+              }
+            }
+            bf16x4 zz;
+            if constexpr (EPI == 1) {
+              zz = *reinterpret_cast<const bf16x4*>(a.sz + o);
+              if (a.mscale != nullptr) {  // the mask the BN_ACT pass stored, recomputed from sz
+                const float4 sc = *reinterpret_cast<const float4*>(a.mscale + co);
+                const float4 sh = *reinterpret_cast<const float4*>(a.mshift + co);
+                const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const __bf16 act = (__bf16)fmaxf(fmaf((float)zz[e], scv[e], shv[e]), 0.f);
+                  v[e] = (float)act > 0.f ? v[e] : 0.f;
+                }
+              } else if (a.smask != nullptr) {
+                const bf16x4 mk = *reinterpret_cast<const bf16x4*>(a.smask + o);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = (float)mk[e] > 0.f ? v[e] : 0.f;
+              }
+            }
+            bf16x4 outv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              if (a.relu) v[e] = fmaxf(v[e], 0.f);
+              outv[e] = (__bf16)v[e];
+              v[e] = (float)outv[e];
+            }
+            *reinterpret_cast<bf16x4*>(a.y + o) = outv;
+            if (a.stats) {
+              if constexpr (EPI == 1) {
+                const float4 mu4 = *reinterpret_cast<const float4*>(a.smean + co);
+                const float4 rs4 = *reinterpret_cast<const float4*>(a.srstd + co);
+                const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, rs[4] = {rs4.x, rs4.y, rs4.z, rs4.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  st1[i][e] += v[e];
+                  st2[i][e] += v[e] * ((float)zz[e] - mu[e]) * rs[e];
+                }
+                if (ds) {
+                  const bf16x4 zd = *reinterpret_cast<const bf16x4*>(a.szd + o);
+                  const float4 md4 = *reinterpret_cast<const float4*>(a.smean_d + co);
+                  const float4 rd4 = *reinterpret_cast<const float4*>(a.srstd_d + co);
+                  const float md[4] = {md4.x, md4.y, md4.z, md4.w}, rd[4] = {rd4.x, rd4.y, rd4.z, rd4.w};
+#pragma unroll
+                  for (int e = 0; e < 4; ++e) st3[i][e] += v[e] * ((float)zd[e] - md[e]) * rd[e];
+                }
+              } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  st1[i][e] += v[e];
+                  st2[i][e] += v[e] * v[e];
+                }
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FI; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // the activation ring is dead from here (bn_tail scratch)
+  if (a.stats) {  // block-uniform
+    const int NS = ds ? 3 : 2;
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float s1 = wr_row16_sum(st1[i][e]), s2 = wr_row16_sum(st2[i][e]);
+        const float s3 = ds ? wr_row16_sum(st3[i][e]) : 0.f;
+        if (ml == 15) {
+          sred[(wv * 3 + 0) * BN + 16 * i + 4 * h + e] = s1;
+          sred[(wv * 3 + 1) * BN + 16 * i + 4 * h + e] = s2;
+          sred[(wv * 3 + 2) * BN + 16 * i + 4 * h + e] = s3;
+        }
+      }
+    __syncthreads();
+    for (int p = tid; p < NS * BN; p += 256) {
+      const int st = p / BN, cl = p - st * BN;
+      const float v = ((sred[(0 * 3 + st) * BN + cl] + sred[(1 * 3 + st) * BN + cl]) + sred[(2 * 3 + st) * BN + cl]) +
+                      sred[(3 * 3 + st) * BN + cl];
+      float* dst = a.stats + ((long)st * GM + gm) * a.Cout + n0 + cl;
+      if (a.tail)
+        ecg::st_sc1(dst, v);  // handed to the tail's last arriver inside this launch (write-through)
+      else
+        *dst = v;
+    }
+    if (a.tail) ecg::bn_tail<256>(a.tail, a.stats, NS, GM, a.Cout, gm, n0, BN, xring);
+  }
+}
+
+// ECG_CONV_WR = largest C_in that takes the weight-resident tap-shared forward (read once; default 0 = off).
+// Measured on MI355X (profiles/r3/conv_wr_ab.txt): in isolation 13.2 vs 15.6 us at 64 channels but 18.2 vs 15.6
+// (128) and 31.7 vs 22.0 (256) - one 4-wave workgroup per CU leaves the LDS-read -> MFMA latency of each k-step
+// exposed - and inside the ResNet1D-34 step 3.84-4.35 vs 3.75-3.77 ms: its CU-filling persistent grid also
+// crowds out the side-lane weight gradients.  Kept as an opt-in variant.
+inline int conv_wr() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ECG_CONV_WR");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+inline int wr_bn(int Cin) { return Cin == 128 ? 128 : 64; }
+inline bool wr_ok(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad, int in_dil) {
+  return Cin <= conv_wr() && Kw == 3 && stride == 1 && pad == 1 && in_dil == 1 && Lin == Lout && Lout >= 2 &&
+         (Cin == 64 || Cin == 128 || Cin == 256) && Cout % wr_bn(Cin) == 0 &&
+         (long)B * Lout * Cin * 2 < 0x7fff0000L;
+}
+// M-tile groups of the WR grid (= BatchNorm partial rows): about one workgroup per CU in all
+inline int wr_groups(long M, int Cout, int Cin) {
+  const int NT = Cout / wr_bn(Cin);
+  const long MT = (M + WR_BM - 1) / WR_BM;
+  long gm = 256 / NT;
+  if (gm < 1) gm = 1;
+  return (int)(gm < MT ? gm : MT);
+}
+
+template <int BN, int NCH, int EPI>
+int launch_fwd_wr_t(const FwdArgs& a, hipStream_t stream) {
+  constexpr int NST = 3;
+  constexpr int SMEM = WrCfg<BN, NCH>::smem(NST);
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_wr_kernel<BN, NCH, EPI, NST>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
+    attr = true;
+  }
+  const long M = (long)a.B * a.Lout;
+  const int MT = (int)((M + WR_BM - 1) / WR_BM), NT = a.Cout / BN;
+  const int GM = wr_groups(M, a.Cout, a.Cin);
+  hipLaunchKernelGGL((conv1d_nlc_fwd_wr_kernel<BN, NCH, EPI, NST>), dim3((unsigned)(GM * NT)), dim3(256), SMEM, stream,
+                     a, MT, NT, GM);
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
+}
+
+int launch_fwd_wr(const FwdArgs& a, hipStream_t stream) {
+  const bool b = a.stat_mode == 1;
+  switch (a.Cin) {
+    case 64: return b ? launch_fwd_wr_t<64, 1, 1>(a, stream) : launch_fwd_wr_t<64, 1, 0>(a, stream);
+    case 128: return b ? launch_fwd_wr_t<128, 2, 1>(a, stream) : launch_fwd_wr_t<128, 2, 0>(a, stream);
+    case 256: return b ? launch_fwd_wr_t<64, 4, 1>(a, stream) : launch_fwd_wr_t<64, 4, 0>(a, stream);
+    default: return ecg::kBadArg;
+  }
+}
+
 // ------------------------------------------------------------------------------ tap-shared weight gradient
 // Stride-1, pad-1, 3-tap convs (Lin == Lout = L, every 3-tap conv of a ResNet stage except its first):
 //   dw[co][k][ci] = sum_r dy[r][co] * x[r + k - 1][ci]   over rows r = (b, t), the shifted row inside sample b.
@@ -1616,6 +1957,7 @@ ECG_API int ecg_conv1d_nlc_fwd_ex2(const void* x, const void* w, const float* bi
   a.ascale = fold_scale;
   a.ashift = fold_shift;
   if (fold_scale) return launch_fwd_fold(a, stream);
+  if (wr_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return launch_fwd_wr(a, stream);
   int bm, bn;
   pick_fwd_tile((long)B * Lout, Cout, in_dil, &bm, &bn);
   if (bm == 256 && bn == 256) return launch_fwd<256, 256>(a, stream);
@@ -1653,6 +1995,15 @@ ECG_API int ecg_conv1d_nlc_fwd_stat_tiles_fold(long M, int Cout) {
   int bm, bn;
   pick_fwd_tile(M, Cout, 2, &bm, &bn);
   return (int)((M + bm - 1) / bm);
+}
+
+// Rows of BatchNorm partials for the kernel that runs this exact conv (any stride / taps / dilation): the
+// weight-resident kernel's M-tile groups where it applies, else the tile-family rows below.
+ECG_API int ecg_conv1d_nlc_fwd_stat_tiles_ex(int B, int Lout, int Cout, int in_dil);
+ECG_API int ecg_conv1d_nlc_fwd_stat_rows(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad,
+                                         int in_dil) {
+  if (wr_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return wr_groups((long)B * Lout, Cout, Cin);
+  return ecg_conv1d_nlc_fwd_stat_tiles_ex(B, Lout, Cout, in_dil);
 }
 
 // Same for a call with batch B, output length Lout and input dilation in_dil (phase-decomposed data-grad).

@@ -1076,12 +1076,15 @@ inline float F(int64_t v) {
   return (float)d;
 }
 
-// ECG_REDUCE_WIDE=0 keeps the 4-split-group weight-gradient reduce (read once; default: the 16-group wide one).
+// ECG_REDUCE_WIDE=1 selects the 16-split-group weight-gradient reduce (read once; default 0: the 4-group one).
+// The wide one is as fast or faster alone (scripts/wgrad_micro.py) but launches 4x the blocks, and on the side lane
+// of the ResNet1D-34 step that costs 0.12 ms/step (3.87 vs 3.75, profiles/r3/resnet_knob_matrix.txt): side-lane
+// kernels must not crowd the data-gradient chain's CUs.
 inline bool reduce_wide() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("ECG_REDUCE_WIDE");
-    v = (e && atoi(e) == 0) ? 0 : 1;
+    v = (e && atoi(e) == 1) ? 1 : 0;
   }
   return v == 1;
 }

@@ -185,6 +185,19 @@ for s in $STEPS; do
               for kv in "X=0" "ECG_CONV_V128=1" "ECG_CONV_NST=3" "ECG_CONV_V128=1 ECG_CONV_NST=3"; do
                 run "r34_${kv// /_}" 300 env $kv python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
               done ;;
+    wr_ab) run conv_wr1 120 python scripts/conv_micro.py
+           run conv_wr0 120 env ECG_CONV_WR=0 python scripts/conv_micro.py
+           for r in a b; do
+             run r34_wr1_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+             run r34_wr0_$r 300 env ECG_CONV_WR=0 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+           done ;;
+    r34_matrix) for r in a b; do
+                  for kv in "ECG_CONV_WR=0 ECG_WGRAD_TS=0 ECG_REDUCE_WIDE=0" "ECG_CONV_WR=0 ECG_WGRAD_TS=0" \
+                            "ECG_CONV_WR=0 ECG_REDUCE_WIDE=0" "ECG_CONV_WR=0" "ECG_CONV_WR=64" \
+                            "ECG_CONV_WR=64 ECG_WGRAD_TS=0 ECG_REDUCE_WIDE=0"; do
+                    run "m_${kv// /_}_$r" 300 env $kv python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+                  done
+                done ;;
     *) echo "unknown step $s" ;;
   esac
 done
