@@ -59,6 +59,14 @@ def _wprep_ptr(precision: str, prefrag: Optional[bool], device, wprep: Optional[
     return w.data_ptr(), w
 
 
+def head_steps_default() -> int:
+    """Steps of a short head graph a PF round is split into (ECG_TINY_HEAD; default 0 = one graph per round).  The
+    idea: the GPU starts on the head while the runtime still submits the long tail graph.  Measured slower at every
+    split (K=20: 11.8-12.0 us/step unsplit vs 12.0-12.2 split; K=500: 10.89 vs 11.20; profiles/r3/
+    tiny_head_split_ab.txt), so it stays an opt-in knob."""
+    return max(0, int(os.environ.get("ECG_TINY_HEAD", "0")))
+
+
 def slab_stride(num_classes: int) -> int:
     return (num_params(num_classes) + 1 + 63) // 64 * 64
 
@@ -201,6 +209,7 @@ class FusedTinyTrainer:
         pf = prefrag_default() if prefrag is None else bool(prefrag)
         self.prefrag = pf and precision == "bf16" and not self.single_launch and not self.persistent
         self.wprep = new_wprep(self.device) if self.prefrag else None
+        self.head = head_steps_default() if self.prefrag else 0
         self.status = torch.zeros(4, dtype=torch.int32, device=self.device)  # sticky give-up code
         self.ws = None
         if self.persistent:
@@ -234,6 +243,29 @@ class FusedTinyTrainer:
         _lib.check(st, "ecg_round_graph_create")
         self._graphs[key] = g
         return g
+
+    def _part_graph(self, n: int, offset: int) -> C.c_void_p:
+        """Graph of steps [offset, offset + n) of a PF round (offset 0: it runs the image-rebuilding first step)."""
+        key = ("part", n, offset, self.idx_stage.data_ptr())
+        g = self._graphs.get(key)
+        if g is not None:
+            return g
+        g = C.c_void_p()
+        torch.cuda.synchronize(self.device)
+        st = _lib.kernels().ecg_round_graph_create_part(
+            C.byref(g), self.x.data_ptr(), self.x.shape[1], self.x.stride(0), self.idx_stage.data_ptr(),
+            self.y32.data_ptr(), self.params.data_ptr(), self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride,
+            self.B, n, self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd, int(self.nesterov),
+            self.wprep.data_ptr(), offset, int(offset > 0))
+        _lib.check(st, "ecg_round_graph_create_part")
+        self._graphs[key] = g
+        return g
+
+    def _round_graphs(self, n: int):
+        """The graphs one replay of an n-step round launches, in order."""
+        if self.prefrag and 0 < self.head < n:
+            return [self._part_graph(self.head, 0), self._part_graph(n - self.head, self.head)]
+        return [self._graph_for(n)]
 
     def _swap_tables(self) -> None:
         """After a PF graph launch: the buffer it read becomes ``idx_table`` (the last round's batches), the other
@@ -305,9 +337,9 @@ class FusedTinyTrainer:
         stream = _lib.stream_ptr(self.device)
         for n in sizes:
             for _ in range(2 if self.prefrag else 1):  # PF: both index buffers
-                g = self._graph_for(n)
-                _lib.check(lib.ecg_round_graph_upload(g, stream), "ecg_round_graph_upload")
-                _lib.check(lib.ecg_round_graph_launch(g, stream), "ecg_round_graph_launch")
+                for g in self._round_graphs(n):
+                    _lib.check(lib.ecg_round_graph_upload(g, stream), "ecg_round_graph_upload")
+                    _lib.check(lib.ecg_round_graph_launch(g, stream), "ecg_round_graph_launch")
                 if self.prefrag:
                     self._swap_tables()
         for t, v in zip(state, snap):
@@ -352,9 +384,9 @@ class FusedTinyTrainer:
             raise RuntimeError("launch_round without prepare_round: no batches staged for this round")
         self._staged = None
         if self.use_graph:
-            g = self._graph_for(n)
-            _lib.check(_lib.kernels().ecg_round_graph_launch(g, _lib.stream_ptr(self.device)),
-                       "ecg_round_graph_launch")
+            stream = _lib.stream_ptr(self.device)
+            for g in self._round_graphs(n):
+                _lib.check(_lib.kernels().ecg_round_graph_launch(g, stream), "ecg_round_graph_launch")
             if self.prefrag:
                 self._swap_tables()
         elif self.prefrag:  # the graph's kernels enqueued from one C++ loop, reading the staged table in place

@@ -1847,7 +1847,7 @@ static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws
                          const float* X, int L, long ldx, const int* idx_table, const int* Y, float* params,
                          float* mom, int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr,
                          float momentum, float wd, int nesterov, int* ctl, float* gslab, const int* idx_stage,
-                         unsigned char* wprep) {
+                         unsigned char* wprep, int step_offset = 0, int image_current = 0) {
   hipStream_t cap;
   ECG_HIP_CHECK(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
   RoundGraph* rg = new RoundGraph();
@@ -1874,10 +1874,12 @@ static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws
   } else if (pa) {
     st = round_dispatch(*pa, ws, ws_bytes, prec, cap);
   } else {
-    for (int s = 0; s < steps && st == 0; ++s)
-      st = train_step(X, L, ldx, tab + (long)s * B, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr,
-                      momentum, wd, nesterov, ctl, gslab, prec, wprep, s == 0 ? 2 : 1, cap,
-                      s + 1 < steps ? tab + (long)(s + 1) * B : nullptr);
+    for (int s = 0; s < steps && st == 0; ++s) {
+      const long row = (long)(step_offset + s) * B;
+      st = train_step(X, L, ldx, tab + row, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr, momentum, wd,
+                      nesterov, ctl, gslab, prec, wprep, (s == 0 && !image_current) ? 2 : 1, cap,
+                      s + 1 < steps ? tab + row + B : nullptr);
+    }
   }
   e = hipStreamEndCapture(cap, &rg->graph);
   (void)hipStreamDestroy(cap);
@@ -1912,6 +1914,23 @@ ECG_API int ecg_round_graph_create(void** handle, const float* X, int L, long ld
   return capture_round(handle, steps, nullptr, nullptr, 0, prec, X, L, ldx, idx_table, Y, params, mom, nc, slab,
                        slab_stride, B, loss_acc, lr, momentum, wd, nesterov, ctl, gslab, idx_stage,
                        static_cast<unsigned char*>(wprep));
+}
+
+// A PF round split in two graphs (``ecg_round_graph_create`` with ``wprep`` and ``idx_stage``): this one captures
+// steps [step_offset, step_offset + steps) of the staged table; ``image_current`` = 1 when an earlier graph of the
+// same round already ran the LDS-path first step that rewrites the PF image.  Launching a short head graph first
+// lets the GPU start while the runtime still submits the long tail graph: a graph's launch latency grows with its
+// node count and sits in front of its first kernel.
+ECG_API int ecg_round_graph_create_part(void** handle, const float* X, int L, long ldx, const int* idx_stage,
+                                        const int* Y, float* params, float* mom, int nc, float* slab, int slab_stride,
+                                        int B, int steps, float* loss_acc, float lr, float momentum, float wd,
+                                        int nesterov, void* wprep, int step_offset, int image_current) {
+  if (!handle || steps <= 0 || step_offset < 0 || !wprep || !idx_stage) return ecg::kBadArg;
+  int st = check_step_args(L, nc, B, slab_stride, 0, false);
+  if (st) return st;
+  return capture_round(handle, steps, nullptr, nullptr, 0, 0, X, L, ldx, idx_stage, Y, params, mom, nc, slab,
+                       slab_stride, B, loss_acc, lr, momentum, wd, nesterov, nullptr, nullptr, idx_stage,
+                       static_cast<unsigned char*>(wprep), step_offset, image_current);
 }
 
 // The persistent round (workspace memset + one launch) captured as a hipGraph, replayed once per round.

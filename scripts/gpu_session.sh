@@ -198,6 +198,10 @@ for s in $STEPS; do
                     run "m_${kv// /_}_$r" 300 env $kv python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
                   done
                 done ;;
+    head_ab) for r in a b c; do for h in 0 1 2 4; do
+               run "head${h}_$r" 300 env ECG_TINY_HEAD=$h python bench.py --steps 20 --warmup 5 --no-extras
+             done; done
+             for h in 0 2; do run "head${h}_500" 300 env ECG_TINY_HEAD=$h python bench.py --steps 500 --warmup 100 --no-extras; done ;;
     *) echo "unknown step $s" ;;
   esac
 done

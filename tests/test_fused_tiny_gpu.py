@@ -316,3 +316,25 @@ def test_prefrag_round_graph_bitwise_equal_lds_eager_with_external_updates(graph
     assert a.avg_loss() == b.avg_loss()
     a.close()
     b.close()
+
+
+def test_split_round_graphs_bitwise_equal_one_graph():
+    """A PF round launched as a short head graph + the tail graph (ECG_TINY_HEAD) == the one-graph round, bit for
+    bit, over full and partial rounds (rounds not longer than the head take the one-graph path)."""
+    from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
+    plan = [7, 1, 2, 3, 7]
+    outs = []
+    for head in (2, 0):
+        dev, x, y, model, _ = _setup(B=128, N=1024)
+        tr = FusedTinyTrainer(model, x, y, 128, 7, seed=13, persistent=False, prefrag=True)
+        tr.head = head
+        tr.prepare(sorted(set(plan)))
+        for i, n in enumerate(plan):
+            tr.run_round(n, reset_loss=False, next_n=plan[i + 1] if i + 1 < len(plan) else None)
+        torch.cuda.synchronize()
+        outs.append((tr.params.clone(), tr.mom.clone(), tr.avg_loss()))
+        if head:
+            assert any(isinstance(k, tuple) and k[0] == "part" for k in tr._graphs)
+        tr.close()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]
