@@ -79,6 +79,9 @@ def _bind_kernels(lib: C.CDLL) -> None:
                                          f32, f32, f32, i32, vp, vp, i32, vp, vp])
     _sig(lib, "ecg_round_graph_create_part", [C.POINTER(vp), vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, i32,
                                               vp, f32, f32, f32, i32, vp, i32, i32])
+    _sig(lib, "ecg_round_graph_create_pf", [C.POINTER(vp), vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, i32,
+                                            vp, f32, f32, f32, i32, vp, i32, i32, vp, vp])
+    _sig(lib, "ecg_tiny_gather_floats", [i32, i32], i64)
     _sig(lib, "ecg_tiny_step_grads_twice", [vp, i32, i64, vp, vp, vp, i32, vp, i32, i32, f32, i32, vp, vp])
     _sig(lib, "ecg_tiny_round_ws_bytes", [i32, i32], i64)
     _sig(lib, "ecg_tiny_round_fits", [i32, i32, i32, i32])

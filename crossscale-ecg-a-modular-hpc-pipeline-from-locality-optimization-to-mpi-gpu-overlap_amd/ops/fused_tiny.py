@@ -67,6 +67,15 @@ def head_steps_default() -> int:
     return max(0, int(os.environ.get("ECG_TINY_HEAD", "0")))
 
 
+def gather_default() -> bool:
+    """PF round graphs gather every step's windows and labels into a contiguous ping-pong buffer inside the
+    previous step's reduce launch (ECG_TINY_GATHER, default 1), so the step kernel stages row b without the
+    dependent idx -> window load (csrc/kernels/tiny_ecg_step.hip GatherArgs).  Measured: step kernel 7.76 -> 7.52
+    us and step period 12.35 -> 12.08 us under the kernel tracer (medians of 687 steps), bench K=500 11.17 -> 11.06
+    us/step (profiles/r3/tiny_gather_ab.txt)."""
+    return os.environ.get("ECG_TINY_GATHER", "1") != "0"
+
+
 def slab_stride(num_classes: int) -> int:
     return (num_params(num_classes) + 1 + 63) // 64 * 64
 
@@ -210,6 +219,12 @@ class FusedTinyTrainer:
         self.prefrag = pf and precision == "bf16" and not self.single_launch and not self.persistent
         self.wprep = new_wprep(self.device) if self.prefrag else None
         self.head = head_steps_default() if self.prefrag else 0
+        self.gather = gather_default() if self.prefrag else False
+        self.xg = self.yg = None
+        if self.gather:
+            self.xg = torch.zeros(lib.ecg_tiny_gather_floats(self.x.shape[1], self.B), dtype=torch.float32,
+                                  device=self.device)
+            self.yg = torch.zeros(2 * self.B, dtype=torch.int32, device=self.device)
         self.status = torch.zeros(4, dtype=torch.int32, device=self.device)  # sticky give-up code
         self.ws = None
         if self.persistent:
@@ -232,6 +247,8 @@ class FusedTinyTrainer:
                 self.y32.data_ptr(), self.params.data_ptr(), self.mom.data_ptr(), self.nc, self.B, n,
                 self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd, int(self.nesterov), self.ws.data_ptr(),
                 self.ws.numel(), self.status.data_ptr(), self.prec, self.idx_stage.data_ptr())
+        elif self.prefrag and self.gather:
+            return self._part_graph(n, 0, key)
         else:
             tab, stage = (self.idx_stage, None) if self.prefrag else (self.idx_table, self.idx_stage)
             st = lib.ecg_round_graph_create(C.byref(g), self.x.data_ptr(), self.x.shape[1], self.x.stride(0),
@@ -244,20 +261,21 @@ class FusedTinyTrainer:
         self._graphs[key] = g
         return g
 
-    def _part_graph(self, n: int, offset: int) -> C.c_void_p:
-        """Graph of steps [offset, offset + n) of a PF round (offset 0: it runs the image-rebuilding first step)."""
-        key = ("part", n, offset, self.idx_stage.data_ptr())
+    def _part_graph(self, n: int, offset: int, key=None) -> C.c_void_p:
+        """Graph of steps [offset, offset + n) of a PF round (offset 0: it runs the image-rebuilding first step),
+        with the next-step gather when ``self.gather``."""
+        key = key or ("part", n, offset, self.idx_stage.data_ptr())
         g = self._graphs.get(key)
         if g is not None:
             return g
         g = C.c_void_p()
         torch.cuda.synchronize(self.device)
-        st = _lib.kernels().ecg_round_graph_create_part(
+        st = _lib.kernels().ecg_round_graph_create_pf(
             C.byref(g), self.x.data_ptr(), self.x.shape[1], self.x.stride(0), self.idx_stage.data_ptr(),
             self.y32.data_ptr(), self.params.data_ptr(), self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride,
             self.B, n, self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd, int(self.nesterov),
-            self.wprep.data_ptr(), offset, int(offset > 0))
-        _lib.check(st, "ecg_round_graph_create_part")
+            self.wprep.data_ptr(), offset, int(offset > 0), _lib.ptr(self.xg), _lib.ptr(self.yg))
+        _lib.check(st, "ecg_round_graph_create_pf")
         self._graphs[key] = g
         return g
 

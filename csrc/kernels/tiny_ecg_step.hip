@@ -19,6 +19,8 @@
 // Precision: bf16 MFMA operands, fp32 accumulation, fp32 master weights/optimizer state (native bf16 AMP).
 #include "../include/ecg_common.h"
 
+#include <climits>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -1140,12 +1142,53 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
 // order (fixed by RED_ROWG and the chunking below), so every width gives bitwise-identical results.
 constexpr int kRedColsDefault = 32;
 constexpr int RED_ROWG = 16;
+
+// Next-step gather riding on the reduce launch (ECG_TINY_GATHER): blocks >= nred copy the windows and labels of
+// the NEXT step's batch (idx) into a contiguous buffer xg [B][ldg] / yg [B], so that step's kernel stages row b
+// directly - its phase 0 loses the dependent idx -> window round trip.  The reduce blocks are latency-bound
+// (46 blocks on 256 CUs), so the copy runs beside them on otherwise idle CUs instead of as a launch of its own
+// (a separate pre-gather node was measured slower in round 1: profiles/r1_round_kernel/ab_pregather.log).
+struct GatherArgs {
+  const float* X;
+  long ldx;
+  const int* idx;  // [B] dataset rows of the next step
+  const int* Y;
+  float* xg;       // [B][ldg] written write-through
+  int* yg;         // [B]
+  int L, ldg, B, vec;  // vec: 16-byte rows (L % 4 == 0, ldx % 4 == 0, X 16-byte aligned)
+  int nred;            // blocks below this index reduce; INT_MAX = no gather
+};
+__host__ __device__ inline int gather_rows_per_block(int L, int vec, int nt) {
+  const int per_row = vec ? L / 4 : L;
+  return per_row >= nt ? 1 : nt / per_row;
+}
+
 template <int RED_COLS>
 __global__ __launch_bounds__(RED_COLS * RED_ROWG) void slab_reduce_sgd_kernel(
     const float* __restrict__ slab, int G, int stride, int P,
     float* __restrict__ params, float* __restrict__ mom, float* __restrict__ grad_out,
     float* __restrict__ loss_acc, float lr, float momentum, float wd, int nesterov, int apply,
-    unsigned char* __restrict__ wprep) {  // wprep: PF image kept current with the updated parameters (nullable)
+    unsigned char* __restrict__ wprep,  // wprep: PF image kept current with the updated parameters (nullable)
+    GatherArgs ga) {
+  constexpr int NT = RED_COLS * RED_ROWG;
+  if ((int)blockIdx.x >= ga.nred) {  // block-uniform: gather blocks never reach the barrier below
+    const int per_row = ga.vec ? ga.L / 4 : ga.L;
+    const int rpb = gather_rows_per_block(ga.L, ga.vec, NT);
+    const int r0 = ((int)blockIdx.x - ga.nred) * rpb;
+    const __amdgpu_buffer_rsrc_t xr = make_rsrc(ga.xg, (long)ga.B * ga.ldg * 4);
+    for (int e = threadIdx.x; e < rpb * per_row; e += NT) {
+      const int lr_ = e / per_row, j = e - lr_ * per_row, b = r0 + lr_;
+      if (b >= ga.B) break;  // e only grows, so every later e is past the batch too
+      const long row = ga.idx[b];
+      if (ga.vec) {
+        st_wt4(xr, b * ga.ldg + 4 * j, *reinterpret_cast<const f32x4*>(ga.X + row * ga.ldx + 4 * j));
+      } else {
+        st_wt(xr, b * ga.ldg + j, ga.X[row * ga.ldx + j]);
+      }
+      if (j == 0) ga.yg[b] = ga.Y[row];
+    }
+    return;
+  }
   __shared__ float part[RED_ROWG][RED_COLS + 1];
   const int cl = threadIdx.x % RED_COLS, rg = threadIdx.x / RED_COLS;
   const int col = blockIdx.x * RED_COLS + cl;
@@ -1550,7 +1593,7 @@ FusedOpt no_fuse() {
 
 int reduce_dispatch(const float* slab, int G, int stride, int P, float* params, float* mom, float* grad_out,
                     float* loss_acc, float lr, float momentum, float wd, int nesterov, int apply,
-                    unsigned char* wprep, hipStream_t stream) {
+                    unsigned char* wprep, hipStream_t stream, const GatherArgs* gather = nullptr) {
   if (G <= 0 || P <= 0 || stride < P + 1) return ecg::kBadArg;
   if (apply && (!params || (momentum != 0.f && !mom))) return ecg::kBadArg;
   static const int cols = [] {  // ECG_RED_COLS in {4, 8, 16, 32, 64}: columns per reduction block (A/B knob)
@@ -1563,21 +1606,29 @@ int reduce_dispatch(const float* slab, int G, int stride, int P, float* params, 
     hipLaunchKernelGGL(ablate_kernel, dim3(blocks), dim3(cols * RED_ROWG), 0, stream, nullptr);
     return ecg::kOk;
   }
+  GatherArgs ga{};
+  ga.nred = INT_MAX;
+  int grid = blocks;
+  if (gather) {
+    ga = *gather;
+    ga.nred = blocks;
+    const int rpb = gather_rows_per_block(ga.L, ga.vec, cols * RED_ROWG);
+    grid += (ga.B + rpb - 1) / rpb;
+  }
+#define ECG_RED_LAUNCH(NC)                                                                                       \
+  hipLaunchKernelGGL(slab_reduce_sgd_kernel<NC>, dim3(grid), dim3(NC * RED_ROWG), 0, stream, slab, G, stride, P, \
+                     params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply, wprep, ga)
   if (cols == 4)
-    hipLaunchKernelGGL(slab_reduce_sgd_kernel<4>, dim3(blocks), dim3(4 * RED_ROWG), 0, stream, slab, G, stride, P,
-                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply, wprep);
+    ECG_RED_LAUNCH(4);
   else if (cols == 8)
-    hipLaunchKernelGGL(slab_reduce_sgd_kernel<8>, dim3(blocks), dim3(8 * RED_ROWG), 0, stream, slab, G, stride, P,
-                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply, wprep);
+    ECG_RED_LAUNCH(8);
   else if (cols == 64)
-    hipLaunchKernelGGL(slab_reduce_sgd_kernel<64>, dim3(blocks), dim3(64 * RED_ROWG), 0, stream, slab, G, stride, P,
-                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply, wprep);
+    ECG_RED_LAUNCH(64);
   else if (cols == 32)
-    hipLaunchKernelGGL(slab_reduce_sgd_kernel<32>, dim3(blocks), dim3(32 * RED_ROWG), 0, stream, slab, G, stride, P,
-                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply, wprep);
+    ECG_RED_LAUNCH(32);
   else
-    hipLaunchKernelGGL(slab_reduce_sgd_kernel<16>, dim3(blocks), dim3(16 * RED_ROWG), 0, stream, slab, G, stride, P,
-                       params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply, wprep);
+    ECG_RED_LAUNCH(16);
+#undef ECG_RED_LAUNCH
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
@@ -1761,7 +1812,7 @@ ECG_API int ecg_slab_reduce_sgd(const float* slab, int G, int stride, int P, flo
 static int train_step(const float* X, int L, long ldx, const int* idx, const int* Y, float* params, float* mom,
                       int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr, float momentum, float wd,
                       int nesterov, int* ctl, float* gslab, int prec, unsigned char* wprep, int image,
-                      hipStream_t stream, const int* idx_next = nullptr) {
+                      hipStream_t stream, const int* idx_next = nullptr, const GatherArgs* gather = nullptr) {
   if (ctl) {
     if (wprep) return ecg::kBadArg;
     FusedOpt o{ctl, gslab, params, mom, loss_acc, lr, momentum, wd, nesterov, B};
@@ -1783,7 +1834,7 @@ static int train_step(const float* X, int L, long ldx, const int* idx, const int
                      image == 2 ? nullptr : wprep, stream);
   if (st) return st;
   return reduce_dispatch(slab, B, slab_stride, make_layout(nc).P, params, mom, nullptr, loss_acc, lr, momentum, wd,
-                         nesterov, 1, wprep, stream);
+                         nesterov, 1, wprep, stream, gather);
 }
 
 // Full training step.  With ``ctl``/``gslab`` (see ecg_tiny_ctl_ints) it is ONE launch: per-sample
@@ -1847,7 +1898,8 @@ static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws
                          const float* X, int L, long ldx, const int* idx_table, const int* Y, float* params,
                          float* mom, int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr,
                          float momentum, float wd, int nesterov, int* ctl, float* gslab, const int* idx_stage,
-                         unsigned char* wprep, int step_offset = 0, int image_current = 0) {
+                         unsigned char* wprep, int step_offset = 0, int image_current = 0, float* xg = nullptr,
+                         int* yg = nullptr) {
   hipStream_t cap;
   ECG_HIP_CHECK(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
   RoundGraph* rg = new RoundGraph();
@@ -1874,11 +1926,25 @@ static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws
   } else if (pa) {
     st = round_dispatch(*pa, ws, ws_bytes, prec, cap);
   } else {
+    // Gathered steps (xg/yg): step s > 0 reads ping-pong buffer s & 1, which the reduce launch of step s - 1 filled
+    // (stream order: that buffer's previous reader, step s - 2's kernel, finished before that reduce started).
+    const int ldg = (L + 3) / 4 * 4;
+    GatherArgs ga{X, ldx, nullptr, Y, nullptr, nullptr, L, ldg, B,
+                  (L % 4 == 0 && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 16 == 0) ? 1 : 0, INT_MAX};
     for (int s = 0; s < steps && st == 0; ++s) {
       const long row = (long)(step_offset + s) * B;
-      st = train_step(X, L, ldx, tab + row, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr, momentum, wd,
-                      nesterov, ctl, gslab, prec, wprep, (s == 0 && !image_current) ? 2 : 1, cap,
-                      s + 1 < steps ? tab + row + B : nullptr);
+      const bool gathered = xg && s > 0;
+      const bool gather_next = xg && s + 1 < steps;
+      if (gather_next) {
+        ga.idx = tab + row + B;
+        ga.xg = xg + (long)((s + 1) & 1) * B * ldg;
+        ga.yg = yg + (long)((s + 1) & 1) * B;
+      }
+      st = train_step(gathered ? xg + (long)(s & 1) * B * ldg : X, L, gathered ? (long)ldg : ldx,
+                      gathered ? nullptr : tab + row, gathered ? yg + (long)(s & 1) * B : Y, params, mom, nc, slab,
+                      slab_stride, B, loss_acc, lr, momentum, wd, nesterov, ctl, gslab, prec, wprep,
+                      (s == 0 && !image_current) ? 2 : 1, cap, s + 1 < steps ? tab + row + B : nullptr,
+                      gather_next ? &ga : nullptr);
     }
   }
   e = hipStreamEndCapture(cap, &rg->graph);
@@ -1921,17 +1987,33 @@ ECG_API int ecg_round_graph_create(void** handle, const float* X, int L, long ld
 // same round already ran the LDS-path first step that rewrites the PF image.  Launching a short head graph first
 // lets the GPU start while the runtime still submits the long tail graph: a graph's launch latency grows with its
 // node count and sits in front of its first kernel.
-ECG_API int ecg_round_graph_create_part(void** handle, const float* X, int L, long ldx, const int* idx_stage,
-                                        const int* Y, float* params, float* mom, int nc, float* slab, int slab_stride,
-                                        int B, int steps, float* loss_acc, float lr, float momentum, float wd,
-                                        int nesterov, void* wprep, int step_offset, int image_current) {
-  if (!handle || steps <= 0 || step_offset < 0 || !wprep || !idx_stage) return ecg::kBadArg;
+// ``xg``/``yg`` (optional, both or neither): ping-pong gather buffers, floats [2][B][round_up(L, 4)] and int32
+// [2][B] (ecg_tiny_gather_floats): every step after the round's first reads its batch from the buffer its
+// predecessor's reduce launch gathered (see GatherArgs) - bitwise the same step on the same data.
+ECG_API int ecg_round_graph_create_pf(void** handle, const float* X, int L, long ldx, const int* idx_stage,
+                                      const int* Y, float* params, float* mom, int nc, float* slab, int slab_stride,
+                                      int B, int steps, float* loss_acc, float lr, float momentum, float wd,
+                                      int nesterov, void* wprep, int step_offset, int image_current, float* xg,
+                                      int* yg) {
+  if (!handle || steps <= 0 || step_offset < 0 || !wprep || !idx_stage || (!xg) != (!yg)) return ecg::kBadArg;
   int st = check_step_args(L, nc, B, slab_stride, 0, false);
   if (st) return st;
   return capture_round(handle, steps, nullptr, nullptr, 0, 0, X, L, ldx, idx_stage, Y, params, mom, nc, slab,
                        slab_stride, B, loss_acc, lr, momentum, wd, nesterov, nullptr, nullptr, idx_stage,
-                       static_cast<unsigned char*>(wprep), step_offset, image_current);
+                       static_cast<unsigned char*>(wprep), step_offset, image_current, xg, yg);
 }
+
+ECG_API int ecg_round_graph_create_part(void** handle, const float* X, int L, long ldx, const int* idx_stage,
+                                        const int* Y, float* params, float* mom, int nc, float* slab, int slab_stride,
+                                        int B, int steps, float* loss_acc, float lr, float momentum, float wd,
+                                        int nesterov, void* wprep, int step_offset, int image_current) {
+  return ecg_round_graph_create_pf(handle, X, L, ldx, idx_stage, Y, params, mom, nc, slab, slab_stride, B, steps,
+                                   loss_acc, lr, momentum, wd, nesterov, wprep, step_offset, image_current, nullptr,
+                                   nullptr);
+}
+
+// Floats of the gather buffer ``xg`` of ecg_round_graph_create_pf (its ``yg`` holds 2 * B int32).
+ECG_API long ecg_tiny_gather_floats(int L, int B) { return 2L * B * ((L + 3) / 4 * 4); }
 
 // The persistent round (workspace memset + one launch) captured as a hipGraph, replayed once per round.
 ECG_API int ecg_round_graph_create_persistent(void** handle, const float* X, int L, long ldx, const int* idx_table,

@@ -202,6 +202,38 @@ for s in $STEPS; do
                run "head${h}_$r" 300 env ECG_TINY_HEAD=$h python bench.py --steps 20 --warmup 5 --no-extras
              done; done
              for h in 0 2; do run "head${h}_500" 300 env ECG_TINY_HEAD=$h python bench.py --steps 500 --warmup 100 --no-extras; done ;;
+    gather_ab) for r in a b c; do for g in 0 1; do
+                 run "gather${g}_$r" 300 env ECG_TINY_GATHER=$g python bench.py --steps 20 --warmup 5 --no-extras
+               done; done
+               for g in 0 1; do run "gather${g}_500" 300 env ECG_TINY_GATHER=$g python bench.py --steps 500 --warmup 100 --no-extras; done ;;
+    tiny_tests) run tiny_tests 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_fused_tiny_gpu.py ;;
+    m1reps) R=gpurun_out/r3mod; mkdir -p $R
+            run module1_r5 1100 python bench_locality.py --batch-sizes 64 128 256 512 --iters 100 --num-workers 4 \
+              --shard-dir /tmp/ecg_shards --results-dir $R --reps 5 ;;
+    m1pin) R=gpurun_out/r3mod_pin; mkdir -p $R
+           run module1_pin_r5 1100 python bench_locality.py --batch-sizes 64 128 256 512 --iters 100 --num-workers 4 \
+             --shard-dir /tmp/ecg_shards --results-dir $R --reps 5 --pin-thread ;;
+    m23) R=gpurun_out/r3mod; mkdir -p $R
+         run module2 600 python benchmark_part_2.py --results-dir $R --batch-scaling
+         run pseudo_fl 600 python part3_mpi_gpu_train.py --steps 200 --synthetic-windows 20000 \
+           --results-csv $R/part3_mpi_cuda_results.csv --quiet
+         run fedavg1 600 python part3_fedavg_overlap_mpi_gpu.py --synthetic-windows 20000 --rounds 5 \
+           --local-steps 50 --config both --results-csv $R/fedavg_results_w1.csv ;;
+    prof_gather) export TMPDIR=/tmp
+      for g in 0 1; do
+        export ECG_TINY_GATHER=$g
+        run prof_gather$g 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_gather$g" -o run -- \
+          python3 bench.py --steps 500 --warmup 100 --no-extras
+      done
+      unset ECG_TINY_GATHER ;;
+    prof_resnet) export TMPDIR=/tmp
+      run prof_resnet 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_resnet" -o run -- \
+        python3 bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras ;;
+    kscan) run kscan_l3 300 python scripts/conv_kscan.py 1024 32 256
+           run kscan_l4 300 python scripts/conv_kscan.py 1024 16 512
+           run kscan_l2 300 python scripts/conv_kscan.py 1024 63 128
+           run kscan_l3_v1 300 env ECG_CONV_V128=1 python scripts/conv_kscan.py 1024 32 256
+           run kscan_l3_v2 300 env ECG_CONV_V128=2 python scripts/conv_kscan.py 1024 32 256 ;;
     *) echo "unknown step $s" ;;
   esac
 done

@@ -338,3 +338,34 @@ def test_split_round_graphs_bitwise_equal_one_graph():
         tr.close()
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     assert outs[0][2] == outs[1][2]
+
+
+@pytest.mark.parametrize("L,B", [(500, 128), (250, 96)])  # 16-byte rows / scalar rows (L % 4 != 0)
+def test_gather_round_graph_bitwise_equal_plain(L, B):
+    """PF round graphs whose reduce launches gather the next step's windows and labels (ECG_TINY_GATHER) == the
+    plain PF graph and the eager C++ step loop, bit for bit, over full and partial rounds (1-step rounds gather
+    nothing; odd and even step counts end on either ping-pong buffer)."""
+    from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
+    plan = [7, 1, 2, 3, 7, 4]
+    outs = []
+    for gather, graph in ((True, True), (False, True), (False, False)):
+        dev, x, y, model, _ = _setup(B=B, L=L, N=1024, nc=5)
+        tr = FusedTinyTrainer(model, x, y, B, 7, seed=21, persistent=False, prefrag=True, use_graph=graph)
+        tr.gather = gather
+        if gather and tr.xg is None:
+            tr.xg = torch.zeros(2 * B * ((L + 3) // 4 * 4), dtype=torch.float32, device=dev)
+            tr.yg = torch.zeros(2 * B, dtype=torch.int32, device=dev)
+        tr.prepare(sorted(set(plan)))
+        for i, n in enumerate(plan):
+            tr.run_round(n, reset_loss=False, next_n=plan[i + 1] if i + 1 < len(plan) else None)
+        torch.cuda.synchronize()
+        outs.append((tr.params.clone(), tr.mom.clone(), tr.avg_loss()))
+        if gather:  # the last round (4 steps) ran its step 3 on buffer 1, gathered from that step's batch rows
+            rows = tr.idx_table[3].long()
+            ldg = (L + 3) // 4 * 4
+            assert torch.equal(tr.yg[B:], tr.y32[rows])
+            assert torch.equal(tr.xg.view(2, B, ldg)[1, :, :L], tr.x[rows])
+        tr.close()
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0]) and torch.equal(outs[0][1], o[1])
+        assert outs[0][2] == o[2]

@@ -1,0 +1,39 @@
+"""README <-> CSV consistency: the module-result rows of README.md are exactly what
+crossscale_ecg.report.readme renders from the CSV directory the block names, and that directory is the newest
+committed profiles/rN/modules."""
+import os
+
+from crossscale_ecg.report import readme
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_readme_module_rows_match_csvs():
+    ok, expected, found = readme.check(os.path.join(ROOT, "README.md"), root=ROOT)
+    assert ok, "README module block is stale; run `python -m crossscale_ecg.report.readme --write`\n" + expected
+
+
+def test_readme_block_cites_newest_modules_dir():
+    with open(os.path.join(ROOT, "README.md")) as f:
+        block = readme._split(f.read())[1]
+    assert f"<!-- source: {readme.latest_modules_dir(ROOT)} -->" in block
+
+
+def test_render_marks_bar_and_spread(tmp_path):
+    """A synthetic CSV pair: the A3 bar is judged per batch size and the IQR columns are quoted when present."""
+    d = tmp_path / "modules"
+    d.mkdir()
+    hdr = "config,batch_size,pin_memory,contiguous,non_blocking,data_ms,h2d_ms,compute_ms,step_ms,samples_per_s," \
+          "samples_per_s_q1,samples_per_s_q3,reps\n"
+    rows = []
+    for b, a0, a3 in ((64, 100e3, 120e3), (128, 200e3, 210e3)):
+        for cfg, v in (("A0_baseline", a0), ("A1_contiguous", a0), ("A2_contig_pinned", a0),
+                       ("A3_contig_pinned_nb", a3)):
+            rows.append(f"{cfg},{b},0,0,0,0,0,0,0,{v},{v * 0.9},{v * 1.1},5\n")
+    (d / "part1_locality_results.csv").write_text(hdr + "".join(rows))
+    (d / "part2_hip_results.csv").write_text(
+        "batch_size,kernel_size,torch_ms_median,hip_ms_median,speedup_med\n64,3,0.04,0.01,4.0\n64,5,0.045,0.01,4.5\n")
+    row = readme.module1_row(str(d))
+    assert "+20 % (B=64)" in row and "+5 % (B=128)" in row and "bar at B=64." in row
+    assert "Medians of 5 interleaved repetitions" in row and "B=64 90–110 / 90–110 / 108–132" in row
+    assert "**4.00–4.50×**" in readme.module2_row(str(d))
