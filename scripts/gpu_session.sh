@@ -234,6 +234,19 @@ for s in $STEPS; do
            run kscan_l2 300 python scripts/conv_kscan.py 1024 63 128
            run kscan_l3_v1 300 env ECG_CONV_V128=1 python scripts/conv_kscan.py 1024 32 256
            run kscan_l3_v2 300 env ECG_CONV_V128=2 python scripts/conv_kscan.py 1024 32 256 ;;
+    epi_ab) run resnet_tests_epi 600 python -u -m pytest tests/test_resnet_engine_gpu.py tests/test_conv_mc_gpu.py \
+              -x -q -p no:cacheprovider --timeout 300 --timeout-method thread
+            for r in a b c; do
+              run "resnet_epi_$r" 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+            done
+            run op_profile 300 python scripts/resnet_op_profile.py 34 1024
+            export TMPDIR=/tmp
+            run prof_resnet_tl 400 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof_resnet3" -o run -- \
+              python3 bench.py --model resnet1d34 --steps 10 --warmup 3 --no-extras
+            export ECG_BN_TAIL=0
+            run prof_resnet_tail0 400 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof_resnet3_tail0" -o run -- \
+              python3 bench.py --model resnet1d34 --steps 10 --warmup 3 --no-extras
+            unset ECG_BN_TAIL ;;
     *) echo "unknown step $s" ;;
   esac
 done
