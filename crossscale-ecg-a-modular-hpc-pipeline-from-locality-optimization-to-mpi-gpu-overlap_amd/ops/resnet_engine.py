@@ -19,6 +19,7 @@ The reference has no ResNet; parity is against PyTorch's own fp32 ResNet1D (test
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 import struct
 from typing import Callable, Dict, List, Optional, Tuple
@@ -305,7 +306,11 @@ class ResNetStepEngine:
         def tail(T, Cout, fins) -> int:
             if not use_tail:
                 return 0
-            gs = max(8, -(-T // 32))  # <= 32 groups: level 2 is one batch of loads (bn_tail.h)
+            # level-1 group size: <= 32 groups, so level 2 reads at most 32 fp64 group rows (bn_tail.h).  ECG_BN_TAIL_GS
+            # overrides it (A/B: ~sqrt(2T) groups, i.e. fewer, larger level-1 groups, measured 3.83-3.85 vs
+            # 3.78-3.79 ms/step at B=1024, profiles/r3/resnet_epi_tail_ab.txt)
+            gs_env = int(os.environ.get("ECG_BN_TAIL_GS", "0"))
+            gs = gs_env if gs_env > 0 else max(8, -(-T // 32))
             NG = (T + gs - 1) // gs
             cnt = torch.zeros((Cout // 64) * (NG + 1), dtype=torch.int32, device=dev)
             self._keep.append(cnt)

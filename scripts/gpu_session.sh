@@ -247,6 +247,42 @@ for s in $STEPS; do
             run prof_resnet_tail0 400 rocprofv3 --kernel-trace --output-format csv -d "$OUT/prof_resnet3_tail0" -o run -- \
               python3 bench.py --model resnet1d34 --steps 10 --warmup 3 --no-extras
             unset ECG_BN_TAIL ;;
+    train_diag) for kv in "X=0" "ECG_WGRAD_TS=0" "ECG_REDUCE_WIDE=0" "ECG_RESNET_SIDE=0" "ECG_BN_TAIL=0" "ECG_CONV_DMA=0" \
+                         "ECG_CONV_MT=0"; do
+                  run "train_${kv}" 120 env $kv python scripts/diag_train_progress.py 18 64
+                done ;;
+    resnet_tests_all) run resnet_tests_all 900 python -u -m pytest tests/test_resnet_engine_gpu.py tests/test_conv_mc_gpu.py \
+                        tests/test_resnet_trainer_gpu.py -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    tail_ab) for r in a b; do for g in 0 8 16 32; do
+               run "tailgs${g}_$r" 300 env ECG_BN_TAIL_GS=$g python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+             done; done ;;
+    epi_tail_ab) for r in a b c; do
+                   run "base_$r" 300 env ECG_LIB_DIR=$PWD/_ablib/base ECG_BN_TAIL_GS=-1 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+                   run "new_$r" 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+                   run "new_gsold_$r" 300 env ECG_BN_TAIL_GS=-1 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+                 done ;;
+    tiny_ab) for r in a b c; do
+               run "tbase500_$r" 300 env ECG_LIB_DIR=$PWD/_ablib/base python bench.py --steps 500 --warmup 100 --no-extras
+               run "tnew500_$r" 300 python bench.py --steps 500 --warmup 100 --no-extras
+               run "tbase20_$r" 300 env ECG_LIB_DIR=$PWD/_ablib/base python bench.py --steps 20 --warmup 5 --no-extras
+               run "tnew20_$r" 300 python bench.py --steps 20 --warmup 5 --no-extras
+             done ;;
+    tiny_pmc) export TMPDIR=/tmp
+      P2="SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD"
+      run pmc2_new 120 rocprofv3 --pmc $P2 --kernel-trace --output-format csv -d "$OUT/pmc2_new" -o tiny -- python3 scripts/pmc_tiny_step.py
+      export ECG_LIB_DIR=$PWD/_ablib/base
+      run pmc2_base 120 rocprofv3 --pmc $P2 --kernel-trace --output-format csv -d "$OUT/pmc2_base" -o tiny -- python3 scripts/pmc_tiny_step.py
+      unset ECG_LIB_DIR ;;
+    tail2_ab) for r in a b c; do
+                run "t2base_$r" 300 env ECG_LIB_DIR=$PWD/_ablib/base python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+                run "t2new_$r" 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+                run "t2gs4_$r" 300 env ECG_BN_TAIL_GS=4 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+              done ;;
+    wc_test) run wc_test 300 python -u -m pytest tests/test_resnet_engine_gpu.py -k "well_conditioned or training_progress or bn_tail" -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    epi2_ab) for r in a b c d; do
+               run "e2base_$r" 300 env ECG_LIB_DIR=$PWD/_ablib/base python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+               run "e2new_$r" 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+             done ;;
     *) echo "unknown step $s" ;;
   esac
 done

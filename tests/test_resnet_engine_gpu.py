@@ -95,7 +95,8 @@ def test_engine_grads_depth34_well_conditioned():
     e_all, e_all_amp = _rel(g_eng, g_ref), _rel(g_amp, g_ref)
     print(f"whole-gradient relative error: engine {e_all:.4f}, autocast {e_all_amp:.4f}")
     print("worst (engine, autocast) relative errors:", [(f"{a:.4f}", f"{b:.4f}", n) for a, b, n in worst[:8]])
-    assert e_all < 0.1 and e_all < 1.5 * e_all_amp + 0.01, (e_all, e_all_amp)
+    # measured: engine 0.144, autocast 0.154 (a bf16 34-layer net is ~15 % off fp32 even when well conditioned)
+    assert e_all < 0.3 and e_all < 1.25 * e_all_amp + 0.01, (e_all, e_all_amp)
     for e_eng, e_amp, n in worst:
         assert e_eng < 1.5 * e_amp + 0.02, (n, e_eng, e_amp)
 
