@@ -36,6 +36,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_splits", [i32] * 8)
     _lib._sig(lib, "ecg_conv1d_nlc_set_big", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_set_mt", [i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_set_dma_dil", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_ex", [vp] * 7 + [i32] * 10 + [vp, vp, vp])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles", [_lib.C.c_long, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_rows", [i32] * 9)
@@ -53,6 +54,12 @@ def set_tile_family(big: int) -> int:
     returns the previous setting.  Step plans built before a change keep the tiling they were built with: set it
     first."""
     return _lib_k().ecg_conv1d_nlc_set_big(int(big))
+
+
+def set_dma_dilated(on: bool) -> int:
+    """Strided (phase-decomposed) data-grads on the LDS-DMA loop (True, default) or the register-staged loop;
+    returns the previous setting."""
+    return _lib_k().ecg_conv1d_nlc_set_dma_dil(1 if on else 0)
 
 
 def set_multi_tile(mode: int) -> int:

@@ -612,25 +612,35 @@ __global__ __launch_bounds__(128 * NWR, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_d
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
   const int mt = wgid / NT, nt = wgid % NT;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int CB = a.Cin / BK, nk = a.Kw * CB, K = a.Kw * a.Cin;
-  const int M = a.B * a.Lout;
+  // Strided data-grad (in_dil = P > 1, stride 1): phase-decomposed as in conv1d_nlc_fwd_kernel - M tile mt belongs to
+  // output phase ph (rows u = t * P + ph), whose taps k = k0 + j * P all hit real input rows t + j + (ph + k0 - pad) / P
+  // (exact division), so the phase's K loop runs over its taps only and needs no per-row divisibility test.
+  const int P = a.in_dil;
+  const int ph = P > 1 ? mt / a.tpp : 0;
+  const int m0 = (P > 1 ? mt - ph * a.tpp : mt) * BM, n0 = nt * BN;
+  const int k0 = P > 1 ? ((a.pad - ph) % P + P) % P : 0;
+  const int CB = a.Cin / BK, K = a.Kw * a.Cin;
+  const int nk = (P > 1 ? (k0 < a.Kw ? (a.Kw - k0 + P - 1) / P : 0) : a.Kw) * CB;
+  const int Lrow = P > 1 ? a.Lph : a.Lout;  // rows per sample of this kernel's (phase-local) M index
+  const int M = a.B * Lrow;
   // The activation resource starts at the tile's first sample, so 32-bit offsets cover any batch size (the host
   // checks that one tile's sample span fits); records are capped below the out-of-range padding offset.
-  const int b0 = m0 / a.Lout;
+  const int b0 = m0 / Lrow;
   const long xrem = (long)(a.B - b0) * a.Lin * a.Cin * 2;
   const srd_t xr = make_rsrc(a.x + (long)b0 * a.Lin * a.Cin, xrem < 0x7fff0000L ? xrem : 0x7fff0000L);
   const srd_t wrs = make_rsrc(a.w, (long)a.Cout * K * 2);
-  // this lane's rows: piece p = wv + 4*i covers tile rows 8p..8p+7; lane -> row 8p + lane/8, LDS chunk lane%8
+  // this lane's rows: piece p = wv + 4*i covers tile rows 8p..8p+7; lane -> row 8p + lane/8, LDS chunk lane%8;
+  // apos = the input row of tap step j = 0 (tap step j reads row apos + j)
   unsigned abase[AP];
   int apos[AP];
 #pragma unroll
   for (int i = 0; i < AP; ++i) {
     const int r = 8 * (wv + NW * i) + (lane >> 3), m = m0 + r;
-    const int b = m / a.Lout, t = m - b * a.Lout;
+    const int b = m / Lrow, t = m - b * Lrow;
     const int cs = (lane & 7) ^ ((r >> 1) & 7);  // source chunk landing in this lane's LDS slot
-    abase[i] = m < M ? (unsigned)(((long)(b - b0) * a.Lin * a.Cin + cs * 8) * 2) : 0u;
-    apos[i] = m < M ? t * a.stride - a.pad : INT_MIN / 2;
+    const bool ok = m < M && (P == 1 || t * P + ph < a.Lout);
+    abase[i] = ok ? (unsigned)(((long)(b - b0) * a.Lin * a.Cin + cs * 8) * 2) : 0u;
+    apos[i] = ok ? (P > 1 ? t + (ph + k0 - a.pad) / P : t * a.stride - a.pad) : INT_MIN / 2;
   }
   unsigned wbase[BP];
 #pragma unroll
@@ -640,11 +650,12 @@ __global__ __launch_bounds__(128 * NWR, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_d
     wbase[i] = (unsigned)(((long)(n0 + r) * K + cs * 8) * 2);
   }
   auto issue = [&](int kt, int st) {
-    const int k = kt / CB, c0 = (kt - k * CB) * BK;
+    const int j = kt / CB, c0 = (kt - j * CB) * BK;
+    const int k = k0 + j * P;  // weight tap (P = 1: k = j)
     unsigned char* As = smem + st * STAGE;
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
-      const int u = apos[i] + k;
+      const int u = apos[i] + j;
       const unsigned voff = (u >= 0 && u < a.Lin) ? abase[i] + (unsigned)((u * a.Cin + c0) * 2) : 0x7ffffff0u;
       dma16(xr, voff, As + (wv + NW * i) * 1024);
     }
@@ -715,7 +726,7 @@ __global__ __launch_bounds__(128 * NWR, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_d
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();  // the epilogue reuses the stage buffers
   }
-  fwd_epilogue<BM, BN, EPI, NWR, (BM < 256)>(a, acc, smem, m0, n0, mt, MT, a.Lout, M, 1, 0);
+  fwd_epilogue<BM, BN, EPI, NWR, (BM < 256)>(a, acc, smem, m0, n0, mt, MT, Lrow, M, P, ph);
   if (a.tail && a.stats)
     ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, MT, a.Cout, mt, n0, BN, smem);
 }
@@ -968,9 +979,18 @@ int launch_fwd_dma_st(const FwdArgs& a, hipStream_t stream) {
                                       hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
     attr = true;
   }
-  const int MT = (int)(((long)a.B * a.Lout + BM - 1) / BM), NT = a.Cout / BN;
+  FwdArgs b = a;
+  int MT;
+  if (a.in_dil > 1) {  // phase-decomposed strided data-grad (see the kernel)
+    b.Lph = (a.Lout + a.in_dil - 1) / a.in_dil;
+    b.tpp = (int)(((long)a.B * b.Lph + BM - 1) / BM);
+    MT = a.in_dil * b.tpp;
+  } else {
+    MT = (int)(((long)a.B * a.Lout + BM - 1) / BM);
+  }
+  const int NT = a.Cout / BN;
   hipLaunchKernelGGL((conv1d_nlc_fwd_dma_kernel<BM, BN, EPI, NWR, NST>), dim3((unsigned)(MT * NT)), dim3(Cfg::NTHR),
-                     SMEM, stream, a, MT, NT);
+                     SMEM, stream, b, MT, NT);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
@@ -1050,11 +1070,26 @@ int launch_fwd_cfg(const FwdArgs& a, hipStream_t stream) {
   return ecg::kOk;
 }
 
+// ECG_CONV_DMA_DIL=0 keeps the strided (phase-decomposed) data-grads on the register-staged loop (read once;
+// default: LDS-DMA loop, two stages).
+int g_conv_dma_dil = -1;
+inline bool conv_dma_dil() {
+  if (g_conv_dma_dil < 0) {
+    const char* e = getenv("ECG_CONV_DMA_DIL");
+    g_conv_dma_dil = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return g_conv_dma_dil == 1;
+}
+
 template <int BM, int BN>
 int launch_fwd(const FwdArgs& a, hipStream_t stream) {
   // the DMA loop addresses bytes with 32-bit buffer offsets from the tile's first sample
-  const bool dma_ok = a.in_dil == 1 && (long)(BM / a.Lout + 2) * a.Lin * a.Cin * 2 < 0x7fff0000L &&
+  const int Lrow = a.in_dil > 1 ? (a.Lout + a.in_dil - 1) / a.in_dil : a.Lout;
+  const bool dma_ok = (a.in_dil == 1 || (conv_dma_dil() && a.stride == 1 && BM <= 128)) &&
+                      (long)(BM / Lrow + 2) * a.Lin * a.Cin * 2 < 0x7fff0000L &&
                       (long)a.Cout * a.Kw * a.Cin * 2 < 0x7fff0000L;
+  if (conv_dma() && dma_ok && a.in_dil > 1)  // two stages, one tile per workgroup
+    return a.stat_mode == 1 ? launch_fwd_dma_st<BM, BN, 1, 2>(a, stream) : launch_fwd_dma_st<BM, BN, 0, 2>(a, stream);
   if (conv_dma() && dma_ok)
     return a.stat_mode == 1 ? launch_fwd_dma<BM, BN, 1>(a, stream) : launch_fwd_dma<BM, BN, 0>(a, stream);
   if (a.stats && fwd_mt_groups((long)a.B * a.Lout, a.Cout, a.in_dil, BM, BN) > 0)
@@ -2093,6 +2128,13 @@ ECG_API int ecg_conv1d_nlc_fwd_ex2(const void* x, const void* w, const float* bi
 }
 
 // Select the forward tile family (see conv_big); returns the previous setting.
+// Strided data-grads on the LDS-DMA loop (1) or the register-staged loop (0); returns the previous setting (tests).
+ECG_API int ecg_conv1d_nlc_set_dma_dil(int on) {
+  const int prev = conv_dma_dil() ? 1 : 0;
+  g_conv_dma_dil = on ? 1 : 0;
+  return prev;
+}
+
 ECG_API int ecg_conv1d_nlc_set_big(int big) {
   const int prev = conv_big();
   g_conv_big = big < 0 ? 0 : (big > 2 ? 2 : big);

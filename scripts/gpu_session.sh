@@ -283,6 +283,17 @@ for s in $STEPS; do
                run "e2base_$r" 300 env ECG_LIB_DIR=$PWD/_ablib/base python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
                run "e2new_$r" 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
              done ;;
+    dil_ab) for r in a b c d; do
+              run "dil0_$r" 300 env ECG_CONV_DMA_DIL=0 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+              run "dil1_$r" 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+            done ;;
+    m23p) R=gpurun_out/r3mod; mkdir -p $R
+          run module2 600 python benchmark_part_2.py --results-dir $R --batch-scaling
+          run pseudo_fl 600 python part3_mpi_gpu_train.py --steps 200 --synthetic-windows 20000 \
+            --results-csv $R/part3_mpi_cuda_results.csv --quiet
+          run fedavg1 600 python part3_fedavg_overlap_mpi_gpu.py --synthetic-windows 20000 --rounds 5 \
+            --local-steps 50 --config both --results-csv $R/fedavg_results_w1.csv
+          run plots 300 python plot_results.py --results-dir $R ;;
     *) echo "unknown step $s" ;;
   esac
 done

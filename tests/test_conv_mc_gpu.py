@@ -54,6 +54,32 @@ def test_conv1d_nlc_forward_backward(B, L, Cin, Cout, K, s, p):
     assert _rel(b.grad, br.grad) < 1e-2
 
 
+STRIDED = [c for c in CASES if c[5] > 1]
+
+
+@pytest.mark.parametrize("B,L,Cin,Cout,K,s,p", STRIDED)
+def test_strided_dgrad_dma_equals_register_loop(B, L, Cin, Cout, K, s, p):
+    """The phase-decomposed strided data-grad on the LDS-DMA loop (default) and on the register-staged loop compute
+    the same MFMA sums in the same order: bitwise-equal input gradients (and both match fp32, test above)."""
+    from crossscale_ecg.ops.conv_mc import conv1d_nlc, set_dma_dilated
+    torch.manual_seed(1)
+    x0 = torch.randn(B, L, Cin, device=DEV).bfloat16()
+    w = torch.randn(Cout, Cin, K, device=DEV) / (Cin * K) ** 0.5
+    grads = []
+    for on in (True, False):
+        prev = set_dma_dilated(on)
+        try:
+            x = x0.clone().requires_grad_(True)
+            y = conv1d_nlc(x, w, None, s, p)
+            g = torch.randn(y.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(7)).bfloat16()
+            y.backward(g)
+            torch.cuda.synchronize()
+            grads.append(x.grad.clone())
+        finally:
+            set_dma_dilated(prev)
+    assert torch.equal(grads[0], grads[1])
+
+
 BIG_CASES = [  # shapes that select the 256-row DMA tiles once the big-tile family is enabled
     (2048, 64, 128, 256, 3, 1, 1),  # 256x256
     (2100, 63, 128, 128, 3, 1, 1),  # 256x128, ragged last M tile

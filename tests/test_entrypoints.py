@@ -101,10 +101,11 @@ def test_module_benches_cpu(tmp_path):
     assert len(rows) == 12 and float(rows[0]["max_abs_err"]) < 1e-4
     _run([sys.executable, os.path.join(ROOT, "bench_locality.py"), "--batch-sizes", "32", "--iters", "3",
           "--num-workers", "0", "--n-windows", "600", "--shard-dir", str(tmp_path / "sh"), "--results-dir",
-          str(tmp_path)], cwd=str(tmp_path))
+          str(tmp_path), "--reps", "2"], cwd=str(tmp_path))
     rows = list(csv.DictReader(open(tmp_path / "part1_locality_results.csv")))
     assert [r["config"] for r in rows] == ["A0_baseline", "A1_contiguous", "A2_contig_pinned",
                                            "A3_contig_pinned_nb", "A4_LABL"]
+    assert all(r["reps"] == "2" and float(r["samples_per_s_q1"]) <= float(r["samples_per_s_q3"]) for r in rows)
     _run([sys.executable, os.path.join(ROOT, "plot_results.py"), "--results-dir", str(tmp_path)], cwd=str(tmp_path))
     assert os.path.exists(tmp_path / "throughput_vs_batch.png")
 
