@@ -294,6 +294,12 @@ for s in $STEPS; do
           run fedavg1 600 python part3_fedavg_overlap_mpi_gpu.py --synthetic-windows 20000 --rounds 5 \
             --local-steps 50 --config both --results-csv $R/fedavg_results_w1.csv
           run plots 300 python plot_results.py --results-dir $R ;;
+    lib_ab) LIBB=${LIBB:-nnan}; for r in a b c d; do
+              run "lb_cur500_$r" 300 python bench.py --steps 500 --warmup 100 --no-extras
+              run "lb_${LIBB}500_$r" 300 env ECG_LIB_DIR=$PWD/_ablib/$LIBB python bench.py --steps 500 --warmup 100 --no-extras
+              run "lb_cur20_$r" 300 python bench.py --steps 20 --warmup 5 --no-extras
+              run "lb_${LIBB}20_$r" 300 env ECG_LIB_DIR=$PWD/_ablib/$LIBB python bench.py --steps 20 --warmup 5 --no-extras
+            done ;;
     *) echo "unknown step $s" ;;
   esac
 done
