@@ -41,6 +41,11 @@ def hipcc() -> str:
 
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
              "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+# Per-source extra flags.  The fused TinyECG step is VALU-issue bound (four 16-wave phases per SIMD share one
+# vector issue port): without NaN / signed-zero semantics hipcc drops the canonicalising v_max before every ReLU and
+# the 0 + x seeds of the running sums (-95 static VALU of ~1,800) - 11.02 -> 10.86 us/step at K=500
+# (profiles/r3/tiny_fp_flags_ab.txt).  ReLU of a NaN is 0 either way (v_max_f32 returns the non-NaN operand).
+FILE_FLAGS = {"tiny_ecg_step.hip": ["-fno-honor-nans", "-fno-signed-zeros"]}
 CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-pthread"]
 
 
@@ -74,13 +79,14 @@ def build_kernels(force: bool, jobs: int, extra: List[str]) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "include", "*.h")))
     target = os.path.join(LIBDIR, "libecg_kernels.so")
-    dig = _digest(srcs + hdrs, HIP_FLAGS + extra)
+    dig = _digest(srcs + hdrs, HIP_FLAGS + extra + sorted(f"{k}:{' '.join(v)}" for k, v in FILE_FLAGS.items()))
     if not force and _up_to_date(target, dig):
         return target
     os.makedirs(OBJDIR, exist_ok=True)
     objs = [os.path.join(OBJDIR, os.path.basename(s) + ".o") for s in srcs]
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        futs = [ex.submit(_run, [hipcc(), *HIP_FLAGS, *extra, "-I", os.path.join(CSRC, "include"), "-c", s, "-o", o])
+        futs = [ex.submit(_run, [hipcc(), *HIP_FLAGS, *FILE_FLAGS.get(os.path.basename(s), []), *extra, "-I",
+                                 os.path.join(CSRC, "include"), "-c", s, "-o", o])
                 for s, o in zip(srcs, objs)]
         for f in futs:
             f.result()

@@ -82,7 +82,7 @@ struct FusedOpt {
 };
 // conv2 wgrad work split: 5 taps x msplit(WAVES) pair ranges, one (tap, range) per wave 1.. (wave 0 runs the head)
 __host__ __device__ constexpr int msplit(int waves) { return (waves - 1) / 5 < 1 ? 1 : (waves - 1) / 5; }
-__host__ __device__ constexpr int red_cnt(int waves) { return RED_POOL + waves * 16; }      // [WAVES][16] relu'(h2) counts
+__host__ __device__ constexpr int red_cnt(int waves) { return RED_POOL + waves * 16; }      // relu'(h2) counts: [msplit][16] (bf16), [WAVES][16] (fp32)
 __host__ __device__ constexpr int red_m(int waves) { return red_cnt(waves) + waves * 16; }  // [msplit][16*16*5] M partials
 __host__ __device__ constexpr int red_dw1(int waves) { return red_m(waves) + msplit(waves) * 1280; }  // [WAVES][16][8]
 __host__ __device__ constexpr int red_head(int waves) { return red_dw1(waves) + waves * 128; }  // dWh, dbh, loss
@@ -272,9 +272,9 @@ struct TinySample {
     for (int s = 0; s < 3; ++s) pf_wf[s] = *reinterpret_cast<const bf16x8*>(wb + WP_FRAGF + (s * 64 + lane) * 8);
   }
   __device__ __forceinline__ void pf_load_dgrad(const unsigned char* __restrict__ wp) {
+    // only waves 0..2 scale the dgrad fragments (dgrad()): wave w loads set s = w into pf_wd[0]
     const __bf16* wb = reinterpret_cast<const __bf16*>(wp);
-#pragma unroll
-    for (int s = 0; s < 3; ++s) pf_wd[s] = *reinterpret_cast<const bf16x8*>(wb + WP_FRAGD + (s * 64 + lane) * 8);
+    if (w < 3) pf_wd[0] = *reinterpret_cast<const bf16x8*>(wb + WP_FRAGD + (w * 64 + lane) * 8);
   }
 
   __device__ __forceinline__ TinySample(unsigned char* smem, int L_, int nc_)
@@ -477,7 +477,7 @@ struct TinySample {
       // B[(k,ci)][co] or A[co][(k,ci)]), B = h1col[(k,ci)][t] read straight from the [t][ci] rows.  The K padding
       // (tap 5) carries the bias: B rows r = 80..95 are the constant {1, 0, ...} (quarter 2) / 0 (quarter 3).
       bf16x8 Wf[3];
-      float pool[4], cnt[4];
+      float pool[4];
       if constexpr (PF) {
 #pragma unroll
         for (int s = 0; s < 3; ++s) Wf[s] = pf_wf[s];
@@ -490,7 +490,7 @@ struct TinySample {
       for (int j = 0; j < 8; ++j) Bone[j] = ecg::to_bf16(0.f);
       if (h == 2) Bone[0] = ecg::to_bf16(1.f);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) pool[i] = cnt[i] = 0.f;
+      for (int i = 0; i < 4; ++i) pool[i] = 0.f;
 #pragma unroll
       for (int pi = 0; pi < MAX_PAIRS_PER_WAVE; ++pi) {
         const int pair = w + pi * WAVES;
@@ -528,7 +528,6 @@ struct TinySample {
                 const float v = tv ? fmaxf(accs[half][i], 0.f) : 0.f;
                 const bool on = v > 0.f;
                 pool[i] += v;
-                cnt[i] += on ? 1.f : 0.f;
                 mk[i] = ecg::to_bf16(on ? 1.f : 0.f);
               }
               *reinterpret_cast<bf16x4*>(ms + (t + 4) * C + 4 * h) = mk;
@@ -541,16 +540,11 @@ struct TinySample {
         }
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        pool[i] = row16_sum(pool[i]);
-        cnt[i] = row16_sum(cnt[i]);
-      }
+      for (int i = 0; i < 4; ++i) pool[i] = row16_sum(pool[i]);
+      // (the relu'(h2) counts behind db2 come from the M phase's MFMAs: head_and_M)
       if ((lane & 15) == 15) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          red[RED_POOL + w * 16 + 4 * h + i] = pool[i];
-          red[red_cnt(WAVES) + w * 16 + 4 * h + i] = cnt[i];
-        }
+        for (int i = 0; i < 4; ++i) red[RED_POOL + w * 16 + 4 * h + i] = pool[i];
       }
       return;
     }
@@ -690,7 +684,14 @@ struct TinySample {
         }
       } else {
         const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
-        auto mfma_pair = [&](int pair, f32x4 a) {
+        // The centre-tap waves (k == 2) also count relu'(h2) per channel for db2: the same A (mask) fragment times
+        // an all-ones B gives sum_t m[t][co] in every column (exact small integers in fp32) - one MFMA per pair
+        // instead of a compare, an add and a 16-lane DPP reduction per value in every wave's conv2 epilogue.
+        bf16x8 ones;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ones[j] = ecg::to_bf16(1.f);
+        f32x4 cnt1 = {0.f, 0.f, 0.f, 0.f}, cnt2 = {0.f, 0.f, 0.f, 0.f};
+        auto mfma_pair = [&](int pair, f32x4 a, f32x4& cn) {
           // Reduction slot (h, j) holds time 32*pair + 4h + j (j < 4) or 32*pair + 16 + 4h + (j - 4): the two
           // lane quarters of one 32-lane LDS cycle read 8 consecutive 32-B rows (256 B, conflict-free); with
           // 8h + j their rows were 256 B apart (2-way conflicts on every transposing read of this phase).
@@ -700,18 +701,23 @@ struct TinySample {
           // B[t][ci] = h1[t + k - 2][ci]
           const bf16x8 Bm =
               cat44(lds_tr16(h1s + (ta + k - 2 + 2) * C + p4), lds_tr16(h1s + (ta + 16 + k - 2 + 2) * C + p4));
+          if (k == 2) cn = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, ones, cn, 0, 0, 0);  // wave-uniform
           return __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, Bm, a, 0, 0, 0);
         };
         // two independent accumulation chains so the next pair's transposing reads overlap this pair's MFMA
         f32x4 acc2 = {0.f, 0.f, 0.f, 0.f};
         int pair = p0;
         for (; pair + 1 < p1; pair += 2) {
-          acc = mfma_pair(pair, acc);
-          acc2 = mfma_pair(pair + 1, acc2);
+          acc = mfma_pair(pair, acc, cnt1);
+          acc2 = mfma_pair(pair + 1, acc2, cnt2);
         }
-        if (pair < p1) acc = mfma_pair(pair, acc);
+        if (pair < p1) acc = mfma_pair(pair, acc, cnt1);
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i] += acc2[i];
+        if (k == 2 && (lane & 15) == 0) {  // cnt[co = 4h + i] of this part's pairs (every column holds it)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) red[red_cnt(WAVES) + part * 16 + 4 * h + i] = cnt1[i] + cnt2[i];
+        }
       }
       // acc[i] = M_k[co = 4h+i][ci = c]
       float* pm = red + red_m(WAVES) + part * 1280;
@@ -733,16 +739,28 @@ struct TinySample {
     float Wd[F32_KSTEPS];
     if constexpr (!F32) {
       // (g W2) fragments, used as A[ci][(k,co)]
+      if constexpr (PF) {
+        // The scaled fragments are the same in every wave: waves 0..2 build set s = w once into the LDS fragD slots
+        // (unused by the prepared-fragment kernels: their operands come from the global image) and every wave
+        // reads its three back - 16 waves x 48 scaling VALU become 3 x 16 plus one barrier (the step is VALU-issue
+        // bound: profiles/r3/tiny_fp_flags_ab.txt).  Same products, same rounding: bitwise the same operands.
+        if (w < 3) {  // wave-uniform
+          const bf16x8 raw = pf_wd[0];  // set s = w (pf_load_dgrad)
+          bf16x8 sc;
 #pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        bf16x8 raw;
-        if constexpr (PF) {
-          raw = pf_wd[s];
-        } else {
-          raw = *reinterpret_cast<const bf16x8*>(fragD + (s * 64 + lane) * 8);
+          for (int j = 0; j < 8; ++j) sc[j] = ecg::to_bf16(ecg::from_bf16(raw[j]) * gq[j]);
+          *reinterpret_cast<bf16x8*>(fragD + (w * 64 + lane) * 8) = sc;
         }
+        __syncthreads();
 #pragma unroll
-        for (int j = 0; j < 8; ++j) Bd[s][j] = ecg::to_bf16(ecg::from_bf16(raw[j]) * gq[j]);
+        for (int s = 0; s < 3; ++s) Bd[s] = *reinterpret_cast<const bf16x8*>(fragD + (s * 64 + lane) * 8);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const bf16x8 raw = *reinterpret_cast<const bf16x8*>(fragD + (s * 64 + lane) * 8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) Bd[s][j] = ecg::to_bf16(ecg::from_bf16(raw[j]) * gq[j]);
+        }
       }
       const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4;
       const __bf16* xzero = xcol + Lp * 8;
@@ -893,8 +911,10 @@ struct TinySample {
       v *= red[RED_G + e / (C * K2)];
     } else {
       const int co = i - lay.b2;
+      // relu'(h2) counts: bf16 path - one partial per M part (head_and_M), fp32 path - one per wave (conv2)
+      constexpr int NCP = F32 ? WAVES : msplit(WAVES);
 #pragma unroll
-      for (int ww = 0; ww < WAVES; ++ww) v += red[red_cnt(WAVES) + ww * 16 + co];
+      for (int pp = 0; pp < NCP; ++pp) v += red[red_cnt(WAVES) + pp * 16 + co];
       v *= red[RED_G + co];
     }
     return v;

@@ -300,6 +300,10 @@ for s in $STEPS; do
               run "lb_cur20_$r" 300 python bench.py --steps 20 --warmup 5 --no-extras
               run "lb_${LIBB}20_$r" 300 env ECG_LIB_DIR=$PWD/_ablib/$LIBB python bench.py --steps 20 --warmup 5 --no-extras
             done ;;
+    tiny_bench3) for r in a b c; do
+                   run "tb500_$r" 300 python bench.py --steps 500 --warmup 100 --no-extras
+                   run "tb20_$r" 300 python bench.py --steps 20 --warmup 5 --no-extras
+                 done ;;
     *) echo "unknown step $s" ;;
   esac
 done

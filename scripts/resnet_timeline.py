@@ -57,6 +57,21 @@ def parse(path, last=4):
         print(f"queue {q}: {len(kk) // last} kernels/step, busy {busy / last:.1f} us/step")
         for name, us in agg.most_common(8):
             print(f"    {us / last:8.1f} us/step  {name}")
+    # the main (critical) queue: the one that runs the weight prep; idle gaps between its consecutive kernels
+    mq = next(k[2] for k in sel if "weight_prep" in k[3])
+    mk = sorted(by_q[mq])
+    gaps = []
+    for a, b in zip(mk, mk[1:]):
+        gaps.append(((b[0] - a[1]) / 1e3, a[3][:60], b[3][:60]))
+    idle = sum(max(0.0, g[0]) for g in gaps)
+    print(f"main queue {mq}: idle between kernels {idle / last:.1f} us/step "
+          f"({len(gaps) // last} boundaries, {idle / max(1, len(gaps)):.2f} us each on average)")
+    agg_g = collections.Counter()
+    for g, a, b in gaps:
+        agg_g[(a, b)] += max(0.0, g)
+    print("largest idle gaps (summed over the steps, per step):")
+    for (a, b), us in agg_g.most_common(10):
+        print(f"    {us / last:8.1f} us  after {a}  ->  {b}")
 
 
 if __name__ == "__main__":
