@@ -304,6 +304,15 @@ for s in $STEPS; do
                    run "tb500_$r" 300 python bench.py --steps 500 --warmup 100 --no-extras
                    run "tb20_$r" 300 python bench.py --steps 20 --warmup 5 --no-extras
                  done ;;
+    tiny_pmc_valu) export TMPDIR=/tmp
+      P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY"
+      run pmcv_new 120 rocprofv3 --pmc $P1 --kernel-trace --output-format csv -d "$OUT/pmcv_new" -o tiny -- python3 scripts/pmc_tiny_step.py ;;
+    env_ab) for r in a b c d; do
+              run "ea_on500_$r" 300 python bench.py --steps 500 --warmup 100 --no-extras
+              run "ea_off500_$r" 300 env $ENVA python bench.py --steps 500 --warmup 100 --no-extras
+              run "ea_on20_$r" 300 python bench.py --steps 20 --warmup 5 --no-extras
+              run "ea_off20_$r" 300 env $ENVA python bench.py --steps 20 --warmup 5 --no-extras
+            done ;;
     *) echo "unknown step $s" ;;
   esac
 done
