@@ -1033,6 +1033,13 @@ int launch_fwd_dma(const FwdArgs& a, hipStream_t stream) {
   if constexpr (BN == 64 && BM <= 128) {
     if (conv_nst64() == 3) return launch_fwd_dma_st<BM, BN, EPI, 3>(a, stream);
   }
+  if constexpr (BM == 256 && BN == 128) {  // ECG_CONV_NST256=3: three LDS stages (3 x 48 KB) for the 8-wave tile
+    static const int nst = [] {
+      const char* e = getenv("ECG_CONV_NST256");
+      return e && atoi(e) == 3 ? 3 : 2;
+    }();
+    if (nst == 3) return launch_fwd_dma_st<BM, BN, EPI, 3>(a, stream);
+  }
   if constexpr (BN == 128 && BM == 128) {
     switch (conv_v128()) {
       case 1: return launch_fwd_dma_st<BM, BN, EPI, 3, 2>(a, stream);
