@@ -867,9 +867,11 @@ __global__ __launch_bounds__(TPB) void reduce_wgrad_kernel(const float* __restri
   __shared__ float4 red[4][64];
   const long N = (long)Cout * K * Cin;
   const int tid = threadIdx.x, col = tid & 63, sg = tid >> 6;
-  const long i4 = (long)blockIdx.x * 64 + col;  // float4 index
   const float4* p4 = reinterpret_cast<const float4*>(part);
   const long N4 = N / 4;
+  // grid-stride over 64-column groups (a capped grid keeps the side lane to fewer, longer blocks)
+  for (long blk = blockIdx.x; blk * 64 < N4; blk += gridDim.x) {
+  const long i4 = blk * 64 + col;  // float4 index
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i4 < N4) {
     int s = sg;
@@ -903,6 +905,8 @@ __global__ __launch_bounds__(TPB) void reduce_wgrad_kernel(const float* __restri
       const int k = (int)(r % K), co = (int)(r / K);
       grad[((long)co * Cin + ci) * K + k] = vv[e];
     }
+  }
+  __syncthreads();  // red[] is rewritten by the next column group
   }
 }
 
@@ -1080,13 +1084,26 @@ inline float F(int64_t v) {
 // The wide one is as fast or faster alone (scripts/wgrad_micro.py) but launches 4x the blocks, and on the side lane
 // of the ResNet1D-34 step that costs 0.12 ms/step (3.87 vs 3.75, profiles/r3/resnet_knob_matrix.txt): side-lane
 // kernels must not crowd the data-gradient chain's CUs.
-inline bool reduce_wide() {
+// ECG_REDUCE_WIDE=2: the wide reduce only where the split count is large (S >= 128: the tap-shared stride-1
+// layer-1 gradients, 256 splits of a 48 KB |dW|, whose 4-group reduce is a 16-deep dependent load chain).
+inline bool reduce_wide(int S) {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("ECG_REDUCE_WIDE");
-    v = (e && atoi(e) == 1) ? 1 : 0;
+    v = e ? atoi(e) : 0;
   }
-  return v == 1;
+  return v == 1 || (v == 2 && S >= 128);
+}
+
+// ECG_REDUCE_GRID=<n>: cap the 4-group reduce's grid at n blocks (grid-stride); 0 (default) = one block per
+// 64 float4 columns.
+inline long reduce_grid_cap() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("ECG_REDUCE_GRID");
+    v = e ? atol(e) : 0;
+  }
+  return v;
 }
 
 // ECG_BN_FIN=ticket selects the single-launch ticketed finalize (fence + last-block reduction); default: two
@@ -1120,12 +1137,15 @@ int run_op(const int64_t* o, hipStream_t st) {
     case OP_REDUCE_WGRAD: {
       const long N = o[3] * o[4] * o[5];
       if (N % 256) return ecg::kBadArg;
-      if (reduce_wide())
+      if (reduce_wide((int)o[2])) {
         hipLaunchKernelGGL(reduce_wgrad_wide_kernel, dim3((unsigned)(N / 64)), dim3(TPB), 0, st, P<const float>(o[1]),
                            (int)o[2], (int)o[3], (int)o[4], (int)o[5], P<float>(o[6]));
-      else
-        hipLaunchKernelGGL(reduce_wgrad_kernel, dim3((unsigned)(N / 256)), dim3(TPB), 0, st, P<const float>(o[1]),
+      } else {
+        const long cap = reduce_grid_cap();
+        const long nb = (cap > 0 && N / 256 > cap) ? cap : N / 256;
+        hipLaunchKernelGGL(reduce_wgrad_kernel, dim3((unsigned)nb), dim3(TPB), 0, st, P<const float>(o[1]),
                            (int)o[2], (int)o[3], (int)o[4], (int)o[5], P<float>(o[6]));
+      }
       break;
     }
     case OP_BN_FIN: {
