@@ -1084,15 +1084,18 @@ inline float F(int64_t v) {
 // The wide one is as fast or faster alone (scripts/wgrad_micro.py) but launches 4x the blocks, and on the side lane
 // of the ResNet1D-34 step that costs 0.12 ms/step (3.87 vs 3.75, profiles/r3/resnet_knob_matrix.txt): side-lane
 // kernels must not crowd the data-gradient chain's CUs.
-// ECG_REDUCE_WIDE=2: the wide reduce only where the split count is large (S >= 128: the tap-shared stride-1
-// layer-1 gradients, 256 splits of a 48 KB |dW|, whose 4-group reduce is a 16-deep dependent load chain).
+// ECG_REDUCE_WIDE=2: the wide reduce only where the split count is large (S >= ECG_REDUCE_WIDE_MIN, default 128:
+// the tap-shared stride-1 layer-1 gradients, 256 splits of a 48 KB |dW|, whose 4-group reduce is a 16-deep
+// dependent load chain).
 inline bool reduce_wide(int S) {
-  static int v = -1;
+  static int v = -1, smin = 128;
   if (v < 0) {
     const char* e = getenv("ECG_REDUCE_WIDE");
     v = e ? atoi(e) : 0;
+    const char* m = getenv("ECG_REDUCE_WIDE_MIN");
+    if (m && atoi(m) > 0) smin = atoi(m);
   }
-  return v == 1 || (v == 2 && S >= 128);
+  return v == 1 || (v == 2 && S >= smin);
 }
 
 // ECG_REDUCE_GRID=<n>: cap the 4-group reduce's grid at n blocks (grid-stride); 0 (default) = one block per
