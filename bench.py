@@ -62,6 +62,8 @@ def parse(argv=None):
     ap.add_argument("--device", choices=["gpu", "cpu"], default="gpu",
                     help="cpu: plumbing rehearsal of the launch/sync/JSON contract (gloo, eager torch)")
     ap.add_argument("--no-extras", action="store_true", help="skip torch-eager and conv1d side measurements")
+    ap.add_argument("--no-numa-bind", action="store_true",
+                    help="keep the inherited CPU affinity (default: each rank pins itself to its GPU's NUMA node)")
     return ap.parse_args(argv)
 
 
@@ -126,22 +128,104 @@ def round_plan(steps: int, local_steps: int):
     return [local_steps] * full + ([rem] if rem else [])
 
 
+class CommTimer:
+    """Times the timed region's FedAvg collectives (reference: comm timed apart from local work,
+    Module_3/TRUE_FL_M3/part3_fedavg_overlap_mpi_gpu.py:188-214).
+
+    GPU: hipEvents.  ``issue`` is recorded on the compute stream right before the collective is enqueued (RCCL's
+    stream is ordered after it); completion is recorded on a side stream that waits for RCCL (``done``); the
+    compute stream's own wait for ``done`` is bracketed by two compute-stream events.  So per collective
+    ``comm_ms`` = issue -> done (the collective's span) and ``exposed_ms`` = the compute stream's stall on it.
+    CPU (gloo): host clocks around the same points.  Resolved once, after the timed region."""
+
+    def __init__(self, gpu: bool, device=None):
+        self.gpu = gpu
+        self.recs = []  # (issue, done, wait_before, wait_after)
+        self.side = None
+        if gpu:
+            import torch
+            self.side = torch.cuda.Stream(device=device)
+
+    def _mark(self, stream=None):
+        if self.gpu:
+            import torch
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(stream) if stream is not None else ev.record()
+            return ev
+        return time.perf_counter()
+
+    def collective(self, fn, async_op: bool):
+        """Run ``fn(async_op)`` (the all-reduce call); returns a handle whose ``wait()`` makes the compute stream
+        (GPU) / the host (CPU) wait and records the stall."""
+        issue = self._mark()
+        work = fn(async_op)
+        rec = [issue, None, None, None]
+        self.recs.append(rec)
+        timer = self
+
+        class _Handle:
+            def wait(self_inner):
+                if rec[3] is not None:
+                    return
+                rec[2] = timer._mark()
+                if timer.gpu:
+                    import torch
+                    torch.cuda.current_stream().wait_event(rec[1])
+                elif work is not None:
+                    work.wait()
+                    rec[1] = timer._mark()
+                rec[3] = timer._mark()
+
+        if not async_op:  # blocking: the compute stream (GPU) / the host (CPU) stalls for the whole collective
+            rec[1] = rec[3] = self._mark()
+            rec[2] = issue
+        elif self.gpu and work is not None:
+            import torch
+            with torch.cuda.stream(self.side):
+                work.wait()  # the side stream waits for RCCL (whose stream is ordered after ``issue``)
+                rec[1] = self._mark(self.side)
+        return _Handle()
+
+    def summary(self):
+        """(comm_ms, exposed_ms) summed over the collectives (call after a device synchronize)."""
+        comm = exp = 0.0
+        for issue, done, w0, w1 in self.recs:
+            if done is None:
+                continue
+            if self.gpu:
+                comm += issue.elapsed_time(done)
+                exp += w0.elapsed_time(w1) if w1 is not None else 0.0
+            else:
+                comm += (done - issue) * 1e3
+                exp += (w1 - w0) * 1e3 if w1 is not None else 0.0
+        return comm, exp
+
+
 class FedAvgRunner:
     """Runs a round plan on a trainer: each round = local steps then the FedAvg all-reduce (AVG).
 
     Per round, in enqueue order: launch the round's steps -> issue the all-reduce -> stage the NEXT round's
     batches (weight-independent) -> [next round] wait for the all-reduce -> launch.  With ``tail`` the
     collective is issued async, so RCCL's stream waits only for the round's steps and the staging kernels run
-    on the compute stream beside it; with ``none`` the host blocks on the collective before staging."""
+    on the compute stream beside it; with ``none`` the host blocks on the collective before staging.
+    ``timer`` (a CommTimer, optional) measures each collective's span and the compute stream's stall on it."""
 
-    def __init__(self, trainer, flat, ctx, overlap: str, allreduce=None):
+    def __init__(self, trainer, flat, ctx, overlap: str, allreduce=None, timer=None):
         if allreduce is None:
             from crossscale_ecg.parallel.fedavg import allreduce_mean_ as allreduce
         self.trainer, self.flat, self.ctx = trainer, flat, ctx
         self.allreduce = allreduce
         self.overlap = overlap if ctx.distributed else "none"
         self.syncs = 0
+        self.timer = timer
         self._pending = None
+
+    def _collective(self, async_op: bool):
+        if self.timer is not None and self.ctx.distributed:
+            return self.timer.collective(lambda a: self.allreduce(self.flat, self.ctx, async_op=a), async_op)
+        if async_op:
+            return self.allreduce(self.flat, self.ctx, async_op=True)
+        return self.allreduce(self.flat, self.ctx)
 
     def run(self, plan, then=None):
         """``then``: size of the round that will follow ``plan`` (its batches are staged behind the last round)."""
@@ -153,9 +237,9 @@ class FedAvgRunner:
                 self._pending = None
             self.trainer.launch_round(n)
             if self.overlap == "tail":
-                self._pending = self.allreduce(self.flat, self.ctx, async_op=True)
+                self._pending = self._collective(True)
             else:
-                self.allreduce(self.flat, self.ctx)
+                self._collective(False)
             self.syncs += 1
             if next_n is not None and hasattr(self.trainer, "stage"):
                 self.trainer.stage(next_n)
@@ -262,6 +346,10 @@ def main(argv=None):
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={ctx.world_size}")
     dev = ctx.device
     on_gpu = dev.type == "cuda"
+    placement = {"numa_node": -1, "cpus": "", "bound": False}
+    if on_gpu and not a.no_numa_bind:  # this rank -> its slice of its GPU's NUMA-node CPUs (parallel/numa.py)
+        from crossscale_ecg.parallel.numa import bind_to_gpu_numa
+        placement = bind_to_gpu_numa(dev.index)
     if a.device == "gpu" and not on_gpu:
         raise SystemExit("bench.py needs a GPU (use --device cpu for the plumbing rehearsal)")
     if not on_gpu:
@@ -324,30 +412,43 @@ def main(argv=None):
     ev0 = ev1 = None
     if on_gpu:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # the timed collectives' span and the compute stream's stall on them (events; resolved after the region)
+    runner.timer = CommTimer(on_gpu, dev) if ctx.distributed else None
     # no cyclic-GC pass inside the timed region (a collection there is host jitter, not work: one K=20 run measured
     # 15.7 us/step wall at 11.4 us/step of GPU time); the same work runs, the collector resumes right after
     gc.collect()
     gc.disable()
-    bracket()
-    if ev0 is not None:  # recorded on the idle stream just before the clock starts (its host cost stays outside)
-        ev0.record()
-    t0 = time.perf_counter()
-    runner.run(timed_plan)
-    if ev1 is not None:
-        ev1.record()
-    bracket()
-    elapsed = time.perf_counter() - t0
-    gc.enable()
+    try:
+        bracket()
+        if ev0 is not None:  # recorded on the idle stream just before the clock starts (its host cost stays outside)
+            ev0.record()
+        t0 = time.perf_counter()
+        runner.run(timed_plan)
+        if ev1 is not None:
+            ev1.record()
+        bracket()
+        elapsed = time.perf_counter() - t0
+    finally:
+        gc.enable()
     gpu_s = ev0.elapsed_time(ev1) / 1e3 if ev0 is not None else float("nan")
+    comm_ms, exposed_ms = runner.timer.summary() if runner.timer is not None else (0.0, 0.0)
     tbar_kind = tbar.kind
     tbar.close()
     world_seen, dist_backend = 1, "none"
+    per_rank = [[elapsed, gpu_s, comm_ms, exposed_ms]]
+    placements = [placement]
     if ctx.distributed:
         import torch.distributed as dist
         world_seen, dist_backend = dist.get_world_size(), dist.get_backend()
-        t = torch.tensor([elapsed, gpu_s], device=dev if dist_backend == "nccl" else "cpu", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, gpu_s = float(t[0].item()), float(t[1].item())
+        mine = torch.tensor([elapsed, gpu_s, comm_ms, exposed_ms], dtype=torch.float64,
+                            device=dev if dist_backend == "nccl" else "cpu")
+        allv = [torch.zeros_like(mine) for _ in range(world_seen)]
+        dist.all_gather(allv, mine)
+        per_rank = [[float(v) for v in t.tolist()] for t in allv]
+        placements = [None] * world_seen
+        dist.all_gather_object(placements, placement)
+        elapsed = max(r[0] for r in per_rank)
+        gpu_s = max(r[1] for r in per_rank)
     total = a.gpus * B * a.steps
     value = total / elapsed
     loss = trainer.avg_loss() if hasattr(trainer, "avg_loss") else float("nan")
@@ -404,6 +505,18 @@ def main(argv=None):
             "timing_barrier": tbar_kind,
             "timed_round_plan": timed_plan if len(timed_plan) <= 4 else f"{len(timed_plan)} rounds",
             "final_avg_loss": round(loss, 6) if loss == loss else None,
+            # per-rank diagnosis of the MAX: wall and GPU-event ms/step, the timed collectives' span (comm_ms) and
+            # the compute stream's stall on them (comm_exposed_ms), summed over the timed rounds, per rank
+            "per_rank_ms_per_step": [round(r[0] * 1e3 / a.steps, 5) for r in per_rank],
+            "per_rank_gpu_ms_per_step": [round(r[1] * 1e3 / a.steps, 5) if r[1] == r[1] else None for r in per_rank],
+            "comm_ms": [round(r[2], 4) for r in per_rank],
+            "comm_exposed_ms": [round(r[3], 4) for r in per_rank],
+            "rank_cpus": [f"node{p.get('numa_node', -1)}:{p.get('cpus', '')}" + ("" if p.get("bound") else " (unbound)")
+                          for p in placements],
+            # timing method: the cyclic GC is paused inside the timed region (restarted right after); the first
+            # timed round's batch indices were drawn behind the last warmup round (later rounds' staging is timed)
+            "gc_paused_in_timed_region": True,
+            "first_round_staged_in_warmup": a.warmup > 0,
             **extras,
         }
         print(json.dumps(rec), flush=True)

@@ -98,14 +98,17 @@ def split_cpus(cpus: Optional[Sequence[int]] = None):
 
 
 def _pin_threads(it, pin_cpus) -> Optional[tuple]:
-    """Put the DataLoader iterator's pin-memory thread and the calling (training) thread on two different CPUs so
-    the pinning copy no longer competes with the launch-bound step for one core.  Returns the calling thread's
-    previous affinity (to restore), or None when not applicable."""
-    th = getattr(it, "_pin_memory_thread", None)
-    if pin_cpus is None or th is None or getattr(th, "native_id", None) is None:
+    """Put the calling (training) thread on CPU ``pin_cpus[0]`` - for EVERY configuration, so A0-A3 differ only in
+    contiguity / pin_memory / non_blocking (the reference's comparison, bench_locality.py:111-116) - and, when the
+    iterator has a pin-memory thread (A2/A3), that thread on ``pin_cpus[1]``, so the pinning copy does not compete
+    with the launch-bound step for one core.  Call after the iterator (and its worker processes) exist, so the
+    workers keep the inherited affinity.  Returns the calling thread's previous affinity (to restore), or None."""
+    if pin_cpus is None:
         return None
     prev = os.sched_getaffinity(0)
-    os.sched_setaffinity(th.native_id, {pin_cpus[1]})
+    th = getattr(it, "_pin_memory_thread", None)
+    if th is not None and getattr(th, "native_id", None) is not None:
+        os.sched_setaffinity(th.native_id, {pin_cpus[1]})
     os.sched_setaffinity(0, {pin_cpus[0]})  # (Linux: pid 0 = the calling thread)
     return prev
 
@@ -303,7 +306,9 @@ def run_locality(shard_dir: str, batch_sizes: List[int], iters: int = 100, num_w
     """A0-A5 per batch size.  ``reps`` > 1: every (config, batch) cell is measured ``reps`` times, the
     configurations interleaved within each repetition (A0 A1 A2 A3 A4 A5, A0 A1 ...), and the CSV holds the
     median of each column plus the samples/s interquartile range (``samples_per_s_q1/q3``, ``reps``).
-    ``pin_thread``: the pinned configurations run with the pin-memory thread on its own CPU."""
+    ``pin_thread``: the training thread of every A0-A3 configuration runs on one fixed CPU, and the pinned
+    configurations' pin-memory thread on another (pinning only A2/A3 mixed thread placement into the
+    A3-vs-A0 comparison)."""
     dev = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
     paths = ensure_synthetic_shards(shard_dir, n_windows, shard_size=8192) if not list_shards(shard_dir) \
         else list_shards(shard_dir)
@@ -318,8 +323,7 @@ def run_locality(shard_dir: str, batch_sizes: List[int], iters: int = 100, num_w
                 dl = DataLoader(ds, batch_size=bs, sampler=sampler, num_workers=num_workers,
                                 pin_memory=pin and dev.type == "cuda", drop_last=True,
                                 persistent_workers=num_workers > 0)
-                st = measure_step(dl, dev, non_blocking=nb, iters=iters, compute=compute,
-                                  pin_cpus=pin_cpus if pin else None)
+                st = measure_step(dl, dev, non_blocking=nb, iters=iters, compute=compute, pin_cpus=pin_cpus)
                 # retire this loader's persistent worker processes (and its pin-memory thread) before the next
                 # config is timed: left alive they prefetch beside it (the A4 B=256 outlier of round 1)
                 del dl

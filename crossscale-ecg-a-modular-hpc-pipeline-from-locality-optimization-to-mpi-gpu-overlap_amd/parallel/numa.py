@@ -1,0 +1,121 @@
+"""Per-rank CPU placement: bind each rank to CPUs of its own GPU's NUMA node.
+
+Reference: every FedAvg client gets ``--cpus-per-task=4`` from Slurm (Module_3/TRUE_FL_M3/run_part3_sweep.sh:38-42).
+On one 8-GPU MI355X node the eight ranks are launch-latency bound (a TinyECG step is ~11 µs of GPU work behind a
+host-side graph launch), so a rank whose launch thread lands on a far socket, or shares a core with another rank,
+turns into a straggler that the MAX-over-ranks timing exposes.  Each rank therefore pins itself, after it selected
+its GPU, to a disjoint slice of the CPUs of that GPU's NUMA node:
+
+    GPU PCI address (torch device properties) -> /sys/bus/pci/devices/<bdf>/numa_node
+    -> /sys/devices/system/node/node<n>/cpulist  (intersected with the CPUs this process may use)
+    -> ranks on the same node split that list into contiguous, equal slices (in device order).
+
+Everything reads a ``sysfs`` root argument so the mapping is unit-tested on a fake tree.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+
+def parse_cpulist(text: str) -> List[int]:
+    """``"0-3,8,10-11"`` -> [0, 1, 2, 3, 8, 10, 11] (the sysfs cpulist format)."""
+    cpus: List[int] = []
+    for part in text.strip().split(","):
+        part = part.strip()
+        if not part:
+            continue
+        if "-" in part:
+            lo, hi = part.split("-", 1)
+            cpus.extend(range(int(lo), int(hi) + 1))
+        else:
+            cpus.append(int(part))
+    return sorted(set(cpus))
+
+
+def format_cpulist(cpus: Iterable[int]) -> str:
+    """Inverse of ``parse_cpulist`` (compact ranges)."""
+    s = sorted(set(cpus))
+    out, i = [], 0
+    while i < len(s):
+        j = i
+        while j + 1 < len(s) and s[j + 1] == s[j] + 1:
+            j += 1
+        out.append(str(s[i]) if i == j else f"{s[i]}-{s[j]}")
+        i = j + 1
+    return ",".join(out)
+
+
+def _read(path: str) -> Optional[str]:
+    try:
+        with open(path) as f:
+            return f.read()
+    except OSError:
+        return None
+
+
+def numa_node_of(bdf: str, sysfs: str = "/sys") -> int:
+    """NUMA node of a PCI device (-1 when unknown / single-node systems report -1)."""
+    v = _read(os.path.join(sysfs, "bus", "pci", "devices", bdf, "numa_node"))
+    try:
+        return int(v.strip()) if v is not None else -1
+    except ValueError:
+        return -1
+
+
+def node_cpus(node: int, sysfs: str = "/sys") -> List[int]:
+    v = _read(os.path.join(sysfs, "devices", "system", "node", f"node{node}", "cpulist"))
+    return parse_cpulist(v) if v else []
+
+
+def plan_affinity(bdfs: Sequence[str], index: int, allowed: Iterable[int],
+                  sysfs: str = "/sys") -> Tuple[int, List[int]]:
+    """CPUs for the rank driving GPU ``bdfs[index]``: its NUMA node's CPUs (within ``allowed``), split into equal
+    contiguous slices among the GPUs of ``bdfs`` on the same node, in list order.  Returns (node, cpus); cpus is
+    empty when nothing can be decided (unknown node, no allowed CPU on it)."""
+    allowed = set(allowed)
+    nodes = [numa_node_of(b, sysfs) for b in bdfs]
+    node = nodes[index]
+    if node < 0:
+        return node, []
+    cpus = [c for c in node_cpus(node, sysfs) if c in allowed]
+    if not cpus:
+        return node, []
+    peers = [i for i, n in enumerate(nodes) if n == node]
+    k, n_peers = peers.index(index), len(peers)
+    if len(cpus) < n_peers:  # fewer CPUs than ranks on this node: share the node's CPUs
+        return node, cpus
+    per = len(cpus) // n_peers
+    return node, cpus[k * per:(k + 1) * per]
+
+
+def device_bdfs() -> List[str]:
+    """PCI addresses (``dddd:bb:dd.0``) of the visible GPUs, in device order (initialises the HIP runtime)."""
+    import torch
+    out = []
+    for i in range(torch.cuda.device_count()):
+        p = torch.cuda.get_device_properties(i)
+        out.append(f"{int(getattr(p, 'pci_domain_id', 0)):04x}:{int(p.pci_bus_id):02x}:{int(p.pci_device_id):02x}.0")
+    return out
+
+
+def bind_to_gpu_numa(device_index: int, sysfs: str = "/sys", bdfs: Optional[Sequence[str]] = None) -> Dict:
+    """Pin this process to its slice of the CPUs of GPU ``device_index``'s NUMA node.  Returns a record
+    {"numa_node", "cpus", "bound"} for the bench JSON; never raises (placement is a performance measure)."""
+    rec: Dict = {"numa_node": -1, "cpus": "", "bound": False}
+    try:
+        allowed = os.sched_getaffinity(0)
+        if bdfs is None:
+            bdfs = device_bdfs()
+        if not 0 <= device_index < len(bdfs):
+            return rec
+        node, cpus = plan_affinity(bdfs, device_index, allowed, sysfs)
+        rec["numa_node"] = node
+        if cpus:
+            os.sched_setaffinity(0, cpus)
+            rec["cpus"], rec["bound"] = format_cpulist(cpus), True
+        else:
+            rec["cpus"] = format_cpulist(allowed)
+    except Exception as e:  # pragma: no cover - sysfs / affinity quirks must not break a run
+        rec["error"] = repr(e)[:120]
+    return rec

@@ -1,0 +1,68 @@
+#!/bin/bash
+# Round-4 GPU measurement session on one MI355X (run by gpurun from the repo root):
+#   bash scripts/r4_gpu_session.sh <tag> <steps...>
+# steps: tests | bench | resnet | probe | pmc | stats | tinypmc   (any subset, in order)
+# Every GPU step runs under its own time limit; a crash, abort or timeout ends the session.
+set -u
+cd "$(dirname "$0")/.."
+TAG=${1:-base}
+shift
+OUT=gpurun_out/r4_$TAG
+mkdir -p "$OUT"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+step() {  # step <name> <timeout_s> <cmd...>
+  local name=$1 tmo=$2
+  shift 2
+  echo "=== [$name] $(date +%T)"
+  timeout -k 10 "$tmo" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== [$name] rc=$rc"
+  tail -n 4 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "!!! [$name] rc=$rc: stopping"
+    exit $rc
+  fi
+  if [ $rc -eq 1 ]; then echo "!!! [$name] failed (rc=1)"; fi
+}
+smi() { rocm-smi --showclocks --showpower --showtemp > "$OUT/smi_$1.txt" 2>&1 || true; }
+{ hostname; rocm-smi --showserial --showproductname 2>/dev/null | grep -iE "serial|card series" | head -4; } > "$OUT/host.txt" 2>&1
+smi start
+for s in "$@"; do
+  case $s in
+    tests)
+      step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    smoke)
+      step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)
+      for i in 1 2 3; do step bench20_$i 300 python bench.py --steps 20 --warmup 5; done
+      step bench500 300 python bench.py --steps 500 --warmup 100 --no-extras ;;
+    bench20)
+      for i in 1 2 3; do step bench20_$i 300 python bench.py --steps 20 --warmup 5 --no-extras; done ;;
+    resnet)
+      for i in 1 2 3; do step resnet_$i 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras; done ;;
+    probe)
+      step probe 300 python scripts/r4_conv_probe.py 30 1024,4096 ;;
+    pmc)
+      export TMPDIR=/tmp
+      step pmc_resnet 240 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 \
+        SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --kernel-trace --output-format csv \
+        -d "$OUT/pmc_resnet" -o p -- python3 bench.py --model resnet1d34 --steps 3 --warmup 2 --no-extras
+      step pmc_resnet2 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
+        SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD --kernel-trace --output-format csv \
+        -d "$OUT/pmc_resnet2" -o p -- python3 bench.py --model resnet1d34 --steps 3 --warmup 2 --no-extras ;;
+    stats)
+      export TMPDIR=/tmp
+      step prof_tiny 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_tiny" -o tiny -- \
+        python3 bench.py --steps 200 --warmup 50 --no-extras
+      step prof_resnet 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_resnet" -o resnet -- \
+        python3 bench.py --model resnet1d34 --steps 10 --warmup 3 --no-extras ;;
+    tinypmc)
+      export TMPDIR=/tmp
+      step pmc_tiny 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAVE_CYCLES \
+        SQ_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 --kernel-trace --output-format csv -d "$OUT/pmc_tiny" -o p -- \
+        python3 bench.py --steps 100 --warmup 20 --no-extras ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+smi end
+echo "=== session $TAG done $(date +%T)"

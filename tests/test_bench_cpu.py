@@ -39,3 +39,15 @@ def test_bench_single_rank():
     rec = _bench("--steps", "3", "--warmup", "1", "--local-steps", "2")
     assert rec["n_gpus"] == 1 and rec["rccl_world_size"] == 1 and rec["fedavg_syncs_timed"] == 2
     assert rec["timing_barrier"] == "none"
+
+
+def test_bench_world2_reports_per_rank_comm_and_placement():
+    """The N>1 JSON line diagnoses its own MAX: per-rank wall / GPU ms, the timed all-reduces' span and the stall
+    on them, and each rank's CPU placement."""
+    rec = _bench("--gpus", "2", "--steps", "6", "--warmup", "2", "--local-steps", "3")
+    assert len(rec["per_rank_ms_per_step"]) == 2 and max(rec["per_rank_ms_per_step"]) == rec["ms_per_step"]
+    assert len(rec["per_rank_gpu_ms_per_step"]) == 2
+    assert len(rec["comm_ms"]) == 2 and all(c > 0 for c in rec["comm_ms"])  # two timed all-reduces per rank
+    assert len(rec["comm_exposed_ms"]) == 2 and all(0 <= e for e in rec["comm_exposed_ms"])
+    assert len(rec["rank_cpus"]) == 2 and all(s.startswith("node") for s in rec["rank_cpus"])
+    assert rec["gc_paused_in_timed_region"] is True and rec["first_round_staged_in_warmup"] is True

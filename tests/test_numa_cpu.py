@@ -1,0 +1,56 @@
+"""Per-rank NUMA placement (parallel/numa.py) on a fake sysfs tree: GPU PCI address -> numa_node -> the node's
+cpulist, intersected with the allowed CPUs and split among the ranks whose GPUs share the node."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import crossscale_ecg  # noqa: E402,F401
+from crossscale_ecg.parallel import numa  # noqa: E402
+
+
+def _fake_sysfs(tmp_path, gpu_nodes, node_cpus):
+    for bdf, node in gpu_nodes.items():
+        d = tmp_path / "bus" / "pci" / "devices" / bdf
+        d.mkdir(parents=True)
+        (d / "numa_node").write_text(f"{node}\n")
+    for node, cl in node_cpus.items():
+        d = tmp_path / "devices" / "system" / "node" / f"node{node}"
+        d.mkdir(parents=True)
+        (d / "cpulist").write_text(cl + "\n")
+    return str(tmp_path)
+
+
+def test_cpulist_roundtrip():
+    assert numa.parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    assert numa.format_cpulist([11, 10, 8, 3, 2, 1, 0]) == "0-3,8,10-11"
+    assert numa.parse_cpulist("") == []
+
+
+def test_eight_gpus_two_sockets(tmp_path):
+    bdfs = [f"0000:{b:02x}:00.0" for b in (0x05, 0x15, 0x25, 0x35, 0x85, 0x95, 0xa5, 0xb5)]
+    root = _fake_sysfs(tmp_path, {b: (0 if i < 4 else 1) for i, b in enumerate(bdfs)},
+                       {0: "0-31,64-95", 1: "32-63,96-127"})
+    allowed = range(128)
+    plans = [numa.plan_affinity(bdfs, i, allowed, root) for i in range(8)]
+    assert [p[0] for p in plans] == [0, 0, 0, 0, 1, 1, 1, 1]
+    assert plans[0][1] == list(range(0, 16)) and plans[3][1] == list(range(80, 96))
+    assert plans[4][1] == list(range(32, 48)) and plans[7][1] == list(range(112, 128))
+    seen = [c for _, cpus in plans for c in cpus]
+    assert len(seen) == len(set(seen)) == 128  # disjoint, complete
+
+
+def test_allowed_set_and_unknown_node(tmp_path):
+    bdfs = ["0000:05:00.0", "0000:15:00.0", "0000:25:00.0"]
+    root = _fake_sysfs(tmp_path, {bdfs[0]: 0, bdfs[1]: 0, bdfs[2]: -1}, {0: "0-7"})
+    node, cpus = numa.plan_affinity(bdfs, 1, [2, 3, 4, 5], root)  # container cpuset 2-5
+    assert node == 0 and cpus == [4, 5]
+    assert numa.plan_affinity(bdfs, 2, range(8), root) == (-1, [])  # single-node systems report -1
+    assert numa.plan_affinity(bdfs, 0, [100], root) == (0, [])  # nothing allowed on the node
+
+
+def test_bind_record_never_raises(tmp_path):
+    rec = numa.bind_to_gpu_numa(5, sysfs=str(tmp_path), bdfs=["0000:05:00.0"])
+    assert rec["bound"] is False and rec["numa_node"] == -1
