@@ -36,6 +36,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_splits", [i32] * 8)
     _lib._sig(lib, "ecg_conv1d_nlc_set_big", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_set_mt", [i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_set_tap", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_set_dma_dil", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_ex", [vp] * 7 + [i32] * 10 + [vp, vp, vp])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles", [_lib.C.c_long, i32])
@@ -60,6 +61,12 @@ def set_dma_dilated(on: bool) -> int:
     """Strided (phase-decomposed) data-grads on the LDS-DMA loop (True, default) or the register-staged loop;
     returns the previous setting."""
     return _lib_k().ecg_conv1d_nlc_set_dma_dil(1 if on else 0)
+
+
+def set_tap_shared(mode: int) -> int:
+    """Tap-shared 256-row forward/data-grad kernel for stride-1 pad-1 3-tap convs (0: off, 1 (default): outputs with
+    C_out % 128 == 0, 2: also 64-channel outputs); returns the previous mode.  Build step plans after setting it."""
+    return _lib_k().ecg_conv1d_nlc_set_tap(int(mode))
 
 
 def set_multi_tile(mode: int) -> int:

@@ -585,10 +585,15 @@ __device__ __forceinline__ srd_t make_rsrc(const void* p, long bytes) {
 __device__ __forceinline__ unsigned lds_addr(const unsigned char* p) {
   return (unsigned)reinterpret_cast<unsigned long>((__attribute__((address_space(3))) const unsigned char*)p);
 }
-// one 16-B piece per lane into LDS at (wave-uniform) lds + 16 * lane; s_nop covers the M0 -> LDS-DMA hazard
+// one 16-B piece per lane into LDS at (wave-uniform) lds + 16 * lane; s_nop covers the M0 -> LDS-DMA hazard.
+// M0 is compiler-reserved and assumed unchanged across an asm statement, so the statement restores it (a "m0"
+// clobber is not honoured: MI355X guide §5.7) - any compiler use of M0 around these loops stays correct.
 __device__ __forceinline__ void dma16_at(srd_t r, unsigned voff, unsigned lds) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(r),
-               "s"(__builtin_amdgcn_readfirstlane(lds))
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(r), "s"(__builtin_amdgcn_readfirstlane(lds))
                : "memory");
 }
 __device__ __forceinline__ void dma16(srd_t r, unsigned voff, unsigned char* lds_piece) {
@@ -854,6 +859,199 @@ __global__ __launch_bounds__(128 * NWR, 2) void conv1d_nlc_fwd_dma_mt_kernel(Fwd
     fwd_epi_stats<BM, BN, EPI, NWR>(a, eps, k, n0, gm, GM);
     if (a.tail) ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, GM, a.Cout, gm, n0, BN, smem);
   }
+}
+
+// ------------------------------------------------------------------ tap-shared 256-row forward / data-grad
+// Stride-1, pad-1, 3-tap convs over whole samples (Lin == Lout = L: every conv of a ResNet stage but its strided
+// first one, forward AND data-grad).  The three taps of one 64-channel chunk read the SAME activation rows shifted
+// by one: output row m, tap k reads input row m + k - 1 of its sample.  So per chunk the workgroup stages the
+// activation rows [m0 - 1, m0 + 263) ONCE (the "A' image") and each tap's MFMAs read it at row offset k, while the
+// weight tile of each (chunk, tap) step streams through a ring of its own.  Against the one-tap kernels (a 128 x 128
+// tile restaging 16 KB of activations per tap) a 256 x BN tile moves 11 KB of activations + BN*128 B of weights per
+// 64-deep step: 27 KB per 256x128x64 MACs instead of 64 KB for two 128x128 workgroups - and the one-tap loop is
+// bound by its staged bytes (a CU keeps ~64 KB in flight against a ~1 us L2 round trip at B=1024: the isolated
+// layer-4 forward ran at 690 TF/s at B=1024 vs 1000 TF/s with 256x256 tiles at B=4096, scripts/r4_conv_probe.py).
+// Rows that cross a sample boundary are masked per lane: tap 0 at t == 0 and tap 2 at t == L-1 read a row of the
+// neighbouring sample, so those A fragments are zeroed (zero padding).
+// Layout: 8 waves as 4 (M) x 2 (N), each 64 x BN/2 (one workgroup per CU, two waves per SIMD).  LDS: two A' slots
+// [264 rows][128 B] (16-B chunk cc of row r at cc ^ (r & 7): conflict-free ds_read_b128 at any row offset) and three
+// weight slots [BN rows][128 B]; step s = 3c + k uses weight slot k, A' slot c & 1.  LDS-DMA from inline asm,
+// counted vmcnt waits, raw s_barrier (a __syncthreads() would drain the DMA kept in flight).
+constexpr int TAP_BM = 256;
+constexpr int TAP_AROWS = TAP_BM + 8;       // image rows m0-1 .. m0+262 (258 used); 33 DMA pieces of 8 rows
+constexpr int TAP_ASLOT = TAP_AROWS * 128;  // 33,792 B
+constexpr int TAP_NA = 5;                   // DMA instructions per wave per A' image (4 full pieces + 1 row)
+
+template <int BN>
+struct TapCfg {
+  static constexpr int BSLOT = BN * 128;
+  static constexpr int BP = BN / 64;  // weight pieces per wave per step (8 waves x 8 rows)
+  static constexpr int STAGES = 2 * TAP_ASLOT + 3 * BSLOT;
+  static constexpr int SMEM = STAGES > FwdCfg<TAP_BM, BN, 4>::EP_BYTES ? STAGES : FwdCfg<TAP_BM, BN, 4>::EP_BYTES;
+};
+
+template <int BN, int EPI>
+__global__ __launch_bounds__(512, 2) void conv1d_nlc_fwd_tap_kernel(FwdArgs a, int MT, int NT) {
+  constexpr int BM = TAP_BM, NWR = 4, NW = 8;
+  using Cfg = FwdCfg<BM, BN, NWR>;
+  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
+  constexpr int BP = TapCfg<BN>::BP, BSLOT = TapCfg<BN>::BSLOT;
+  static_assert(WM == 64 && FM == 4, "64-row wave tiles");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wv >> 1, wc = wv & 1;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int mt = wgid / NT, nt = wgid % NT;  // the NT column blocks of one M tile share an XCD (same A rows)
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int L = a.Lout, M = a.B * L, Cin = a.Cin, CB = Cin / 64, K3 = 3 * Cin;
+  const srd_t xr = make_rsrc(a.x, (long)M * Cin * 2);
+  const srd_t wrs = make_rsrc(a.w, (long)a.Cout * K3 * 2);
+  const unsigned lds0 = lds_addr(smem);
+  const unsigned ldsA = lds0, ldsB = lds0 + 2 * TAP_ASLOT;
+  // A' DMA: pieces p = wv + 8i (i < 4) cover image rows 8p .. 8p+7 (lane -> row 8p + lane/8, LDS chunk lane%8);
+  // piece 32 (rows 256..263) is issued by every wave with lanes 8wv .. 8wv+7 only (row 256 + wv).
+  unsigned aoff[TAP_NA];
+#pragma unroll
+  for (int i = 0; i < TAP_NA; ++i) {
+    const int row = i < 4 ? 8 * (wv + NW * i) + (lane >> 3) : 256 + (lane >> 3);
+    const int g = m0 - 1 + row;
+    const int src = (lane & 7) ^ (row & 7);
+    aoff[i] = (g >= 0 && g < M) ? (unsigned)(g * Cin * 2 + src * 16) : 0x7ffffff0u;
+  }
+  unsigned boff[BP];
+#pragma unroll
+  for (int i = 0; i < BP; ++i) {
+    const int n = 8 * (wv + NW * i) + (lane >> 3);
+    boff[i] = (unsigned)((n0 + n) * K3 * 2 + (((lane & 7) ^ (n & 7)) * 16));
+  }
+  auto issue_a = [&](int c, int slot) {
+    const unsigned base = ldsA + slot * TAP_ASLOT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dma16_at(xr, aoff[i] + c * 128, base + (wv + NW * i) * 1024);
+    if ((lane >> 3) == wv) dma16_at(xr, aoff[4] + c * 128, base + 32 * 1024);
+  };
+  auto issue_b = [&](int c, int k, int slot) {
+    const unsigned base = ldsB + slot * BSLOT;
+#pragma unroll
+    for (int i = 0; i < BP; ++i) dma16_at(wrs, boff[i] + (k * Cin + c * 64) * 2, base + (wv + NW * i) * 1024);
+  };
+  // this lane's fragment rows: i_f = wr*64 + 16f + (lane & 15); tap 0 is invalid at t == 0, tap 2 at t == L-1
+  unsigned ok0 = 0u, ok2 = 0u;
+#pragma unroll
+  for (int f = 0; f < FM; ++f) {
+    const int m = m0 + wr * WM + 16 * f + (lane & 15);
+    const int t = m - (m / L) * L;
+    ok0 |= (t != 0 ? 1u : 0u) << f;
+    ok2 |= (t != L - 1 ? 1u : 0u) << f;
+  }
+  // read addresses (bytes from the slot base): row r chunk cc at r*128 + ((cc ^ (r & 7)) << 4).  A rows i_f + k have
+  // r & 7 == (lane + k) & 7; B rows n = wc*WN + 16j + (lane & 15) have n & 7 == lane & 7.
+  const int arow = (wr * WM + (lane & 15)) * 128, brow = (wc * WN + (lane & 15)) * 128;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = 3 * CB;
+  issue_a(0, 0);
+  issue_b(0, 0, 0);
+  issue_b(0, 1, 1);
+  for (int c = 0; c < CB; ++c) {
+    const bool more = c + 1 < CB;  // block-uniform
+    const unsigned char* As = smem + (c & 1) * TAP_ASLOT;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int s = 3 * c + k;
+      // wait for weight step s (and, at k == 0, A'(c), issued before it): the younger DMA of this wave is counted
+      if (k == 0) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BP) : "memory");
+      } else if (k == 1) {
+        if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BP + TAP_NA) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BP) : "memory");
+      } else {
+        if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BP + TAP_NA) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of step s-1 retired (WAR)
+      __builtin_amdgcn_s_barrier();
+      if (s + 2 < nk) issue_b((s + 2) / 3, (k + 2) % 3, (k + 2) % 3);  // into the slot step s-1 read
+      if (k == 0 && more) issue_a(c + 1, (c + 1) & 1);                  // into the slot chunk c-1 read
+      const unsigned char* Bs = smem + 2 * TAP_ASLOT + k * BSLOT;
+      const unsigned okm = k == 0 ? ok0 : ok2;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int cc = 4 * ks + (lane >> 4);
+        const int asw = (cc ^ ((lane + k) & 7)) << 4, bsw = (cc ^ (lane & 7)) << 4;
+        bf16x8 af[FM], bfr[FN];
+#pragma unroll
+        for (int f = 0; f < FM; ++f) {
+          af[f] = *reinterpret_cast<const bf16x8*>(As + arow + (16 * f + k) * 128 + asw);
+          if (k != 1 && !((okm >> f) & 1u)) af[f] = bf16x8{};
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + brow + 16 * j * 128 + bsw);
+#pragma unroll
+        for (int f = 0; f < FM; ++f)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f], bfr[j], acc[f][j], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // the epilogue reuses the stage buffers
+  fwd_epilogue<BM, BN, EPI, NWR, false>(a, acc, smem, m0, n0, mt, MT, L, M, 1, 0);
+  if (a.tail && a.stats)
+    ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, MT, a.Cout, mt, n0, BN, smem);
+}
+
+// The tap-shared kernel applies to stride-1, pad-1, 3-tap convs over whole samples with BN | C_out (BN = 128 when
+// C_out % 128 == 0, else 64) and 32-bit addressable operands.
+inline bool tap_ok(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad, int in_dil) {
+  return Kw == 3 && stride == 1 && pad == 1 && in_dil == 1 && Lin == Lout && Lout >= 2 && Cin % 64 == 0 &&
+         Cout % 64 == 0 && (long)B * Lout * Cin * 2 < 0x7fff0000L && (long)Cout * 3 * Cin * 2 < 0x7fff0000L;
+}
+inline int tap_mtiles(int B, int Lout) { return (int)(((long)B * Lout + TAP_BM - 1) / TAP_BM); }
+
+template <int BN, int EPI>
+int launch_fwd_tap_t(const FwdArgs& a, hipStream_t stream) {
+  constexpr int SMEM = TapCfg<BN>::SMEM;
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_tap_kernel<BN, EPI>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
+    attr = true;
+  }
+  const int MT = tap_mtiles(a.B, a.Lout), NT = a.Cout / BN;
+  hipLaunchKernelGGL((conv1d_nlc_fwd_tap_kernel<BN, EPI>), dim3((unsigned)(MT * NT)), dim3(512), SMEM, stream, a, MT,
+                     NT);
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
+}
+
+int launch_fwd_tap(const FwdArgs& a, hipStream_t stream) {
+  const bool b = a.stat_mode == 1;
+  if (a.Cout % 128 == 0) return b ? launch_fwd_tap_t<128, 1>(a, stream) : launch_fwd_tap_t<128, 0>(a, stream);
+  return b ? launch_fwd_tap_t<64, 1>(a, stream) : launch_fwd_tap_t<64, 0>(a, stream);
+}
+
+// ECG_CONV_TAP=0|1|2: the tap-shared 256-row kernel for eligible convs with C_out % 128 == 0 (1, default), also
+// for 64-channel outputs (2), or never (0).  Read once.
+int g_conv_tap = -1;
+inline int conv_tap_mode() {
+  if (g_conv_tap < 0) {
+    const char* e = getenv("ECG_CONV_TAP");
+    g_conv_tap = e ? atoi(e) : 1;
+  }
+  return g_conv_tap;
+}
+inline bool conv_tap(int Cout) {
+  const int v = conv_tap_mode();
+  return v >= 2 || (v == 1 && Cout % 128 == 0);
 }
 
 inline bool conv_dma();
@@ -1433,344 +1631,169 @@ __global__ __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) void conv1d_nlc_wgrad_
   wgrad_epilogue<BM, BN, NWR>(a, acc, smem, split, co0, n0);
 }
 
-// ------------------------------------------------------------------ weight-resident tap-shared forward (WR)
-// Stride-1, pad-1, 3-tap convs with C_in in {64, 128, 256} (the forward and the data-grad of every 3-tap conv of a
-// ResNet stage except its strided first one: in_dil 1, Lin == Lout).  One workgroup per CU (4 waves):
-//   * the weights of its BN output channels, all 3 taps x C_in, stay resident in LDS for the workgroup's life
-//     (loaded once; the one-tap kernels restream a weight tile per 64-deep K step of every M tile);
-//   * per 128-row M tile and 64-channel chunk it stages x[m0 - 1, m0 + 135) ONCE (LDS-DMA, 3-stage ring, counted
-//     vmcnt, raw barriers); the 3 taps read that image at row offsets 0, 1, 2.
-// So a CU moves ~17 KB of activations per 128 x BN x 192 MACs instead of 32 KB per 128 x 128 x 64.
-// Orientation out^T[co][m] = W[co][kk] x X^T[kk][m] (A = weights, B = activations): a lane's accumulator holds 4
-// consecutive channels of ONE output row, so the epilogue is 8-byte loads / stores straight from registers and
-// the BatchNorm partials reduce over rows with DPP - the LDS holds only the weights and the activation ring.
-// Sample boundaries: a lane's B fragment is one output row; it is zeroed for tap 0 at t == 0 and for tap 2 at
-// t == L - 1 (the shifted row belongs to the neighbouring sample).
-// Work split: workgroup (gm, nt) of a GM x NT grid owns channels [nt * BN, + BN) and M tiles gm, gm + GM, ...; its
-// statistics accumulate over those tiles into partial row gm of GM (the rows the BatchNorm tail reduces).
-// Weight image: row co = 3 * C_in bf16 (tap-major), padded to a multiple of 256 B; 16-B chunk ch of row co is
-// stored at (ch & ~15) | ((ch & 15) ^ (co & 15)), so the 16 rows x 2 chunk offsets of a ds_read_b128 lane group
-// land on 16 distinct slots.  Activation image: [136 rows][64] bf16, chunk cc of row r at cc ^ ((r >> 1) & 7).
-__device__ __forceinline__ float wr_row16_sum(float v) {  // lane 15 of each 16-lane DPP row ends with the row sum
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
-  return v;
-}
-
-constexpr int WR_BM = 128;
-constexpr int WR_XSTAGE = 136 * 128;  // activation image bytes per stage (rows m0-1 .. m0+134, 130 used)
-
-template <int BN, int NCH>
-struct WrCfg {
-  static constexpr int CIN = 64 * NCH;
-  static constexpr int WROW = (3 * CIN * 2 + 255) / 256 * 256;  // weight-image row bytes
-  static constexpr int W_BYTES = BN * WROW;
-  static constexpr int FI = BN / 16;                             // co fragments per wave
-  static constexpr int SRED_BYTES = 4 * 3 * BN * 4;              // [wave][stat][BN] partials
-  static constexpr int smem(int nst) { return W_BYTES + nst * WR_XSTAGE + SRED_BYTES; }
-};
-
-template <int BN, int NCH, int EPI, int NST>
-__global__ __launch_bounds__(256, 1) void conv1d_nlc_fwd_wr_kernel(FwdArgs a, int MT, int NT, int GM) {
-  using Cfg = WrCfg<BN, NCH>;
-  constexpr int CIN = Cfg::CIN, WROW = Cfg::WROW, FI = Cfg::FI;
+// Two-group LDS-DMA weight gradient (128x128 tiles, 8 waves): the workgroup's row-chunk range is split between two
+// 4-wave groups that run the loop above side by side (each with its own two LDS stages, in lockstep on the one
+// workgroup barrier); at the end group 1 hands its accumulators to group 0 through LDS and group 0 stores the sum.
+// So one 8-wave workgroup per CU does the work of two 4-wave workgroups while writing ONE 64 KB partial tile: the
+// split-K partial traffic (written here, re-read by the reduce) halves at equal occupancy, and the launch needs half
+// the workgroups for the same depth of work per CU.
+template <int NG>
+__global__ __launch_bounds__(256 * NG, NG == 2 ? 2 : 1) void conv1d_nlc_wgrad_dma2_kernel(WgradArgs a, int TM, int TN,
+                                                                                          int splits) {
+  constexpr int BM = 128, BN = 128, NWR = 2;
+  using Cfg = WgCfg<BM, BN, NWR>;
+  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NW = Cfg::NW;  // per group: 4 waves
+  constexpr int RA = BM * 2, RB = BN * 2;
+  constexpr int A_BYTES = 64 * RA, STAGE = 64 * (RA + RB);  // 32 KB
+  constexpr int AP = A_BYTES / 1024 / NW, BP = 64 * RB / 1024 / NW;
+  constexpr int RPP = 1024 / RA, SH = 4, SLOT = RA / 16 - 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* const wimg = smem;
-  unsigned char* const xring = smem + Cfg::W_BYTES;
-  float* const sred = reinterpret_cast<float*>(smem + Cfg::W_BYTES + NST * WR_XSTAGE);
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 4, ml = lane & 15;
+  const int wg = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave in the workgroup
+  const int grp = wg >> 2, wv = wg & 3;                      // group, wave in the group
+  const int wr = wv >> 1, wc = wv & 1;
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int gm = wgid / NT, nt = wgid % NT;  // the NT workgroups of one gm (same activation rows) share an XCD
-  const int n0 = nt * BN;
-  const int L = a.Lout;
-  const int M = a.B * L;
-  const int ntiles = gm < MT ? (MT - gm + GM - 1) / GM : 0;
-  const int total = ntiles * NCH;
-  const srd_t xr = make_rsrc(a.x, (long)M * CIN * 2);
-  const unsigned ring0 = lds_addr(xring);
-  const int prow = lane >> 3;
-  // stage s = (tile j, chunk c): rows m0 - 1 + [0, 136) of channels [64c, 64c + 64); 5 DMA instructions per wave
-  auto issue = [&](int s, int st) {
-    const int j = s / NCH, c = s - j * NCH;
-    const int m0 = (gm + j * GM) * WR_BM;
-    const unsigned base = ring0 + st * WR_XSTAGE;
+  const int tiles = TM * TN;
+  const int split = wgid / tiles, tile = wgid % tiles;
+  const int co0 = (tile / TN) * BM, n0 = (tile % TN) * BN;
+  const int k = n0 / a.Cin, c0 = n0 % a.Cin;
+  const int R = a.B * a.Lout;
+  const int nchunks = (R + 63) / 64;
+  const int w0 = split * a.chunks_per_split, w1 = min(nchunks, w0 + a.chunks_per_split);  // the workgroup's chunks
+  const int half = (w1 - w0 + NG - 1) / NG;                                              // lockstep steps
+  const int ch0 = min(w1, w0 + grp * half), ch1 = min(w1, ch0 + half);                   // this group's chunks
+  unsigned char* const gs = smem + grp * 2 * STAGE;                                      // this group's stages
+  f32x4 acc[FM][FN];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int p = wv + 4 * u, row = 8 * p + prow, r = m0 - 1 + row;
-      const int src = (lane & 7) ^ ((row >> 1) & 7);
-      dma16_at(xr, (r >= 0 && r < M) ? (unsigned)((r * CIN + c * 64 + src * 8) * 2) : 0x7ffffff0u, base + p * 1024);
-    }
-    {  // piece 16 (rows 128..135): lanes 16w .. 16w + 15 of wave w write rows 128 + 2w, 129 + 2w
-      const int row = 128 + prow, r = m0 - 1 + row;
-      const int src = (lane & 7) ^ ((row >> 1) & 7);
-      if ((lane >> 4) == wv)
-        dma16_at(xr, (r >= 0 && r < M) ? (unsigned)((r * CIN + c * 64 + src * 8) * 2) : 0x7ffffff0u,
-                 base + 16 * 1024);
-    }
-  };
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-  for (int i = 0; i < NST - 1; ++i)
-    if (i < total) issue(i, i);
-  // resident weights (plain 16-B loads -> swizzled ds_write_b128; once per workgroup)
-  {
-    constexpr int RCH = 3 * CIN / 8;  // 16-B chunks per weight row
-    constexpr int LPT = BN * RCH / 256;
-    static_assert(LPT * 256 == BN * RCH, "weight image must split evenly over the threads");
-    uint4 wv4[LPT];
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (w0 < w1) {  // block-uniform
+    const int r0 = w0 * 64, b0 = r0 / a.Lout;
+    const long dyrem = (long)(R - r0) * a.Cout * 2, xrem = (long)(a.B - b0) * a.Lin * a.Cin * 2;
+    const srd_t dyr = make_rsrc(a.dy + (long)r0 * a.Cout, dyrem < 0x7fff0000L ? dyrem : 0x7fff0000L);
+    const srd_t xr = make_rsrc(a.x + (long)b0 * a.Lin * a.Cin, xrem < 0x7fff0000L ? xrem : 0x7fff0000L);
+    const unsigned lds_g = lds_addr(gs);
+    int arow[AP], brow[BP];
+    unsigned asrc[AP];
 #pragma unroll
-    for (int u = 0; u < LPT; ++u) {
-      const int q = tid + 256 * u, co = q / RCH, ch = q - co * RCH;
-      wv4[u] = *reinterpret_cast<const uint4*>(a.w + (long)(n0 + co) * (3 * CIN) + ch * 8);
+    for (int i = 0; i < AP; ++i) {
+      arow[i] = RPP * (wv + NW * i) + (lane >> SH);
+      asrc[i] = (unsigned)((co0 + ((lane & SLOT) ^ wg_swz(arow[i])) * 8) * 2);
     }
 #pragma unroll
-    for (int u = 0; u < LPT; ++u) {
-      const int q = tid + 256 * u, co = q / RCH, ch = q - co * RCH;
-      const int phys = (ch & ~15) | ((ch & 15) ^ (co & 15));
-      *reinterpret_cast<uint4*>(wimg + co * WROW + phys * 16) = wv4[u];
-    }
-  }
-  __syncthreads();
-  f32x4 acc[FI][2];
+    for (int i = 0; i < BP; ++i) brow[i] = RPP * (wv + NW * i) + (lane >> SH);
+    auto issue = [&](int ch, int st) {
+      const unsigned base = lds_g + st * STAGE;
+      const int rel = (ch - w0) * 64;
 #pragma unroll
-  for (int i = 0; i < FI; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float st1[FI][4], st2[FI][4], st3[FI][4];
-#pragma unroll
-  for (int i = 0; i < FI; ++i)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) st1[i][q] = st2[i][q] = st3[i][q] = 0.f;
-  const bool ds = EPI == 1 && a.szd != nullptr;
-  bool v0[2] = {true, true}, v2[2] = {true, true};  // this lane's rows: tap 0 / tap 2 inside the sample
-  for (int s = 0; s < total; ++s) {
-    const int ahead = min(NST - 2, total - 1 - s);
-    if constexpr (NST >= 4) {
-      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if constexpr (NST == 3) {
-      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (s + NST - 1 < total) issue(s + NST - 1, (s + NST - 1) % NST);  // into the stage read at s - 1
-    const int j = s / NCH, c = s - j * NCH;
-    const int m0 = (gm + j * GM) * WR_BM;
-    if (c == 0) {
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int m = m0 + 32 * wv + 16 * jj + ml;
-        const int t = m - (m / L) * L;
-        v0[jj] = t != 0;
-        v2[jj] = t != L - 1;
+      for (int i = 0; i < AP; ++i) {
+        const int r = rel + arow[i];
+        const unsigned voff = r0 + r < R ? (unsigned)(r * a.Cout * 2) + asrc[i] : 0x7ffffff0u;
+        dma16_at(dyr, voff, base + (wv + NW * i) * 1024);
       }
-    }
-    const unsigned char* ximg = xring + (s % NST) * WR_XSTAGE;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+      for (int i = 0; i < BP; ++i) {
+        const int rg = r0 + rel + brow[i];
+        const int b = fdiv(rg, a.lout), t = rg - b * a.Lout;
+        const int u = t * a.stride + k - a.pad;
+        const int src = (lane & SLOT) ^ wg_swz(brow[i]);
+        const unsigned voff = (rg < R && u >= 0 && u < a.Lin)
+                                  ? (unsigned)((((long)(b - b0) * a.Lin + u) * a.Cin + c0 + src * 8) * 2)
+                                  : 0x7ffffff0u;
+        dma16_at(xr, voff, base + A_BYTES + (wv + NW * i) * 1024);
+      }
+    };
+    const int q = (lane & 15) >> 2, p4 = (lane & 3) * 4, h = lane >> 4;
+    auto tr_at = [&](const unsigned char* img, int RB_, int rr, int col) -> s16x4 {
+      return tr16(reinterpret_cast<const __bf16*>(img + rr * RB_ + ((((col >> 3) ^ wg_swz(rr))) << 4) +
+                                                  ((col & 7) << 1)));
+    };
+    auto mma = [&](int st) {
+      const unsigned char* As = gs + st * STAGE;
+      const unsigned char* Bs = As + A_BYTES;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        bf16x8 wf[FI], xf[2];
-        const int ch = k * 8 * NCH + c * 8 + ks * 4 + h;
+        typedef short s16x8v __attribute__((ext_vector_type(8)));
+        bf16x8 af[FM], bfr[FN];
+        const int rr = ks * 32 + 8 * h + q;
 #pragma unroll
-        for (int i = 0; i < FI; ++i) {
-          const int co = 16 * i + ml;
-          const int phys = (ch & ~15) | ((ch & 15) ^ (co & 15));
-          wf[i] = *reinterpret_cast<const bf16x8*>(wimg + co * WROW + phys * 16);
+        for (int i = 0; i < FM; ++i) {
+          const int col = wr * WM + i * 16 + p4;
+          const s16x4 lo = tr_at(As, RA, rr, col), hi = tr_at(As, RA, rr + 4, col);
+          s16x8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          af[i] = __builtin_bit_cast(bf16x8, v);
         }
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          const int row = 32 * wv + 16 * jj + ml + k;
-          const int cc = (ks * 4 + h) ^ ((row >> 1) & 7);
-          uint4 v = *reinterpret_cast<const uint4*>(ximg + row * 128 + cc * 16);
-          const bool ok = k == 1 || (k == 0 ? v0[jj] : v2[jj]);
-          if (!ok) v = make_uint4(0u, 0u, 0u, 0u);
-          xf[jj] = __builtin_bit_cast(bf16x8, v);
+        for (int j = 0; j < FN; ++j) {
+          const int col = wc * WN + j * 16 + p4;
+          const s16x4 lo = tr_at(Bs, RB, rr, col), hi = tr_at(Bs, RB, rr + 4, col);
+          s16x8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          bfr[j] = __builtin_bit_cast(bf16x8, v);
         }
 #pragma unroll
-        for (int i = 0; i < FI; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
-            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[jj], acc[i][jj], 0, 0, 0);
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
-    }
-    if (c == NCH - 1) {  // tile j complete: epilogue from registers (rows m, 4 channels per lane and fragment)
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        const int m = m0 + 32 * wv + 16 * jj + ml;
-        if (m < M) {
-#pragma unroll
-          for (int i = 0; i < FI; ++i) {
-            const int co = n0 + 16 * i + 4 * h;
-            const long o = (long)m * a.Cout + co;
-            float v[4] = {acc[i][jj][0], acc[i][jj][1], acc[i][jj][2], acc[i][jj][3]};
-            if (a.bias) {
-              const float4 b4 = *reinterpret_cast<const float4*>(a.bias + co);
-              v[0] += b4.x; v[1] += b4.y; v[2] += b4.z; v[3] += b4.w;
-            }
-            if (a.add) {
-              const bf16x4 ad = *reinterpret_cast<const bf16x4*>(a.add + o);
-              if (a.add_mask) {
-                const bf16x4 mk = *reinterpret_cast<const bf16x4*>(a.add_mask + o);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] += (float)mk[e] > 0.f ? (float)ad[e] : 0.f;
-              } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] += (float)ad[e];
-              }
-            }
-            bf16x4 zz;
-            if constexpr (EPI == 1) {
-              zz = *reinterpret_cast<const bf16x4*>(a.sz + o);
-              if (a.mscale != nullptr) {  // the mask the BN_ACT pass stored, recomputed from sz
-                const float4 sc = *reinterpret_cast<const float4*>(a.mscale + co);
-                const float4 sh = *reinterpret_cast<const float4*>(a.mshift + co);
-                const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                  const __bf16 act = (__bf16)fmaxf(fmaf((float)zz[e], scv[e], shv[e]), 0.f);
-                  v[e] = (float)act > 0.f ? v[e] : 0.f;
-                }
-              } else if (a.smask != nullptr) {
-                const bf16x4 mk = *reinterpret_cast<const bf16x4*>(a.smask + o);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = (float)mk[e] > 0.f ? v[e] : 0.f;
-              }
-            }
-            bf16x4 outv;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              if (a.relu) v[e] = fmaxf(v[e], 0.f);
-              outv[e] = (__bf16)v[e];
-              v[e] = (float)outv[e];
-            }
-            *reinterpret_cast<bf16x4*>(a.y + o) = outv;
-            if (a.stats) {
-              if constexpr (EPI == 1) {
-                const float4 mu4 = *reinterpret_cast<const float4*>(a.smean + co);
-                const float4 rs4 = *reinterpret_cast<const float4*>(a.srstd + co);
-                const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, rs[4] = {rs4.x, rs4.y, rs4.z, rs4.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                  st1[i][e] += v[e];
-                  st2[i][e] += v[e] * ((float)zz[e] - mu[e]) * rs[e];
-                }
-                if (ds) {
-                  const bf16x4 zd = *reinterpret_cast<const bf16x4*>(a.szd + o);
-                  const float4 md4 = *reinterpret_cast<const float4*>(a.smean_d + co);
-                  const float4 rd4 = *reinterpret_cast<const float4*>(a.srstd_d + co);
-                  const float md[4] = {md4.x, md4.y, md4.z, md4.w}, rd[4] = {rd4.x, rd4.y, rd4.z, rd4.w};
-#pragma unroll
-                  for (int e = 0; e < 4; ++e) st3[i][e] += v[e] * ((float)zd[e] - md[e]) * rd[e];
-                }
-              } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                  st1[i][e] += v[e];
-                  st2[i][e] += v[e] * v[e];
-                }
-              }
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < FI; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    const int n = ch1 - ch0;  // 0 <= n <= half (group 1 may have fewer chunks, or none)
+    if (n > 0) issue(ch0, 0);
+    for (int i = 0; i < half; ++i) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // step i's stage landed; step i-1's reads done
+      __builtin_amdgcn_s_barrier();
+      if (i + 1 < n) issue(ch0 + i + 1, (i + 1) & 1);  // into the stage step i-1 read
+      if (i < n) mma(i & 1);
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();  // the activation ring is dead from here (bn_tail scratch)
-  if (a.stats) {  // block-uniform
-    const int NS = ds ? 3 : 2;
+  __syncthreads();  // every stage is dead
+  if constexpr (NG == 2) {  // group 1 -> LDS (lane-linear per accumulator: no conflicts) -> group 0 adds
+    f32x4* red = reinterpret_cast<f32x4*>(smem) + wv * (FM * FN * 64) + lane;
+    if (grp == 1) {
 #pragma unroll
-    for (int i = 0; i < FI; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float s1 = wr_row16_sum(st1[i][e]), s2 = wr_row16_sum(st2[i][e]);
-        const float s3 = ds ? wr_row16_sum(st3[i][e]) : 0.f;
-        if (ml == 15) {
-          sred[(wv * 3 + 0) * BN + 16 * i + 4 * h + e] = s1;
-          sred[(wv * 3 + 1) * BN + 16 * i + 4 * h + e] = s2;
-          sred[(wv * 3 + 2) * BN + 16 * i + 4 * h + e] = s3;
-        }
-      }
-    __syncthreads();
-    for (int p = tid; p < NS * BN; p += 256) {
-      const int st = p / BN, cl = p - st * BN;
-      const float v = ((sred[(0 * 3 + st) * BN + cl] + sred[(1 * 3 + st) * BN + cl]) + sred[(2 * 3 + st) * BN + cl]) +
-                      sred[(3 * 3 + st) * BN + cl];
-      float* dst = a.stats + ((long)st * GM + gm) * a.Cout + n0 + cl;
-      if (a.tail)
-        ecg::st_sc1(dst, v);  // handed to the tail's last arriver inside this launch (write-through)
-      else
-        *dst = v;
+        for (int j = 0; j < FN; ++j) red[(i * FN + j) * 64] = acc[i][j];
     }
-    if (a.tail) ecg::bn_tail<256>(a.tail, a.stats, NS, GM, a.Cout, gm, n0, BN, xring);
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] += red[(i * FN + j) * 64];
+    }
   }
-}
-
-// ECG_CONV_WR = largest C_in that takes the weight-resident tap-shared forward (read once; default 0 = off).
-// Measured on MI355X (profiles/r3/conv_wr_ab.txt): in isolation 13.2 vs 15.6 us at 64 channels but 18.2 vs 15.6
-// (128) and 31.7 vs 22.0 (256) - one 4-wave workgroup per CU leaves the LDS-read -> MFMA latency of each k-step
-// exposed - and inside the ResNet1D-34 step 3.84-4.35 vs 3.75-3.77 ms: its CU-filling persistent grid also
-// crowds out the side-lane weight gradients.  Kept as an opt-in variant.
-inline int conv_wr() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ECG_CONV_WR");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-inline int wr_bn(int Cin) { return Cin == 128 ? 128 : 64; }
-inline bool wr_ok(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad, int in_dil) {
-  return Cin <= conv_wr() && Kw == 3 && stride == 1 && pad == 1 && in_dil == 1 && Lin == Lout && Lout >= 2 &&
-         (Cin == 64 || Cin == 128 || Cin == 256) && Cout % wr_bn(Cin) == 0 &&
-         (long)B * Lout * Cin * 2 < 0x7fff0000L;
-}
-// M-tile groups of the WR grid (= BatchNorm partial rows): about one workgroup per CU in all
-inline int wr_groups(long M, int Cout, int Cin) {
-  const int NT = Cout / wr_bn(Cin);
-  const long MT = (M + WR_BM - 1) / WR_BM;
-  long gm = 256 / NT;
-  if (gm < 1) gm = 1;
-  return (int)(gm < MT ? gm : MT);
-}
-
-template <int BN, int NCH, int EPI>
-int launch_fwd_wr_t(const FwdArgs& a, hipStream_t stream) {
-  constexpr int NST = 3;
-  constexpr int SMEM = WrCfg<BN, NCH>::smem(NST);
-  static_assert(SMEM <= 160 * 1024, "LDS budget");
-  static bool attr = false;
-  if (!attr) {
-    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_wr_kernel<BN, NCH, EPI, NST>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
-    attr = true;
-  }
-  const long M = (long)a.B * a.Lout;
-  const int MT = (int)((M + WR_BM - 1) / WR_BM), NT = a.Cout / BN;
-  const int GM = wr_groups(M, a.Cout, a.Cin);
-  hipLaunchKernelGGL((conv1d_nlc_fwd_wr_kernel<BN, NCH, EPI, NST>), dim3((unsigned)(GM * NT)), dim3(256), SMEM, stream,
-                     a, MT, NT, GM);
-  ECG_HIP_CHECK(hipGetLastError());
-  return ecg::kOk;
-}
-
-int launch_fwd_wr(const FwdArgs& a, hipStream_t stream) {
-  const bool b = a.stat_mode == 1;
-  switch (a.Cin) {
-    case 64: return b ? launch_fwd_wr_t<64, 1, 1>(a, stream) : launch_fwd_wr_t<64, 1, 0>(a, stream);
-    case 128: return b ? launch_fwd_wr_t<128, 2, 1>(a, stream) : launch_fwd_wr_t<128, 2, 0>(a, stream);
-    case 256: return b ? launch_fwd_wr_t<64, 4, 1>(a, stream) : launch_fwd_wr_t<64, 4, 0>(a, stream);
-    default: return ecg::kBadArg;
+  // group 0's waves store the partial tile (LDS-staged float4 rows, as wgrad_epilogue); group 1 joins the barriers
+  constexpr int EP_LD = Cfg::EP_LD, HR = WM / 2;
+  float* ep = reinterpret_cast<float*>(smem) + (NG == 2 ? 64 * 1024 / 4 : 0) + wv * HR * EP_LD;  // past red[]
+  constexpr int C4 = WN / 4, RSTEP = 64 / C4;
+  const int c4 = lane % C4, rs = lane / C4;
+  const long N = (long)a.Kw * a.Cin;
+  float* out = a.part + (long)split * a.Cout * N;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+      for (int i = 0; i < FM / 2; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq)
+            ep[(i * 16 + 4 * (lane >> 4) + qq) * EP_LD + j * 16 + (lane & 15)] = acc[hh * (FM / 2) + i][j][qq];
+    }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll 4
+      for (int r = rs; r < HR; r += RSTEP) {
+        const float4 v = *reinterpret_cast<const float4*>(ep + r * EP_LD + c4 * 4);
+        *reinterpret_cast<float4*>(out + (long)(co0 + wr * WM + hh * HR + r) * N + n0 + wc * WN + c4 * 4) = v;
+      }
+    }
   }
 }
 
@@ -2026,6 +2049,31 @@ inline bool wgrad_dma() {
   return v == 1;
 }
 
+// ECG_WGRAD_G2=0|1: the two-group 8-wave weight gradient for 128x128 tiles (1, default) or the 4-wave kernel (0).
+inline bool wgrad_g2() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ECG_WGRAD_G2");
+    v = e ? atoi(e) : 1;
+  }
+  return v == 1;
+}
+
+int launch_wgrad_dma2(const WgradArgs& a, int splits, hipStream_t stream) {
+  constexpr int SMEM = 2 * 2 * 64 * (128 + 128) * 2;  // two groups x two stages x 32 KB
+  static bool attr = false;
+  if (!attr) {
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_wgrad_dma2_kernel<2>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
+    attr = true;
+  }
+  const int TM = a.Cout / 128, TN = a.Kw * a.Cin / 128;
+  hipLaunchKernelGGL((conv1d_nlc_wgrad_dma2_kernel<2>), dim3((unsigned)(TM * TN * splits)), dim3(512), SMEM, stream, a,
+                     TM, TN, splits);
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
+}
+
 template <int BM, int BN>
 int launch_wgrad_dma(const WgradArgs& a, int splits, hipStream_t stream) {
   constexpr int NWR = BM >= 256 ? 4 : 2;
@@ -2124,7 +2172,7 @@ ECG_API int ecg_conv1d_nlc_fwd_ex2(const void* x, const void* w, const float* bi
   a.ascale = fold_scale;
   a.ashift = fold_shift;
   if (fold_scale) return launch_fwd_fold(a, stream);
-  if (wr_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return launch_fwd_wr(a, stream);
+  if (conv_tap(Cout) && tap_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return launch_fwd_tap(a, stream);
   int bm, bn;
   pick_fwd_tile((long)B * Lout, Cout, in_dil, &bm, &bn);
   if (bm == 256 && bn == 256) return launch_fwd<256, 256>(a, stream);
@@ -2139,6 +2187,14 @@ ECG_API int ecg_conv1d_nlc_fwd_ex2(const void* x, const void* w, const float* bi
 ECG_API int ecg_conv1d_nlc_set_dma_dil(int on) {
   const int prev = conv_dma_dil() ? 1 : 0;
   g_conv_dma_dil = on ? 1 : 0;
+  return prev;
+}
+
+// Select the tap-shared kernel mode (see conv_tap); returns the previous setting.  Step plans size their BatchNorm
+// partial rows when built: set it first.
+ECG_API int ecg_conv1d_nlc_set_tap(int mode) {
+  const int prev = conv_tap_mode();
+  g_conv_tap = mode < 0 ? 0 : (mode > 2 ? 2 : mode);
   return prev;
 }
 
@@ -2176,7 +2232,7 @@ ECG_API int ecg_conv1d_nlc_fwd_stat_tiles_fold(long M, int Cout) {
 ECG_API int ecg_conv1d_nlc_fwd_stat_tiles_ex(int B, int Lout, int Cout, int in_dil);
 ECG_API int ecg_conv1d_nlc_fwd_stat_rows(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad,
                                          int in_dil) {
-  if (wr_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return wr_groups((long)B * Lout, Cout, Cin);
+  if (conv_tap(Cout) && tap_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return tap_mtiles(B, Lout);
   return ecg_conv1d_nlc_fwd_stat_tiles_ex(B, Lout, Cout, in_dil);
 }
 
@@ -2215,7 +2271,8 @@ ECG_API int ecg_conv1d_nlc_wgrad(const void* dy, const void* x, float* part, int
                       (rows / Lout + 2) * (long)Lin * Cin * 2 < 0x7fff0000L;
   if (wgrad_big(Cout, Cin)) return dma_ok ? launch_wgrad_dma<256, 256>(a, splits, stream)
                                           : launch_wgrad<256, 256>(a, splits, stream);
-  if (bm128 && bn128 && dma_ok) return launch_wgrad_dma<128, 128>(a, splits, stream);
+  if (bm128 && bn128 && dma_ok) return wgrad_g2() ? launch_wgrad_dma2(a, splits, stream)
+                                                   : launch_wgrad_dma<128, 128>(a, splits, stream);
   if (bm128 && bn128) return launch_wgrad<128, 128>(a, splits, stream);
   if (bm128) return launch_wgrad<128, 64>(a, splits, stream);
   if (bn128) return launch_wgrad<64, 128>(a, splits, stream);
@@ -2244,5 +2301,14 @@ ECG_API int ecg_conv1d_nlc_wgrad_splits(int B, int Lin, int Cin, int Lout, int C
 // tiles, ~2 rounds of one per CU for the 8-wave 256x256 tile.
 ECG_API int ecg_conv1d_nlc_wgrad_target_wgs(int Cout, int Kw, int Cin) {
   (void)Kw;
-  return wgrad_big(Cout, Cin) ? 512 : 1024;
+  if (wgrad_big(Cout, Cin)) return 512;
+  if (Cout % 128 == 0 && Cin % 128 == 0 && wgrad_g2()) {  // 8-wave workgroups, one per CU
+    static int t = -1;
+    if (t < 0) {
+      const char* e = getenv("ECG_WGRAD_TARGET");
+      t = e ? atoi(e) : 512;
+    }
+    return t;
+  }
+  return 1024;
 }

@@ -189,3 +189,40 @@ def test_conv1d_nlc_stats_multi_tile(mode, B, L, C):
     s1, s2 = stats.double().sum(1)
     torch.testing.assert_close(s1, yd.sum(0), rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(s2, (yd * yd).sum(0), rtol=1e-5, atol=1e-3)
+
+
+TAP_CASES = [  # stride-1 pad-1 3-tap convs on the tap-shared 256-row kernel: sample boundaries inside fragments,
+    (3, 37, 64, 128),  # ragged last M tile (111 rows), one 64-channel chunk
+    (5, 8, 128, 128),  # L = 8: boundaries every 8 rows
+    (7, 2, 128, 256),  # L = 2: every row is a boundary row for one of the outer taps
+    (300, 63, 128, 128),  # the ResNet layer-2 shape, 74 M tiles, ragged last tile
+    (33, 16, 512, 512),  # 8 chunks x 3 taps, 4 column blocks
+    (40, 125, 64, 64),  # 64-column tiles (mode 2)
+]
+
+
+@pytest.mark.parametrize("B,L,Cin,Cout", TAP_CASES)
+def test_tap_shared_forward_matches_fp64(B, L, Cin, Cout):
+    """The tap-shared kernel (A' image staged once per chunk, taps read at row offsets 0/1/2, outer taps masked at
+    sample boundaries) against an fp64 conv of the same bf16 inputs, plus its BatchNorm partial rows against the
+    statistics of its own stored outputs."""
+    from crossscale_ecg.ops import conv_mc
+    prev = conv_mc.set_tap_shared(2)
+    try:
+        torch.manual_seed(11)
+        x = torch.randn(B, L, Cin, device=DEV).bfloat16()
+        w = (torch.randn(Cout, 3, Cin, device=DEV) / (3 * Cin) ** 0.5).bfloat16()
+        y = conv_mc.fwd_raw(x, w, None, 1, 1, L)
+        ys, stats = conv_mc.fwd_stats_raw(x, w, 1, 1, L)
+        torch.cuda.synchronize()
+        assert stats.shape[1] == (B * L + 255) // 256  # one partial row per 256-row tile
+    finally:
+        conv_mc.set_tap_shared(prev)
+    ref = F.conv1d(x.double().transpose(1, 2), w.double().permute(0, 2, 1), None, stride=1, padding=1)
+    got = y.double().transpose(1, 2)
+    assert (got - ref).abs().max().item() <= 8e-3 * ref.abs().max().item()
+    assert _rel(got, ref) < 4e-3
+    assert torch.equal(y, ys)
+    yf = ys.float().reshape(-1, Cout)
+    assert torch.allclose(stats[0].sum(0), yf.sum(0), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(stats[1].sum(0), (yf * yf).sum(0), rtol=1e-4, atol=1e-2)
