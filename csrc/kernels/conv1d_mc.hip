@@ -2306,7 +2306,7 @@ ECG_API int ecg_conv1d_nlc_wgrad_target_wgs(int Cout, int Kw, int Cin) {
     static int t = -1;
     if (t < 0) {
       const char* e = getenv("ECG_WGRAD_TARGET");
-      t = e ? atoi(e) : 512;
+      t = e ? atoi(e) : 256;
     }
     return t;
   }
