@@ -41,9 +41,9 @@ def prec_id(precision: str) -> int:
 
 
 def prefrag_default() -> bool:
-    """Prepared fragments (PF) on by default; ECG_TINY_PREFRAG=0 builds the conv operands in LDS every step
-    (A/B knob: both paths are bitwise identical, csrc/kernels/tiny_ecg_step.hip WP_* comment)."""
-    return os.environ.get("ECG_TINY_PREFRAG", "1") != "0"
+    """Prepared fragments (PF) on by default (``prefrag=False`` builds the conv operands in LDS every step: both
+    paths are bitwise identical, csrc/kernels/tiny_ecg_step.hip WP_* comment)."""
+    return True
 
 
 def new_wprep(device) -> torch.Tensor:
@@ -59,21 +59,13 @@ def _wprep_ptr(precision: str, prefrag: Optional[bool], device, wprep: Optional[
     return w.data_ptr(), w
 
 
-def head_steps_default() -> int:
-    """Steps of a short head graph a PF round is split into (ECG_TINY_HEAD; default 0 = one graph per round).  The
-    idea: the GPU starts on the head while the runtime still submits the long tail graph.  Measured slower at every
-    split (K=20: 11.8-12.0 us/step unsplit vs 12.0-12.2 split; K=500: 10.89 vs 11.20; profiles/r3/
-    tiny_head_split_ab.txt), so it stays an opt-in knob."""
-    return max(0, int(os.environ.get("ECG_TINY_HEAD", "0")))
-
-
 def gather_default() -> bool:
     """PF round graphs gather every step's windows and labels into a contiguous ping-pong buffer inside the
-    previous step's reduce launch (ECG_TINY_GATHER, default 1), so the step kernel stages row b without the
+    previous step's reduce launch (on by default; the ``gather`` attribute of a trainer), so the step kernel stages row b without the
     dependent idx -> window load (csrc/kernels/tiny_ecg_step.hip GatherArgs).  Measured: step kernel 7.76 -> 7.52
     us and step period 12.35 -> 12.08 us under the kernel tracer (medians of 687 steps), bench K=500 11.17 -> 11.06
     us/step (profiles/r3/tiny_gather_ab.txt)."""
-    return os.environ.get("ECG_TINY_GATHER", "1") != "0"
+    return True
 
 
 def slab_stride(num_classes: int) -> int:
@@ -218,7 +210,6 @@ class FusedTinyTrainer:
         pf = prefrag_default() if prefrag is None else bool(prefrag)
         self.prefrag = pf and precision == "bf16" and not self.single_launch and not self.persistent
         self.wprep = new_wprep(self.device) if self.prefrag else None
-        self.head = head_steps_default() if self.prefrag else 0
         self.gather = gather_default() if self.prefrag else False
         self.xg = self.yg = None
         if self.gather:
@@ -280,9 +271,10 @@ class FusedTinyTrainer:
         return g
 
     def _round_graphs(self, n: int):
-        """The graphs one replay of an n-step round launches, in order."""
-        if self.prefrag and 0 < self.head < n:
-            return [self._part_graph(self.head, 0), self._part_graph(n - self.head, self.head)]
+        """The graphs one replay of an n-step round launches, in order (one graph: a round split into a short head
+        graph + the tail graph, so the GPU starts while the runtime still submits the tail, measured slower at
+        every split - K=20: 11.8-12.0 vs 12.0-12.2 us/step, K=500: 10.89 vs 11.20, profiles/r3/
+        tiny_head_split_ab.txt - and was removed)."""
         return [self._graph_for(n)]
 
     def _swap_tables(self) -> None:

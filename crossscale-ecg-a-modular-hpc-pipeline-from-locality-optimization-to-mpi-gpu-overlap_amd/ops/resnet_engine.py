@@ -57,7 +57,6 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_target_wgs", [i32, i32, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_splits", [i32] * 8)
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles_ex", [i32, i32, i32, i32])
-    _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles_fold", [ctypes.c_long, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_rows", [i32] * 9)
     lib._plan_bound = True
     if lib.ecg_plan_op_words() != OP_WORDS or lib.ecg_plan_wentry_bytes() != 40:
@@ -221,7 +220,7 @@ class ResNetStepEngine:
             target = self.lib.ecg_conv1d_nlc_wgrad_target_wgs(Cout, K, Cin)
             # A/B knob: capping the splits shrinks the reduce (S x |dW|) but starves the wgrad kernel of workgroups
             # (B=1024: cap 16 -> 5.86, cap 8 -> 7.66 ms/step vs 4.61 uncapped, profiles/r2/resnet_conv_ab.txt)
-            cap = int(os.environ.get("ECG_WGRAD_MAX_SPLITS", "64"))
+            cap = 64
             return max(1, min(cap, 256, max(1, chunks // 8), max(1, target // tiles)))
 
         ws_need = 0
@@ -306,11 +305,10 @@ class ResNetStepEngine:
         def tail(T, Cout, fins) -> int:
             if not use_tail:
                 return 0
-            # level-1 group size: <= 32 groups, so level 2 reads at most 32 fp64 group rows (bn_tail.h).  ECG_BN_TAIL_GS
-            # overrides it (A/B: ~sqrt(2T) groups, i.e. fewer, larger level-1 groups, measured 3.83-3.85 vs
-            # 3.78-3.79 ms/step at B=1024, profiles/r3/resnet_epi_tail_ab.txt)
-            gs_env = int(os.environ.get("ECG_BN_TAIL_GS", "0"))
-            gs = gs_env if gs_env > 0 else max(8, -(-T // 32))
+            # level-1 group size: <= 32 groups, so level 2 reads at most 32 fp64 group rows (bn_tail.h).  (Fewer,
+            # larger level-1 groups - ~sqrt(2T) - measured 3.83-3.85 vs 3.78-3.79 ms/step at B=1024,
+            # profiles/r3/resnet_epi_tail_ab.txt.)
+            gs = max(8, -(-T // 32))
             NG = (T + gs - 1) // gs
             cnt = torch.zeros((Cout // 64) * (NG + 1), dtype=torch.int32, device=dev)
             self._keep.append(cnt)
@@ -324,31 +322,20 @@ class ResNetStepEngine:
 
         # data-grad epilogues re-derive the BN1 ReLU mask from z1 and BN1's scale/shift instead of reading the stored
         # activation a1 (bitwise the same mask: the BN_ACT expression repeated; one activation read less per block).
-        # ECG_DGRAD_MASK_FROM_Z=0: read a1.
-        mask_from_z = os.environ.get("ECG_DGRAD_MASK_FROM_Z", "1") != "0"
-        # BN-backward apply: ECG_BN_APPLY_RPT=2|4 runs several rows per thread at a fixed channel group (per-channel
-        # coefficients loaded once per thread; bitwise the same output) - measured slower than one 8-channel vector
-        # per thread (B=1024: 3.83-3.87 vs 3.79-3.80 ms/step, profiles/r2/resnet_multi_tile/bn_apply_rpt_ab.txt)
-        apply_rpt = int(os.environ.get("ECG_BN_APPLY_RPT", "0"))
-
-        # BN1 + ReLU folded into conv2's A-operand load (register-staged loop): conv2 reads z1 and stages exactly the
-        # a1 values BN_ACT would write; BN_ACT itself moves to the side lane (a1 is read only by the side-lane
-        # weight gradient, the data-grad mask being re-derived from z1).  ECG_BN_FOLD=1: stages with >= 128
-        # channels (the 64-channel stage keeps its multi-tile LDS-DMA conv), 2: every stage, 0 (default): off -
-        # measured slower (B=1024: 3.85 vs 3.755 ms/step, profiles/r2/resnet_multi_tile/bn_fold_ab.txt): the
-        # register-staged loop the fold needs is slower than the LDS-DMA loop by more than the BN_ACT pass costs.
-        bn_fold = int(os.environ.get("ECG_BN_FOLD", "0")) if (mask_from_z and side) else 0
-
+        # BN-backward apply: one 8-channel vector per thread (several rows per thread at a fixed channel group -
+        # per-channel coefficients loaded once - measured slower: 3.83-3.87 vs 3.79-3.80 ms/step at B=1024,
+        # profiles/r2/resnet_multi_tile/bn_apply_rpt_ab.txt; BN1 + ReLU folded into conv2's register-staged
+        # operand load measured slower than the LDS-DMA loop + BN_ACT pass: 3.85 vs 3.755,
+        # profiles/r2/resnet_multi_tile/bn_fold_ab.txt - both removed in round 4)
         def conv(x, Lin, Cin, w_ptr, y, Lout, Cout, K, s, p, dil=1, st=None, add=None, add_mask=None, bnb=None,
-                 tail_ptr=0, lane=0, mbn=None, afold=None):
+                 tail_ptr=0, lane=0, mbn=None):
             # bnb = (mask, z, mean, rstd, zd, mean_d, rstd_d): BN-backward statistics fused into the epilogue;
             # mbn = (scale, shift): the mask is relu(z * scale + shift) > 0 (mask operand not read)
             extra = [P(t) if isinstance(t, torch.Tensor) else int(t or 0) for t in (bnb or ())]
             extra += [0] * (7 - len(extra))
-            m_words = [P(mbn[0]), P(mbn[1])] if (mbn is not None and mask_from_z) else [0, 0]
-            f_words = [P(afold[0]), P(afold[1])] if afold is not None else [0, 0]
+            m_words = [P(mbn[0]), P(mbn[1])] if mbn is not None else [0, 0]
             op("CONV_FWD", P(x), w_ptr, 0, P(y), P(st), P(add), P(add_mask), B, Lin, Cin, Lout, Cout, K, s, p, dil, 0,
-               *extra, tail_ptr, *m_words, *f_words, lane=lane)
+               *extra, tail_ptr, *m_words, lane=lane)
 
         def wgrad(dy, x, Lin, Cin, Lout, Cout, K, s, p, weight):
             S = wsplits(B * Lout, Cout, K, Cin, s, Lin, Lout)
@@ -384,11 +371,10 @@ class ResNetStepEngine:
                  tail_ptr=tail(T, Co, [fin_fwd_words(b1, B * Lo)]))
             if not use_tail:
                 fin_fwd(b1, T, B * Lo)
-            fold = bn_fold == 2 or (bn_fold == 1 and Co >= 128)
-            op("BN_ACT", 0, P(a["z1"]), P(b1.scale), P(b1.shift), 0, 0, 0, P(a["a1"]), B * Lo, Co, lane=1 if fold else 0)
-            T2 = self.lib.ecg_conv1d_nlc_fwd_stat_tiles_fold(B * Lo, Co) if fold else rows(Lo, Co, Lo, Co, 3, 1, 1)
-            conv(a["z1"] if fold else a["a1"], Lo, Co, self._wf[id(blk.conv2)], a["z2"], Lo, Co, 3, 1, 1, st=stats,
-                 tail_ptr=tail(T2, Co, [fin_fwd_words(b2, B * Lo)]), afold=(b1.scale, b1.shift) if fold else None)
+            op("BN_ACT", 0, P(a["z1"]), P(b1.scale), P(b1.shift), 0, 0, 0, P(a["a1"]), B * Lo, Co)
+            T2 = rows(Lo, Co, Lo, Co, 3, 1, 1)
+            conv(a["a1"], Lo, Co, self._wf[id(blk.conv2)], a["z2"], Lo, Co, 3, 1, 1, st=stats,
+                 tail_ptr=tail(T2, Co, [fin_fwd_words(b2, B * Lo)]))
             if not use_tail:
                 fin_fwd(b2, T2, B * Lo)
             if bd is not None:
@@ -455,7 +441,7 @@ class ResNetStepEngine:
                     fin_bwd(bd, T2, R, 2, base)
             op("BN_BWD_APPLY", 1 if bd is not None else 0, P(dzm), 0, P(a["z2"]), P(b2.mean), P(b2.rstd),
                P(b2.scale), P(b2.c1), P(b2.c2), P(dz2), P(a.get("zd")), P(bd.mean) if bd else 0,
-               P(bd.rstd) if bd else 0, P(bd.scale) if bd else 0, P(bd.c2) if bd else 0, P(dzd), R, Co, apply_rpt)
+               P(bd.rstd) if bd else 0, P(bd.scale) if bd else 0, P(bd.c2) if bd else 0, P(dzd), R, Co)
             wgrad(dz2, a["a1"], Lo, Co, Lo, Co, 3, 1, 1, blk.conv2.weight)
             # dgrad conv2 (stride 1, pad 1) -> ReLU-masked grad wrt a1 + BN1 backward statistics
             T1 = rows(Lo, Co, Lo, Co, 3, 1, 1)
@@ -465,7 +451,7 @@ class ResNetStepEngine:
             if not use_tail:
                 fin_bwd(b1, T1, R, 1, stats.data_ptr())
             op("BN_BWD_APPLY", 0, P(ga1), 0, P(a["z1"]), P(b1.mean), P(b1.rstd), P(b1.scale), P(b1.c1),
-               P(b1.c2), P(dz1), 0, 0, 0, 0, 0, 0, R, Co, apply_rpt)
+               P(b1.c2), P(dz1), 0, 0, 0, 0, 0, 0, R, Co)
             wgrad(dz1, a["in"], Li, Ci, Lo, Co, 3, s, 1, blk.conv1.weight)
             add = dzm
             if bd is not None:
@@ -551,8 +537,8 @@ class ResNetStepEngine:
     def _exec(self, key: str, begin: int, end: int):
         # With the side lane the plan runs eagerly: measured on MI355X (ResNet1D-34 B=1024, scripts/
         # diag_resnet_side.py) the fork-join plan takes 3.94 ms/step enqueued directly but 8.05 as a replayed
-        # hipGraph (one stream: 4.56 either way).  ECG_RESNET_SIDE_GRAPH=1 replays the fork-join graph anyway.
-        if self.use_graph and (not self.side_lane or os.environ.get("ECG_RESNET_SIDE_GRAPH") == "1"):
+        # hipGraph (one stream: 4.56 either way).
+        if self.use_graph and not self.side_lane:
             st = self.lib.ecg_plan_graph_launch(self._graph(key, begin, end), _lib.stream_ptr(self.dev))
             _lib.check(st, "ecg_plan_graph_launch")
         else:
@@ -585,7 +571,7 @@ class ResNetStepEngine:
         never waits, so the data-gradient chain runs on beside the weight gradients and the collectives.  Ends
         with the side lane joined into the current stream (before the optimizer)."""
         first = self._segments[0][0]
-        eager = not (self.use_graph and (not self.side_lane or os.environ.get("ECG_RESNET_SIDE_GRAPH") == "1"))
+        eager = not (self.use_graph and not self.side_lane)
         self._exec("fwd", 0, first)
         for i, (b, e, lo, hi) in enumerate(self._segments):
             if eager:

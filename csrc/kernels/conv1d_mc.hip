@@ -56,11 +56,6 @@ struct FwdArgs {
   // exact values the BN_ACT pass stored as smask (conv -> BN -> ReLU), so smask need not be read
   const float* mscale;
   const float* mshift;
-  // A-operand transform (register-staged forward only): when non-null the staged activation is
-  // bf16(max(fmaf(x, ascale[c], ashift[c]), 0)) - a BatchNorm + ReLU folded into the consumer conv's operand load
-  // (padding rows stay zero)
-  const float* ascale;
-  const float* ashift;
   const ecg::BnTail* tail;  // BatchNorm finalize fused into this launch's tail (bn_tail.h), or null
 };
 
@@ -417,11 +412,11 @@ __device__ __forceinline__ void fwd_epilogue(const FwdArgs& a, f32x4 (&acc)[BM /
   if (a.stats) fwd_epi_stats<BM, BN, EPI, NWR>(a, smem, k, n0, mt, MT);  // block-uniform
 }
 
-// NBUF = 2: double-buffered LDS, one barrier per K tile (2 workgroups / CU at 128x128).
-// NBUF = 1: one LDS buffer, two barriers per K tile, half the LDS -> 3 workgroups / CU, i.e. 1.5x the
-//           register-staged tiles in flight per CU for this HBM-latency-bound loop.
-template <int BM, int BN, int EPI, int NBUF>
-__global__ __launch_bounds__(THREADS, NBUF == 1 ? 3 : 2) void conv1d_nlc_fwd_kernel(FwdArgs a, int MT, int NT) {
+// Register-staged forward / data-grad, the fallback of the LDS-DMA loops (operands beyond 32-bit buffer offsets):
+// one LDS buffer, two barriers per K tile, three workgroups per CU; tile t+1's global loads are in flight during
+// tile t's MFMAs.
+template <int BM, int BN, int EPI>
+__global__ __launch_bounds__(THREADS, 3) void conv1d_nlc_fwd_kernel(FwdArgs a, int MT, int NT) {
   using Cfg = FwdCfg<BM, BN>;
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NA = Cfg::NA, NB = Cfg::NB;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -467,14 +462,10 @@ __global__ __launch_bounds__(THREADS, NBUF == 1 ? 3 : 2) void conv1d_nlc_fwd_ker
   }
   const __bf16* wb = a.w + (long)(n0 + (tid >> 3)) * (a.Kw * a.Cin) + (tid & 7) * 8;
   const int Lext = a.in_dil > 1 ? (a.Lin - 1) * a.in_dil + 1 : a.Lin;  // extent of the (dilated) input
-  const bool fold = a.ascale != nullptr;  // block-uniform
-  unsigned aok = 0u;  // rows of the staged A set that are real input rows (fold: padding stays zero)
-  float4 asc0, asc1, ash0, ash1;  // the staged set's 8 channels' BN scale / shift (fold)
   auto ld_set = [&](uint4* ra, uint4* rb, int t) {
     const int tc = t < nk ? t : nk - 1;
     const int k = k0 + (tc / CB) * P, c0 = (tc % CB) * BK;
     const int kk = k * a.Cin + c0;
-    aok = 0u;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       int u = apos[i] + k;
@@ -483,37 +474,15 @@ __global__ __launch_bounds__(THREADS, NBUF == 1 ? 3 : 2) void conv1d_nlc_fwd_ker
         ok = ok && (u % a.in_dil == 0);
         u /= a.in_dil;
       }
-      aok |= (ok ? 1u : 0u) << i;
       ra[i] = ok ? *reinterpret_cast<const uint4*>(a.x + abase[i] + (long)u * a.Cin + c0) : make_uint4(0u, 0u, 0u, 0u);
-    }
-    if (fold) {  // (every A piece of this thread covers channels c0 + (tid & 7) * 8 .. + 8)
-      const float4* sp = reinterpret_cast<const float4*>(a.ascale + c0 + (tid & 7) * 8);
-      const float4* hp = reinterpret_cast<const float4*>(a.ashift + c0 + (tid & 7) * 8);
-      asc0 = sp[0];
-      asc1 = sp[1];
-      ash0 = hp[0];
-      ash1 = hp[1];
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i)
       rb[i] = *reinterpret_cast<const uint4*>(wb + (long)i * (THREADS / 8) * (a.Kw * a.Cin) + kk);
   };
   auto st_set = [&](__bf16* base, const uint4* ra, const uint4* rb) {
-    if (fold) {
-      const float sc[8] = {asc0.x, asc0.y, asc0.z, asc0.w, asc1.x, asc1.y, asc1.z, asc1.w};
-      const float sh[8] = {ash0.x, ash0.y, ash0.z, ash0.w, ash1.x, ash1.y, ash1.z, ash1.w};
 #pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        bf16x8 v = __builtin_bit_cast(bf16x8, ra[i]);
-        const bool ok = (aok >> i) & 1u;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = ok ? (__bf16)fmaxf(fmaf((float)v[e], sc[e], sh[e]), 0.f) : (__bf16)0.f;
-        store_one(base, tid + i * THREADS, __builtin_bit_cast(uint4, v));
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NA; ++i) store_one(base, tid + i * THREADS, ra[i]);
-    }
+    for (int i = 0; i < NA; ++i) store_one(base, tid + i * THREADS, ra[i]);
 #pragma unroll
     for (int i = 0; i < NB; ++i) store_one(base + Cfg::A_EL, tid + i * THREADS, rb[i]);
   };
@@ -537,26 +506,19 @@ __global__ __launch_bounds__(THREADS, NBUF == 1 ? 3 : 2) void conv1d_nlc_fwd_ker
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   };
-  __bf16* const L0 = lds;
-  __bf16* const L1 = lds + (NBUF == 2 ? Cfg::A_EL + Cfg::B_EL : 0);
   if (nk > 0) {  // block-uniform (a phase without taps leaves acc = 0)
     ld_set(ra0, rb0, 0);
-    st_set(L0, ra0, rb0);
+    st_set(lds, ra0, rb0);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       ld_set(ra0, rb0, kt + 1);
-      if constexpr (NBUF == 2) {
-        mma((kt & 1) ? L1 : L0);
-        st_set((kt & 1) ? L0 : L1, ra0, rb0);
-      } else {
-        mma(L0);
-        __syncthreads();  // every wave is done reading the buffer
-        st_set(L0, ra0, rb0);
-      }
+      mma(lds);
+      __syncthreads();  // every wave is done reading the buffer
+      st_set(lds, ra0, rb0);
       __syncthreads();
     }
   }
-  fwd_epilogue<BM, BN, EPI, 2, (NBUF == 2)>(a, acc, smem, m0, n0, mt, MT, Lrow, M, P, ph);  // NBUF 1: 168 VGPRs
+  fwd_epilogue<BM, BN, EPI, 2, false>(a, acc, smem, m0, n0, mt, MT, Lrow, M, P, ph);  // row-wise form: 168 VGPRs
   if (a.tail && a.stats) ecg::bn_tail<THREADS>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, MT, a.Cout, mt, n0, BN, smem);
 }
 
@@ -601,9 +563,10 @@ __device__ __forceinline__ void dma16(srd_t r, unsigned voff, unsigned char* lds
 }
 
 // NWR = waves along M: 2 -> 4 waves (2x2), 4 -> 8 waves (4x2, 2 per SIMD at one workgroup per CU).  256-row
-// tiles need one workgroup per CU (2 x 64 KB of stages at 256x256).  NST = LDS stages: 2 (one K step in flight
-// while the MFMAs run) or 3 (two in flight; the 24 KB stages of the 128x64 tile still fit two workgroups per CU).
-template <int BM, int BN, int EPI, int NWR, int NST = 2>
+// tiles need one workgroup per CU (2 x 64 KB of stages at 256x256).  Two LDS stages: one K step in flight while the
+// MFMAs run (three stages measured slower or neutral for every tile: profiles/r2/resnet_conv_ab.txt,
+// profiles/r3/resnet_tile256_wgrad_ab.txt).
+template <int BM, int BN, int EPI, int NWR>
 __global__ __launch_bounds__(128 * NWR, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_dma_kernel(FwdArgs a, int MT, int NT) {
   using Cfg = FwdCfg<BM, BN, NWR>;
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN, NW = Cfg::NW;
@@ -697,39 +660,16 @@ __global__ __launch_bounds__(128 * NWR, BM >= 256 ? 1 : 2) void conv1d_nlc_fwd_d
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   };
-  if constexpr (NST == 2) {
-    if (nk > 0) {
-      issue(0, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);  // lands during this step's MFMAs
-        mma(kt & 1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next stage has landed (this wave's pieces) ...
-        __syncthreads();                                  // ... for every wave, and nobody reads stage kt any more
-      }
-    }
-  } else {
-    // three stages: K steps kt+1 and kt+2 stream in while step kt's MFMAs run.  Each thread issues AP + BP
-    // DMA loads per stage, so "stage kt landed" = at most one younger stage's loads still outstanding.
-    constexpr int LPS = AP + BP;
-    if (nk > 0) issue(0, 0);
-    if (nk > 1) issue(1, 1);
+  if (nk > 0) {
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // stage kt landed for every wave; every wave is past mma(kt - 1).  A raw barrier: __syncthreads() would
-      // emit vmcnt(0) and drain stage kt+1's DMA, which must stay in flight across it (guide: "Pipelining across
-      // barriers"); the ds_reads of mma(kt - 1) retired with lgkmcnt(0)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);  // into the buffer mma(kt - 1) read
-      mma(kt % 3);
+      if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);  // lands during this step's MFMAs
+      mma(kt & 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next stage has landed (this wave's pieces) ...
+      __syncthreads();                                  // ... for every wave, and nobody reads stage kt any more
     }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();  // the epilogue reuses the stage buffers
   }
   fwd_epilogue<BM, BN, EPI, NWR, (BM < 256)>(a, acc, smem, m0, n0, mt, MT, Lrow, M, P, ph);
   if (a.tail && a.stats)
@@ -1054,37 +994,25 @@ inline bool conv_tap(int Cout) {
   return v >= 2 || (v == 1 && Cout % 128 == 0);
 }
 
-inline bool conv_dma();
 inline int conv_big();
 inline int conv_mt();
 
-// Tile choice: with the LDS-DMA loop (undilated input) 256x256 (8 waves of 64x128) when that gives >= 2 tiles
-// per CU (one workgroup per CU; half the L2->LDS bytes per MAC of 128x128: 1.04 vs 0.87 PF/s on the
-// ResNet layer4 shape, profiles/r1_resnet/cmb_p3_big*.log), [256x128 opt-in: measured slower], else 128x128 when that still gives >= 1 workgroup per CU (256 CUs), else 128x64,
-// else 64x64.
+// Tile choice for the one-tap kernels (every conv the tap-shared kernel does not take: strided convs, 1x1 downsample
+// convs, strided data-grads, 64-channel outputs): 256x256 (8 waves of 64x128) when that gives >= 2 tiles per CU (one
+// workgroup per CU; half the L2->LDS bytes per MAC of 128x128: 1.04 vs 0.87 PF/s on the ResNet layer-4 shape at
+// B=4096, profiles/r1_resnet/cmb_p3_big*.log), 256x128 only in the opt-in family 2 (measured neutral), else 128x128
+// when that still gives >= 1 workgroup per CU, else 128x64, else 64x64.
 inline void pick_fwd_tile(long M, int Cout, int in_dil, int* bm, int* bn) {
-  // ECG_CONV_TILE=<bm>x<bn> forces one tile family wherever it applies (A/B experiments; read once)
-  static int force_bm = -1, force_bn = 0;
-  if (force_bm < 0) {
-    const char* e = getenv("ECG_CONV_TILE");
-    force_bm = 0;
-    if (e && sscanf(e, "%dx%d", &force_bm, &force_bn) != 2) force_bm = 0;
-  }
-  if (force_bm > 0 && Cout % force_bn == 0 && (force_bm <= 128 || (in_dil == 1 && conv_dma()))) {
-    *bm = force_bm;
-    *bn = force_bn;
-    return;
-  }
   const long mt128 = (M + 127) / 128, mt256 = (M + 255) / 256;
-  const int big = (in_dil == 1 && conv_dma()) ? conv_big() : 0;
+  const int big = in_dil == 1 ? conv_big() : 0;
   if (big >= 1 && Cout % 256 == 0 && mt256 * (Cout / 256) >= 512) {
     *bm = 256;
     *bn = 256;
   } else if (big >= 2 && Cout % 128 == 0 && mt256 * (Cout / 128) >= 512) {
     *bm = 256;
     *bn = 128;
-  } else if (Cout == 128 && in_dil == 1 && conv_dma() && conv_mt() >= 2 && mt128 * 2 > 512) {
-    *bm = 128;  // multi-tile 128x64 (ECG_CONV_MT=2)
+  } else if (Cout == 128 && in_dil == 1 && conv_mt() >= 2 && mt128 * 2 > 512) {
+    *bm = 128;  // multi-tile 128x64 (mode 2)
     *bn = 64;
   } else if (Cout % 128 == 0 && mt128 * (Cout / 128) >= 256) {  // >= one tile per CU: 15.1 vs 17.7 us for 128x64
     *bm = 128;                                                      // at M=64512 C=128 (profiles/r2/conv_tiles.txt)
@@ -1098,22 +1026,16 @@ inline void pick_fwd_tile(long M, int Cout, int in_dil, int* bm, int* bn) {
   }
 }
 
-// ECG_CONV_MT=0|1|2: multi-tile forward workgroups (conv1d_nlc_fwd_dma_mt_kernel) for 128x64 tiles when the
-// launch has more tiles than two resident workgroups per CU (1, default), and also for the 128-channel shapes
-// that would otherwise take 128x128 tiles (2); 0 = one tile per workgroup.  Read once.
-int g_conv_mt = -1;
-inline int conv_mt() {
-  if (g_conv_mt < 0) {
-    const char* e = getenv("ECG_CONV_MT");
-    g_conv_mt = e ? atoi(e) : 1;
-  }
-  return g_conv_mt;
-}
+// Multi-tile forward workgroups (conv1d_nlc_fwd_dma_mt_kernel) for 128x64 tiles when the launch has more tiles than
+// two resident workgroups per CU (1, default), also for the 128-channel shapes that would otherwise take 128x128 tiles
+// (2), or never (0): ecg_conv1d_nlc_set_mt (tests).
+int g_conv_mt = 1;
+inline int conv_mt() { return g_conv_mt; }
 
 // Workgroups along M of the multi-tile forward (0: the one-tile-per-workgroup kernels run).  A function of the
 // shape and the tile alone, so the host can size the BatchNorm partial rows (ecg_conv1d_nlc_fwd_stat_tiles).
 inline int fwd_mt_groups(long M, int Cout, int in_dil, int bm, int bn) {
-  if (in_dil != 1 || !conv_dma() || conv_mt() == 0 || bm != 128 || bn != 64) return 0;
+  if (in_dil != 1 || conv_mt() == 0 || bm != 128 || bn != 64) return 0;
   const long MT = (M + bm - 1) / bm, NT = Cout / bn;
   const long slots = 2L * 256;  // two workgroups per CU
   if (MT * NT <= slots) return 0;
@@ -1121,59 +1043,20 @@ inline int fwd_mt_groups(long M, int Cout, int in_dil, int bm, int bn) {
   return (int)((MT + tpw - 1) / tpw);
 }
 
-// ECG_CONV_NBUF=1|2 selects the LDS buffering of the forward/data-grad kernel (read once; default 1).
-inline int conv_nbuf() {
-  static int nb = -1;
-  if (nb < 0) {
-    const char* e = getenv("ECG_CONV_NBUF");
-    nb = (e && atoi(e) == 2) ? 2 : 1;
-  }
-  return nb;
-}
+// 256-row one-tap tiles: 0 = 128-row tiles only, 1 (default) = + 256x256 forward, 2 = + 256x128 forward and 256x256
+// weight-gradient tiles (opt-in family; ecg_conv1d_nlc_set_big, tests).  Plans built before a change keep their tiling.
+int g_conv_big = 1;
+inline int conv_big() { return g_conv_big; }
 
-// ECG_CONV_DMA=0 selects the register-staged main loop for every conv (read once; default: LDS-DMA loop when
-// the input is not dilated).
-inline bool conv_dma() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ECG_CONV_DMA");
-    v = (e && atoi(e) == 0) ? 0 : 1;
-  }
-  return v == 1;
-}
-
-// ECG_CONV_BIG=0|1|2: 256-row tiles (0: 128-row tiles only, 1 (default): + 256x256 forward, 2: + 256x128 forward
-// and 256x256 weight-gradient); read
-// once, overridable with ecg_conv1d_nlc_set_big (tests; plans built before a change keep their tiling).
-int g_conv_big = -1;
-inline int conv_big() {
-  if (g_conv_big < 0) {
-    const char* e = getenv("ECG_CONV_BIG");
-    g_conv_big = e ? atoi(e) : 1;
-  }
-  return g_conv_big;
-}
-
-// ECG_CONV_NST=3 gives the 64-column tiles a three-stage loop (opt-in: ResNet1D-34 B=1024 4.64-4.66 vs 4.61
-// ms/step with two stages, profiles/r2/resnet_conv_ab.txt - the K loops are not bound by DMA latency alone).
-inline int conv_nst64() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ECG_CONV_NST");
-    v = (e && atoi(e) == 3) ? 3 : 2;
-  }
-  return v;
-}
-
-template <int BM, int BN, int EPI, int NST, int NWR = (BM >= 256 ? 4 : 2)>  // 256-row tiles: 8 waves of 64 x BN/2
+template <int BM, int BN, int EPI, int NWR = (BM >= 256 ? 4 : 2)>  // 256-row tiles: 8 waves of 64 x BN/2
 int launch_fwd_dma_st(const FwdArgs& a, hipStream_t stream) {
   using Cfg = FwdCfg<BM, BN, NWR>;
-  constexpr int STAGE_BYTES = NST * (BM + BN) * 128;
+  constexpr int STAGE_BYTES = 2 * (BM + BN) * 128;
   constexpr int SMEM = STAGE_BYTES > Cfg::EP_BYTES ? STAGE_BYTES : Cfg::EP_BYTES;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static bool attr = false;
   if (!attr) {
-    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_dma_kernel<BM, BN, EPI, NWR, NST>,
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_dma_kernel<BM, BN, EPI, NWR>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
     attr = true;
   }
@@ -1187,21 +1070,10 @@ int launch_fwd_dma_st(const FwdArgs& a, hipStream_t stream) {
     MT = (int)(((long)a.B * a.Lout + BM - 1) / BM);
   }
   const int NT = a.Cout / BN;
-  hipLaunchKernelGGL((conv1d_nlc_fwd_dma_kernel<BM, BN, EPI, NWR, NST>), dim3((unsigned)(MT * NT)), dim3(Cfg::NTHR),
-                     SMEM, stream, b, MT, NT);
+  hipLaunchKernelGGL((conv1d_nlc_fwd_dma_kernel<BM, BN, EPI, NWR>), dim3((unsigned)(MT * NT)), dim3(Cfg::NTHR), SMEM,
+                     stream, b, MT, NT);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
-}
-
-// ECG_CONV_NST=3: 64-column tiles take three LDS stages (two workgroups per CU still fit: 2 x 72 KB at 128x64).
-// ECG_CONV_V128=1|2|3: the 128x128 tile with three stages (one workgroup per CU) | eight waves of 32x64 | both.
-inline int conv_v128() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ECG_CONV_V128");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
 }
 
 template <int BM, int BN, int EPI>
@@ -1228,34 +1100,18 @@ int launch_fwd_dma(const FwdArgs& a, hipStream_t stream) {
     const int GM = fwd_mt_groups((long)a.B * a.Lout, a.Cout, a.in_dil, BM, BN);
     if (GM > 0) return launch_fwd_dma_mt<BM, BN, EPI>(a, GM, stream);
   }
-  if constexpr (BN == 64 && BM <= 128) {
-    if (conv_nst64() == 3) return launch_fwd_dma_st<BM, BN, EPI, 3>(a, stream);
-  }
-  if constexpr (BM == 256 && BN == 128) {  // ECG_CONV_NST256=3: three LDS stages (3 x 48 KB) for the 8-wave tile
-    static const int nst = [] {
-      const char* e = getenv("ECG_CONV_NST256");
-      return e && atoi(e) == 3 ? 3 : 2;
-    }();
-    if (nst == 3) return launch_fwd_dma_st<BM, BN, EPI, 3>(a, stream);
-  }
-  if constexpr (BN == 128 && BM == 128) {
-    switch (conv_v128()) {
-      case 1: return launch_fwd_dma_st<BM, BN, EPI, 3, 2>(a, stream);
-      case 2: return launch_fwd_dma_st<BM, BN, EPI, 2, 4>(a, stream);
-      case 3: return launch_fwd_dma_st<BM, BN, EPI, 3, 4>(a, stream);
-      default: break;
-    }
-  }
-  return launch_fwd_dma_st<BM, BN, EPI, 2>(a, stream);
+  return launch_fwd_dma_st<BM, BN, EPI>(a, stream);
 }
 
-template <int BM, int BN, int EPI, int NBUF>
+// Register-staged loop: the fallback for operands beyond the LDS-DMA loop's 32-bit buffer offsets (and, with
+// ecg_conv1d_nlc_set_dma_dil(0), the strided data-grads - a test cross-check).
+template <int BM, int BN, int EPI>
 int launch_fwd_cfg(const FwdArgs& a, hipStream_t stream) {
   using Cfg = FwdCfg<BM, BN>;
-  constexpr int SMEM = Cfg::smem(NBUF);
+  constexpr int SMEM = Cfg::smem(1);
   static bool attr = false;
   if (!attr) {
-    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_kernel<BM, BN, EPI, NBUF>,
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_kernel<BM, BN, EPI>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
     attr = true;
   }
@@ -1269,22 +1125,16 @@ int launch_fwd_cfg(const FwdArgs& a, hipStream_t stream) {
     MT = (int)(((long)a.B * a.Lout + BM - 1) / BM);
   }
   const int NT = a.Cout / BN;
-  hipLaunchKernelGGL((conv1d_nlc_fwd_kernel<BM, BN, EPI, NBUF>), dim3((unsigned)(MT * NT)), dim3(THREADS), SMEM,
-                     stream, b, MT, NT);
+  hipLaunchKernelGGL((conv1d_nlc_fwd_kernel<BM, BN, EPI>), dim3((unsigned)(MT * NT)), dim3(THREADS), SMEM, stream, b,
+                     MT, NT);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
 
-// ECG_CONV_DMA_DIL=0 keeps the strided (phase-decomposed) data-grads on the register-staged loop (read once;
-// default: LDS-DMA loop, two stages).
-int g_conv_dma_dil = -1;
-inline bool conv_dma_dil() {
-  if (g_conv_dma_dil < 0) {
-    const char* e = getenv("ECG_CONV_DMA_DIL");
-    g_conv_dma_dil = (e && atoi(e) == 0) ? 0 : 1;
-  }
-  return g_conv_dma_dil == 1;
-}
+// Strided (phase-decomposed) data-grads on the LDS-DMA loop (1, default) or the register-staged loop (0):
+// ecg_conv1d_nlc_set_dma_dil (tests: the two are bitwise equal).
+int g_conv_dma_dil = 1;
+inline bool conv_dma_dil() { return g_conv_dma_dil == 1; }
 
 template <int BM, int BN>
 int launch_fwd(const FwdArgs& a, hipStream_t stream) {
@@ -1293,18 +1143,13 @@ int launch_fwd(const FwdArgs& a, hipStream_t stream) {
   const bool dma_ok = (a.in_dil == 1 || (conv_dma_dil() && a.stride == 1 && BM <= 128)) &&
                       (long)(BM / Lrow + 2) * a.Lin * a.Cin * 2 < 0x7fff0000L &&
                       (long)a.Cout * a.Kw * a.Cin * 2 < 0x7fff0000L;
-  if (conv_dma() && dma_ok && a.in_dil > 1)  // two stages, one tile per workgroup
-    return a.stat_mode == 1 ? launch_fwd_dma_st<BM, BN, 1, 2>(a, stream) : launch_fwd_dma_st<BM, BN, 0, 2>(a, stream);
-  if (conv_dma() && dma_ok)
-    return a.stat_mode == 1 ? launch_fwd_dma<BM, BN, 1>(a, stream) : launch_fwd_dma<BM, BN, 0>(a, stream);
+  if (dma_ok && a.in_dil > 1)  // two stages, one tile per workgroup
+    return a.stat_mode == 1 ? launch_fwd_dma_st<BM, BN, 1>(a, stream) : launch_fwd_dma_st<BM, BN, 0>(a, stream);
+  if (dma_ok) return a.stat_mode == 1 ? launch_fwd_dma<BM, BN, 1>(a, stream) : launch_fwd_dma<BM, BN, 0>(a, stream);
   if (a.stats && fwd_mt_groups((long)a.B * a.Lout, a.Cout, a.in_dil, BM, BN) > 0)
     return ecg::kBadArg;  // the host sized the partial rows for the multi-tile kernel
   if constexpr (BM > 128) return ecg::kBadArg;  // 256-row tiles exist only as DMA kernels (the picker ensures it)
-  else {
-    if (conv_nbuf() == 2)
-      return a.stat_mode == 1 ? launch_fwd_cfg<BM, BN, 1, 2>(a, stream) : launch_fwd_cfg<BM, BN, 0, 2>(a, stream);
-    return a.stat_mode == 1 ? launch_fwd_cfg<BM, BN, 1, 1>(a, stream) : launch_fwd_cfg<BM, BN, 0, 1>(a, stream);
-  }
+  else return a.stat_mode == 1 ? launch_fwd_cfg<BM, BN, 1>(a, stream) : launch_fwd_cfg<BM, BN, 0>(a, stream);
 }
 
 // ------------------------------------------------------------------------------------------- weight grad
@@ -1958,67 +1803,31 @@ __global__ __launch_bounds__(256, 2) void conv1d_nlc_wgrad_ts_kernel(WgradArgs a
       for (int e = 0; e < 4; ++e) out[(long)(16 * i + hq + e) * N + (long)k * a.Cin] = acc[i][k][e];
 }
 
-// The tap-shared kernel applies (stride 1, pad 1, 3 taps, same length, whole tensors addressable with 32-bit
-// offsets) up to ECG_WGRAD_TS channels (read once; default 64: measured on MI355X, B=1024 ResNet1D-34 shapes,
-// scripts/wgrad_micro.py, profiles/r3/wgrad_ts_ab.txt - 14.1 vs 21.6 us at 64 channels, where the one-tap path
-// is the register-staged 64x64 kernel; slower than the one-tap 128x128 LDS-DMA kernel at 128-512 channels).
-// 0 disables it.
+// The tap-shared weight gradient applies to stride-1, pad-1, 3-tap convs with whole tensors addressable with 32-bit
+// offsets and at most 64 channels (measured on MI355X, B=1024 ResNet1D-34 shapes, scripts/wgrad_micro.py,
+// profiles/r3/wgrad_ts_ab.txt - 14.1 vs 21.6 us at 64 channels, where the one-tap path is the register-staged 64x64
+// kernel; slower than the one-tap 128x128 LDS-DMA kernel at 128-512 channels).  It aims for 256 workgroups (one per
+// CU; the split-K partials are workgroups x 48 KB) and runs a four-stage ring (two chunks in flight).
+constexpr int WGRAD_TS_MAXC = 64, WGRAD_TS_WGS = 256, WGRAD_TS_NST = 4;
 inline bool wgrad_ts_ok(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad) {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ECG_WGRAD_TS");
-    v = e ? atoi(e) : 64;
-  }
   const long R = (long)B * Lout;
-  return Cin <= v && Cout <= v && Kw == 3 && stride == 1 && pad == 1 && Lin == Lout && Lout >= 8 && Cin % 64 == 0 && Cout % 64 == 0 &&
-         R * Cout * 2 < 0x7fff0000L && R * Cin * 2 < 0x7fff0000L;
+  return Cin <= WGRAD_TS_MAXC && Cout <= WGRAD_TS_MAXC && Kw == 3 && stride == 1 && pad == 1 && Lin == Lout &&
+         Lout >= 8 && Cin % 64 == 0 && Cout % 64 == 0 && R * Cout * 2 < 0x7fff0000L && R * Cin * 2 < 0x7fff0000L;
 }
 
-// Workgroups the tap-shared launch aims for (ECG_WGRAD_TS_WGS, default 256: one per CU; the split-K partials are
-// workgroups x 48 KB).
-inline int wgrad_ts_target() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ECG_WGRAD_TS_WGS");
-    v = e ? atoi(e) : 256;
-    if (v < 8) v = 8;
-  }
-  return v;
-}
-
-// ECG_WGRAD_TS_NST = LDS stages of the tap-shared loop (2..4, default 4: two chunks in flight); read once.
-inline int wgrad_ts_nst() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ECG_WGRAD_TS_NST");
-    v = e ? atoi(e) : 4;
-    if (v < 2 || v > 4) v = 4;
-  }
-  return v;
-}
-
-template <int NST>
-int launch_wgrad_ts_n(const WgradArgs& a, int splits, hipStream_t stream) {
-  constexpr int SMEM = NST * TSW_STAGE;
+int launch_wgrad_ts(const WgradArgs& a, int splits, hipStream_t stream) {
+  constexpr int SMEM = WGRAD_TS_NST * TSW_STAGE;
   static bool attr = false;
   if (!attr) {
-    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_wgrad_ts_kernel<NST>,
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_wgrad_ts_kernel<WGRAD_TS_NST>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
     attr = true;
   }
   const int TM = a.Cout / 64, TN = a.Cin / 64;
-  hipLaunchKernelGGL(conv1d_nlc_wgrad_ts_kernel<NST>, dim3((unsigned)(TM * TN * splits)), dim3(256), SMEM, stream, a,
-                     TM, TN, splits);
+  hipLaunchKernelGGL(conv1d_nlc_wgrad_ts_kernel<WGRAD_TS_NST>, dim3((unsigned)(TM * TN * splits)), dim3(256), SMEM,
+                     stream, a, TM, TN, splits);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
-}
-
-int launch_wgrad_ts(const WgradArgs& a, int splits, hipStream_t stream) {
-  switch (wgrad_ts_nst()) {
-    case 2: return launch_wgrad_ts_n<2>(a, splits, stream);
-    case 3: return launch_wgrad_ts_n<3>(a, splits, stream);
-    default: return launch_wgrad_ts_n<4>(a, splits, stream);
-  }
 }
 
 template <int BM, int BN>
@@ -2037,26 +1846,6 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t stream) {
                      Cfg::SMEM, stream, a, TM, TN, splits);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
-}
-
-// ECG_WGRAD_DMA=0 selects the register-staged weight-gradient loop (read once; default: LDS-DMA for 128x128).
-inline bool wgrad_dma() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ECG_WGRAD_DMA");
-    v = (e && atoi(e) == 0) ? 0 : 1;
-  }
-  return v == 1;
-}
-
-// ECG_WGRAD_G2=0|1: the two-group 8-wave weight gradient for 128x128 tiles (1, default) or the 4-wave kernel (0).
-inline bool wgrad_g2() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ECG_WGRAD_G2");
-    v = e ? atoi(e) : 1;
-  }
-  return v == 1;
 }
 
 int launch_wgrad_dma2(const WgradArgs& a, int splits, hipStream_t stream) {
@@ -2108,46 +1897,11 @@ inline bool wgrad_big(int Cout, int Cin) { return conv_big() >= 2 && Cout % 256 
 // ``bnb`` (optional, stat_mode 1): {smask, sz, smean, srstd, szd, smean_d, srstd_d, mscale, mshift} of the
 // BatchNorm whose backward statistics the data-grad epilogue produces ([2 or 3][M tiles][Cout] into ``stats``);
 // mscale / mshift (both or neither) re-derive the ReLU mask from sz instead of reading smask.
-// Register-staged launch for a forward conv with the A-operand BN+ReLU fold (fold_scale/shift): the tile family
-// the picker gives a dilated input (no LDS-DMA, no 256-row tiles, no multi-tile workgroups).
-namespace {
-int launch_fwd_fold(const FwdArgs& a, hipStream_t stream) {
-  int bm, bn;
-  pick_fwd_tile((long)a.B * a.Lout, a.Cout, 2, &bm, &bn);
-  const bool nb2 = conv_nbuf() == 2;
-#define ECG_FOLD(BM_, BN_)                                                                                     \
-  return a.stat_mode == 1 ? (nb2 ? launch_fwd_cfg<BM_, BN_, 1, 2>(a, stream) : launch_fwd_cfg<BM_, BN_, 1, 1>(a, stream)) \
-                          : (nb2 ? launch_fwd_cfg<BM_, BN_, 0, 2>(a, stream) : launch_fwd_cfg<BM_, BN_, 0, 1>(a, stream))
-  if (bm == 128 && bn == 128) ECG_FOLD(128, 128);
-  if (bm == 128) ECG_FOLD(128, 64);
-  ECG_FOLD(64, 64);
-#undef ECG_FOLD
-}
-}  // namespace
-
-ECG_API int ecg_conv1d_nlc_fwd_ex2(const void* x, const void* w, const float* bias, void* y, float* stats,
-                                   const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
-                                   int Kw, int stride, int pad, int in_dil, int relu, const void* const* bnb,
-                                   const void* tail, const float* fold_scale, const float* fold_shift,
-                                   hipStream_t stream);
-
+// ``tail`` (optional, with ``stats``): a BatchNorm finalize fused into this launch (bn_tail.h).
 ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bias, void* y, float* stats,
                                   const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
                                   int Kw, int stride, int pad, int in_dil, int relu, const void* const* bnb,
                                   const void* tail, hipStream_t stream) {
-  return ecg_conv1d_nlc_fwd_ex2(x, w, bias, y, stats, add, add_mask, B, Lin, Cin, Lout, Cout, Kw, stride, pad,
-                                in_dil, relu, bnb, tail, nullptr, nullptr, stream);
-}
-
-// ecg_conv1d_nlc_fwd_ex plus the A-operand fold: with fold_scale / fold_shift (both or neither; in_dil == 1) the
-// conv reads x = z and stages bf16(max(z * fold_scale[c] + fold_shift[c], 0)) - the BN_ACT output it replaces,
-// bitwise - on the register-staged loop.  Its BatchNorm partial rows: ecg_conv1d_nlc_fwd_stat_tiles_fold.
-ECG_API int ecg_conv1d_nlc_fwd_ex2(const void* x, const void* w, const float* bias, void* y, float* stats,
-                                   const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
-                                   int Kw, int stride, int pad, int in_dil, int relu, const void* const* bnb,
-                                   const void* tail, const float* fold_scale, const float* fold_shift,
-                                   hipStream_t stream) {
-  if (!fold_scale != !fold_shift || (fold_scale && in_dil != 1)) return ecg::kBadArg;
   if (!x || !w || !y || B <= 0 || Lin <= 0 || Lout <= 0 || Kw <= 0 || stride <= 0 || in_dil <= 0 || pad < 0)
     return ecg::kBadArg;
   if (Cin % BK != 0 || Cout % 64 != 0 || (add_mask && !add)) return ecg::kBadArg;
@@ -2169,9 +1923,6 @@ ECG_API int ecg_conv1d_nlc_fwd_ex2(const void* x, const void* w, const float* bi
     a.srstd_d = static_cast<const float*>(bnb[6]);
   }
   a.tail = static_cast<const ecg::BnTail*>(tail);
-  a.ascale = fold_scale;
-  a.ashift = fold_shift;
-  if (fold_scale) return launch_fwd_fold(a, stream);
   if (conv_tap(Cout) && tap_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return launch_fwd_tap(a, stream);
   int bm, bn;
   pick_fwd_tile((long)B * Lout, Cout, in_dil, &bm, &bn);
@@ -2182,7 +1933,6 @@ ECG_API int ecg_conv1d_nlc_fwd_ex2(const void* x, const void* w, const float* bi
   return launch_fwd<64, 64>(a, stream);
 }
 
-// Select the forward tile family (see conv_big); returns the previous setting.
 // Strided data-grads on the LDS-DMA loop (1) or the register-staged loop (0); returns the previous setting (tests).
 ECG_API int ecg_conv1d_nlc_set_dma_dil(int on) {
   const int prev = conv_dma_dil() ? 1 : 0;
@@ -2198,6 +1948,7 @@ ECG_API int ecg_conv1d_nlc_set_tap(int mode) {
   return prev;
 }
 
+// Select the one-tap tile family (see conv_big); returns the previous setting.
 ECG_API int ecg_conv1d_nlc_set_big(int big) {
   const int prev = conv_big();
   g_conv_big = big < 0 ? 0 : (big > 2 ? 2 : big);
@@ -2220,15 +1971,8 @@ ECG_API int ecg_conv1d_nlc_fwd_stat_tiles(long M, int Cout) {
   return gm > 0 ? gm : (int)((M + bm - 1) / bm);
 }
 
-// Partial rows of a forward with the A-operand fold (register-staged tiles, one per M tile).
-ECG_API int ecg_conv1d_nlc_fwd_stat_tiles_fold(long M, int Cout) {
-  int bm, bn;
-  pick_fwd_tile(M, Cout, 2, &bm, &bn);
-  return (int)((M + bm - 1) / bm);
-}
-
 // Rows of BatchNorm partials for the kernel that runs this exact conv (any stride / taps / dilation): the
-// weight-resident kernel's M-tile groups where it applies, else the tile-family rows below.
+// tap-shared kernel's 256-row M tiles where it applies, else the tile-family rows below.
 ECG_API int ecg_conv1d_nlc_fwd_stat_tiles_ex(int B, int Lout, int Cout, int in_dil);
 ECG_API int ecg_conv1d_nlc_fwd_stat_rows(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad,
                                          int in_dil) {
@@ -2267,12 +2011,11 @@ ECG_API int ecg_conv1d_nlc_wgrad(const void* dy, const void* x, float* part, int
   const bool bm128 = Cout % 128 == 0, bn128 = Cin % 128 == 0;
   // LDS-DMA loops: 32-bit buffer offsets from the split's first row / sample
   const long rows = (long)cps * 64;
-  const bool dma_ok = wgrad_dma() && rows * Cout * 2 < 0x7fff0000L &&
+  const bool dma_ok = rows * Cout * 2 < 0x7fff0000L &&
                       (rows / Lout + 2) * (long)Lin * Cin * 2 < 0x7fff0000L;
   if (wgrad_big(Cout, Cin)) return dma_ok ? launch_wgrad_dma<256, 256>(a, splits, stream)
                                           : launch_wgrad<256, 256>(a, splits, stream);
-  if (bm128 && bn128 && dma_ok) return wgrad_g2() ? launch_wgrad_dma2(a, splits, stream)
-                                                   : launch_wgrad_dma<128, 128>(a, splits, stream);
+  if (bm128 && bn128 && dma_ok) return launch_wgrad_dma2(a, splits, stream);
   if (bm128 && bn128) return launch_wgrad<128, 128>(a, splits, stream);
   if (bm128) return launch_wgrad<128, 64>(a, splits, stream);
   if (bn128) return launch_wgrad<64, 128>(a, splits, stream);
@@ -2286,29 +2029,25 @@ ECG_API int ecg_conv1d_nlc_wgrad_tiles(int Cout, int Kw, int Cin) {
   return (Cout / bm) * (Kw * Cin / bn);
 }
 
-// Split count for the tap-shared weight-gradient kernel (64 x 64 x 3 output blocks, ~ECG_WGRAD_TS_WGS workgroups,
-// >= 4 row chunks each), or 0 when this conv takes the one-tap kernels (the caller then sizes its own splits).
+// Split count for the tap-shared weight-gradient kernel (64 x 64 x 3 output blocks, ~WGRAD_TS_WGS workgroups, >= 4
+// row chunks each, at most 256 partial slices - the bound the reduce kernels and the engine's workspace assume), or
+// 0 when this conv takes the one-tap kernels (the caller then sizes its own splits).
 ECG_API int ecg_conv1d_nlc_wgrad_splits(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad) {
   if (!wgrad_ts_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad)) return 0;
   const long chunks = ((long)B * Lout + 63) / 64;
   const int tiles = (Cout / 64) * (Cin / 64);
-  long s = (wgrad_ts_target() + tiles - 1) / tiles;
+  long s = (WGRAD_TS_WGS + tiles - 1) / tiles;
   s = s < chunks / 4 ? s : chunks / 4;
-  return (int)(s < 1 ? 1 : (s > 1024 ? 1024 : s));
+  return (int)(s < 1 ? 1 : (s > 256 ? 256 : s));
 }
 
 // Workgroups the weight-gradient launch should aim for (tiles x splits): ~4 resident per CU for the 4-wave
-// tiles, ~2 rounds of one per CU for the 8-wave 256x256 tile.
+// register-staged tiles, ~2 rounds of one per CU for the 8-wave 256x256 tile.
 ECG_API int ecg_conv1d_nlc_wgrad_target_wgs(int Cout, int Kw, int Cin) {
   (void)Kw;
   if (wgrad_big(Cout, Cin)) return 512;
-  if (Cout % 128 == 0 && Cin % 128 == 0 && wgrad_g2()) {  // 8-wave workgroups, one per CU
-    static int t = -1;
-    if (t < 0) {
-      const char* e = getenv("ECG_WGRAD_TARGET");
-      t = e ? atoi(e) : 256;
-    }
-    return t;
-  }
+  // 128x128 tiles: the two-group 8-wave kernel, one workgroup per CU (B=1024 ResNet1D-34: 3.43 ms/step at 256
+  // workgroups vs 3.51 at 512 and 3.81 at 768; profiles/r4/wgrad_g2_ab.txt)
+  if (Cout % 128 == 0 && Cin % 128 == 0) return 256;
   return 1024;
 }

@@ -36,11 +36,6 @@ extern "C" int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* 
                                      const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout,
                                      int Cout, int Kw, int stride, int pad, int in_dil, int relu,
                                      const void* const* bnb, const void* tail, hipStream_t stream);
-extern "C" int ecg_conv1d_nlc_fwd_ex2(const void* x, const void* w, const float* bias, void* y, float* stats,
-                                      const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout,
-                                      int Cout, int Kw, int stride, int pad, int in_dil, int relu,
-                                      const void* const* bnb, const void* tail, const float* fold_scale,
-                                      const float* fold_shift, hipStream_t stream);
 extern "C" int ecg_conv1d_nlc_wgrad(const void* dy, const void* x, float* part, int splits, int B, int Lin, int Cin,
                                     int Lout, int Cout, int Kw, int stride, int pad, hipStream_t stream);
 extern "C" int ecg_sgd_flat(float* params, const float* grads, float* mom, long n, float lr, float momentum,
@@ -348,7 +343,6 @@ struct FinArgs {
   const float* sB;  // [T][C] partials of stat B (fwd: sum x^2; bwd: sum dz*xhat)
   int T, C, mode;   // mode 0 = forward statistics, 1 = backward coefficients
   double* scratch;  // [gridDim.y][2][C]
-  unsigned* ticket; // [gridDim.x], zero between launches (the last block resets it)
   float n, eps, momentum;
   const float* gamma;
   const float* beta;
@@ -388,88 +382,7 @@ __device__ __forceinline__ void bn_fin_outputs(const FinArgs& a, int c, double v
   }
 }
 
-__global__ __launch_bounds__(TPB) void bn_finalize_kernel(FinArgs a) {
-  __shared__ double red[4][2][64];
-  __shared__ unsigned last;
-  const int tid = threadIdx.x, cl = tid & 63, g4 = tid >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  const int G = gridDim.y;
-  const int t0 = (int)((long)a.T * blockIdx.y / G), t1 = (int)((long)a.T * (blockIdx.y + 1) / G);
-  double s1 = 0.0, s2 = 0.0;
-  for (int t = t0 + g4; t < t1; t += 4) {
-    s1 += (double)a.sA[(long)t * a.C + c];
-    s2 += (double)a.sB[(long)t * a.C + c];
-  }
-  red[g4][0][cl] = s1;
-  red[g4][1][cl] = s2;
-  __syncthreads();
-  if (tid < 64) {
-    const double v1 = red[0][0][cl] + red[1][0][cl] + red[2][0][cl] + red[3][0][cl];
-    const double v2 = red[0][1][cl] + red[1][1][cl] + red[2][1][cl] + red[3][1][cl];
-    a.scratch[((long)blockIdx.y * 2 + 0) * a.C + c] = v1;
-    a.scratch[((long)blockIdx.y * 2 + 1) * a.C + c] = v2;
-  }
-  __threadfence();
-  __syncthreads();
-  if (tid == 0) last = atomicAdd(&a.ticket[blockIdx.x], 1u) == (unsigned)(G - 1);
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  {  // last block: all 256 threads sum the G level-2 partials (device-coherent loads, 4 in flight per thread)
-    double v1 = 0.0, v2 = 0.0;
-    int g = g4;
-    for (; g + 12 < G; g += 16) {
-      double t1[4], t2[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        t1[u] = __hip_atomic_load(&a.scratch[((long)(g + 4 * u) * 2 + 0) * a.C + c], __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-        t2[u] = __hip_atomic_load(&a.scratch[((long)(g + 4 * u) * 2 + 1) * a.C + c], __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        v1 += t1[u];
-        v2 += t2[u];
-      }
-    }
-    for (; g < G; g += 4) {
-      v1 += __hip_atomic_load(&a.scratch[((long)g * 2 + 0) * a.C + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      v2 += __hip_atomic_load(&a.scratch[((long)g * 2 + 1) * a.C + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    red[g4][0][cl] = v1;
-    red[g4][1][cl] = v2;
-  }
-  __syncthreads();
-  if (tid < 64) {
-    const double v1 = red[0][0][cl] + red[1][0][cl] + red[2][0][cl] + red[3][0][cl];
-    const double v2 = red[0][1][cl] + red[1][1][cl] + red[2][1][cl] + red[3][1][cl];
-    const double n = (double)a.n;
-    if (a.mode == 0) {
-      const double mu = v1 / n;
-      const double var = fmax(v2 / n - mu * mu, 0.0);
-      const float rs = (float)(1.0 / sqrt(var + (double)a.eps));
-      const float sc = a.gamma[c] * rs;
-      a.mean[c] = (float)mu;
-      a.rstd[c] = rs;
-      a.scale[c] = sc;
-      a.shift[c] = a.beta[c] - (float)mu * sc;
-      if (a.run_mean) {
-        const float m = a.momentum;
-        a.run_mean[c] = (1.f - m) * a.run_mean[c] + m * (float)mu;
-        a.run_var[c] = (1.f - m) * a.run_var[c] + m * (float)(var * n / fmax(n - 1.0, 1.0));
-      }
-    } else {
-      if (a.dbeta) a.dbeta[c] = (float)v1;
-      if (a.dgamma) a.dgamma[c] = (float)v2;
-      a.c1[c] = (float)(v1 / n);
-      a.c2[c] = (float)(v2 / n);
-    }
-  }
-  if (tid == 0) a.ticket[blockIdx.x] = 0u;
-}
-
-// Two-launch form (default): phase 1 writes the G level-2 partials with plain stores, the kernel boundary makes
+// Two launches: phase 1 writes the G level-2 partials with plain stores, the kernel boundary makes
 // them visible, phase 2 (one block per 64 channels) reduces them - no fences on the critical path.
 __global__ __launch_bounds__(TPB) void bn_partial_kernel(FinArgs a) {
   __shared__ double red[4][2][64];
@@ -665,68 +578,6 @@ __global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(
   }
 }
 
-// The same apply with RPT rows per thread at a FIXED channel group (c0 = thread % (C/8)): the five per-channel
-// vectors are loaded once per thread instead of once per 8 elements, and every row's loads are issued before
-// the first store.  Element math identical to bn_bwd_apply_kernel (bitwise the same output).
-template <bool DS, int RPT>
-__global__ __launch_bounds__(TPB) void bn_bwd_apply_rows_kernel(
-    const __bf16* __restrict__ gy, const __bf16* __restrict__ msk, const __bf16* __restrict__ z,
-    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ scale,
-    const float* __restrict__ c1, const float* __restrict__ c2, __bf16* __restrict__ out,
-    const __bf16* __restrict__ zd, const float* __restrict__ mean_d, const float* __restrict__ rstd_d,
-    const float* __restrict__ scale_d, const float* __restrict__ c2_d, __bf16* __restrict__ out_d, long R, int C) {
-  const int cg = C / 8;  // divides TPB (host-checked), so a thread's channel group never changes
-  const long gt = (long)blockIdx.x * TPB + threadIdx.x;
-  const int c0 = (int)(gt % cg) * 8;
-  const long lanes = (long)gridDim.x * TPB / cg;  // row lanes
-  float mu[8], rs[8], sc[8], k1[8], k2[8], mud[8], rsd[8], scd[8], k2d[8];
-  ldf8(mean + c0, mu);
-  ldf8(rstd + c0, rs);
-  ldf8(scale + c0, sc);
-  ldf8(c1 + c0, k1);
-  ldf8(c2 + c0, k2);
-  if (DS) {
-    ldf8(mean_d + c0, mud);
-    ldf8(rstd_d + c0, rsd);
-    ldf8(scale_d + c0, scd);
-    ldf8(c2_d + c0, k2d);
-  }
-  for (long r0 = gt / cg; r0 < R; r0 += lanes * RPT) {
-    float g[RPT][8], zf[RPT][8], zdf[RPT][8];
-#pragma unroll
-    for (int u = 0; u < RPT; ++u) {
-      const long r = r0 + u * lanes;
-      if (r < R) {
-        const long o = r * C + c0;
-        ld8(gy + o, g[u]);
-        if (msk) {
-          float m[8];
-          ld8(msk + o, m);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) g[u][i] = m[i] > 0.f ? g[u][i] : 0.f;
-        }
-        ld8(z + o, zf[u]);
-        if (DS) ld8(zd + o, zdf[u]);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < RPT; ++u) {
-      const long r = r0 + u * lanes;
-      if (r < R) {
-        const long o = r * C + c0;
-        float y[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) y[i] = sc[i] * (g[u][i] - k1[i] - (zf[u][i] - mu[i]) * rs[i] * k2[i]);
-        st8(out + o, y);
-        if (DS) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) y[i] = scd[i] * (g[u][i] - k1[i] - (zdf[u][i] - mud[i]) * rsd[i] * k2d[i]);
-          st8(out_d + o, y);
-        }
-      }
-    }
-  }
-}
 
 // ------------------------------------------------------------------------------------------------ head
 // One block per sample: feat = mean_t h[b,t,:]; logits = W feat + bias; CE loss; g = (softmax - onehot)/B;
@@ -869,7 +720,7 @@ __global__ __launch_bounds__(TPB) void reduce_wgrad_kernel(const float* __restri
   const int tid = threadIdx.x, col = tid & 63, sg = tid >> 6;
   const float4* p4 = reinterpret_cast<const float4*>(part);
   const long N4 = N / 4;
-  // grid-stride over 64-column groups (a capped grid keeps the side lane to fewer, longer blocks)
+  // grid-stride over 64-column groups
   for (long blk = blockIdx.x; blk * 64 < N4; blk += gridDim.x) {
   const long i4 = blk * 64 + col;  // float4 index
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1080,45 +931,11 @@ inline float F(int64_t v) {
   return (float)d;
 }
 
-// ECG_REDUCE_WIDE=1 selects the 16-split-group weight-gradient reduce (read once; default 0: the 4-group one).
-// The wide one is as fast or faster alone (scripts/wgrad_micro.py) but launches 4x the blocks, and on the side lane
-// of the ResNet1D-34 step that costs 0.12 ms/step (3.87 vs 3.75, profiles/r3/resnet_knob_matrix.txt): side-lane
-// kernels must not crowd the data-gradient chain's CUs.
-// ECG_REDUCE_WIDE=2: the wide reduce only where the split count is large (S >= ECG_REDUCE_WIDE_MIN, default 128:
-// the tap-shared stride-1 layer-1 gradients, 256 splits of a 48 KB |dW|, whose 4-group reduce is a 16-deep
-// dependent load chain).
-inline bool reduce_wide(int S) {
-  static int v = -1, smin = 128;
-  if (v < 0) {
-    const char* e = getenv("ECG_REDUCE_WIDE");
-    v = e ? atoi(e) : 0;
-    const char* m = getenv("ECG_REDUCE_WIDE_MIN");
-    if (m && atoi(m) > 0) smin = atoi(m);
-  }
-  return v == 1 || (v == 2 && S >= smin);
-}
-
-// ECG_REDUCE_GRID=<n>: cap the 4-group reduce's grid at n blocks (grid-stride); 0 (default) = one block per
-// 64 float4 columns.
-inline long reduce_grid_cap() {
-  static long v = -1;
-  if (v < 0) {
-    const char* e = getenv("ECG_REDUCE_GRID");
-    v = e ? atol(e) : 0;
-  }
-  return v;
-}
-
-// ECG_BN_FIN=ticket selects the single-launch ticketed finalize (fence + last-block reduction); default: two
-// launches.  Read once.
-inline int fin_mode() {
-  static int m = -1;
-  if (m < 0) {
-    const char* e = getenv("ECG_BN_FIN");
-    m = (e && strcmp(e, "ticket") == 0) ? 1 : 0;
-  }
-  return m;
-}
+// The 16-split-group weight-gradient reduce for the many-split partials (S >= 128: the tap-shared 64-channel
+// gradients, 256 splits of a 48 KB |dW|, whose 4-group reduce is a 16-deep dependent load chain), else the 4-group
+// one: on the side lane the wide reduce's 4x blocks crowd the data-gradient chain's CUs (3.87 vs 3.75 ms/step when
+// used for every conv, profiles/r3/resnet_knob_matrix.txt; -0.2 % for S >= 128 only, profiles/r3/resnet_reduce_ab.txt).
+inline bool reduce_wide(int S) { return S >= 128; }
 
 int run_op(const int64_t* o, hipStream_t st) {
   const int kind = (int)o[0];
@@ -1128,11 +945,10 @@ int run_op(const int64_t* o, hipStream_t st) {
                          // words 26, 27: scale / shift that re-derive the ReLU mask from sz (or 0: load smask)
       const void* bnb[9] = {P<void>(o[18]), P<void>(o[19]), P<void>(o[20]), P<void>(o[21]), P<void>(o[22]),
                             P<void>(o[23]), P<void>(o[24]), P<void>(o[26]), P<void>(o[27])};
-      // words 28, 29: BN scale / shift folded into the A-operand load (x = the pre-BN activation) or 0
-      return ecg_conv1d_nlc_fwd_ex2(P<void>(o[1]), P<void>(o[2]), P<float>(o[3]), P<void>(o[4]), P<float>(o[5]),
-                                    P<void>(o[6]), P<void>(o[7]), (int)o[8], (int)o[9], (int)o[10], (int)o[11],
-                                    (int)o[12], (int)o[13], (int)o[14], (int)o[15], (int)o[16], (int)o[17],
-                                    o[19] ? bnb : nullptr, P<void>(o[25]), P<float>(o[28]), P<float>(o[29]), st);
+      return ecg_conv1d_nlc_fwd_ex(P<void>(o[1]), P<void>(o[2]), P<float>(o[3]), P<void>(o[4]), P<float>(o[5]),
+                                   P<void>(o[6]), P<void>(o[7]), (int)o[8], (int)o[9], (int)o[10], (int)o[11],
+                                   (int)o[12], (int)o[13], (int)o[14], (int)o[15], (int)o[16], (int)o[17],
+                                   o[19] ? bnb : nullptr, P<void>(o[25]), st);
     }
     case OP_CONV_WGRAD:
       return ecg_conv1d_nlc_wgrad(P<void>(o[1]), P<void>(o[2]), P<float>(o[3]), (int)o[4], (int)o[5], (int)o[6],
@@ -1144,9 +960,7 @@ int run_op(const int64_t* o, hipStream_t st) {
         hipLaunchKernelGGL(reduce_wgrad_wide_kernel, dim3((unsigned)(N / 64)), dim3(TPB), 0, st, P<const float>(o[1]),
                            (int)o[2], (int)o[3], (int)o[4], (int)o[5], P<float>(o[6]));
       } else {
-        const long cap = reduce_grid_cap();
-        const long nb = (cap > 0 && N / 256 > cap) ? cap : N / 256;
-        hipLaunchKernelGGL(reduce_wgrad_kernel, dim3((unsigned)nb), dim3(TPB), 0, st, P<const float>(o[1]),
+        hipLaunchKernelGGL(reduce_wgrad_kernel, dim3((unsigned)(N / 256)), dim3(TPB), 0, st, P<const float>(o[1]),
                            (int)o[2], (int)o[3], (int)o[4], (int)o[5], P<float>(o[6]));
       }
       break;
@@ -1159,7 +973,6 @@ int run_op(const int64_t* o, hipStream_t st) {
       a.C = (int)o[4];
       a.mode = (int)o[5];
       a.scratch = P<double>(o[6]);
-      a.ticket = P<unsigned>(o[7]);
       a.n = F(o[8]);
       a.eps = F(o[9]);
       a.momentum = F(o[10]);
@@ -1177,12 +990,8 @@ int run_op(const int64_t* o, hipStream_t st) {
       a.c2 = P<float>(o[22]);
       const int G = (int)o[23];
       if (a.C % 64 || G < 1 || G > 1024) return ecg::kBadArg;
-      if (fin_mode() == 1) {
-        hipLaunchKernelGGL(bn_finalize_kernel, dim3(a.C / 64, G), dim3(TPB), 0, st, a);
-      } else {
-        hipLaunchKernelGGL(bn_partial_kernel, dim3(a.C / 64, G), dim3(TPB), 0, st, a);
-        hipLaunchKernelGGL(bn_final_kernel, dim3(a.C / 64), dim3(TPB), 0, st, a, G);
-      }
+      hipLaunchKernelGGL(bn_partial_kernel, dim3(a.C / 64, G), dim3(TPB), 0, st, a);
+      hipLaunchKernelGGL(bn_final_kernel, dim3(a.C / 64), dim3(TPB), 0, st, a, G);
       break;
     }
     case OP_BN_ACT: {
@@ -1224,26 +1033,6 @@ int run_op(const int64_t* o, hipStream_t st) {
       const bool ds = o[1] != 0;
       const long R = o[17];
       const int C = (int)o[18];
-      // word 19: rows per thread of the fixed-channel variant (ops/resnet_engine.py, ECG_BN_APPLY_RPT; 0 = one
-      // vector per thread, the original kernel)
-      const int rpt = (int)o[19];
-      if (rpt > 0 && C % 8 == 0 && TPB % (C / 8) == 0) {
-        const long lanes_needed = (R + rpt - 1) / rpt;  // row lanes so that each thread gets ~rpt rows
-        const dim3 gr((unsigned)std::max(1L, std::min(8192L, (lanes_needed * (C / 8) + TPB - 1) / TPB)));
-#define ECG_APPLY_ROWS(DSV, RP)                                                                                      \
-  hipLaunchKernelGGL((bn_bwd_apply_rows_kernel<DSV, RP>), gr, dim3(TPB), 0, st, P<const __bf16>(o[2]),               \
-                     P<const __bf16>(o[3]), P<const __bf16>(o[4]), P<const float>(o[5]), P<const float>(o[6]),       \
-                     P<const float>(o[7]), P<const float>(o[8]), P<const float>(o[9]), P<__bf16>(o[10]),            \
-                     P<const __bf16>(o[11]), P<const float>(o[12]), P<const float>(o[13]), P<const float>(o[14]),    \
-                     P<const float>(o[15]), P<__bf16>(o[16]), R, C)
-        if (ds) {
-          if (rpt >= 4) ECG_APPLY_ROWS(true, 4); else if (rpt >= 2) ECG_APPLY_ROWS(true, 2); else ECG_APPLY_ROWS(true, 1);
-        } else {
-          if (rpt >= 4) ECG_APPLY_ROWS(false, 4); else if (rpt >= 2) ECG_APPLY_ROWS(false, 2); else ECG_APPLY_ROWS(false, 1);
-        }
-#undef ECG_APPLY_ROWS
-        break;
-      }
       const dim3 g(grid_for(R * C / 8));
       if (!ds)
         hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]),
@@ -1381,14 +1170,12 @@ int side_lane(SideLane** out) {
   if (dev < 0 || dev >= 64) return ecg::kBadArg;
   SideLane& l = lanes[dev];
   if (!l.side) {
-    // lowest priority: the data-gradient chain is the critical path.  (A CU-masked side queue,
-    // hipExtStreamCreateWithCUMask with 2/4/6 of every 8 CUs, measured 7.5-7.8 ms/step against 3.93 on
-    // ResNet1D-34 B=1024; ECG_RESNET_SIDE_PRIO=hi|normal are A/B knobs for the priority.)
+    // lowest priority: the data-gradient chain is the critical path (profiles/r2/resnet_side_prio_ab.txt; a
+    // CU-masked side queue, hipExtStreamCreateWithCUMask with 2/4/6 of every 8 CUs, measured 7.5-7.8 ms/step
+    // against 3.93 on ResNet1D-34 B=1024)
     int lo = 0, hi = 0;
     ECG_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    const char* e = getenv("ECG_RESNET_SIDE_PRIO");
-    const int prio = !e ? lo : (strcmp(e, "hi") == 0 ? hi : (strcmp(e, "normal") == 0 ? 0 : lo));
-    ECG_HIP_CHECK(hipStreamCreateWithPriority(&l.side, hipStreamNonBlocking, prio));
+    ECG_HIP_CHECK(hipStreamCreateWithPriority(&l.side, hipStreamNonBlocking, lo));
     ECG_HIP_CHECK(hipEventCreateWithFlags(&l.fork, hipEventDisableTiming));
     ECG_HIP_CHECK(hipEventCreateWithFlags(&l.join, hipEventDisableTiming));
   }

@@ -1484,19 +1484,6 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_round_kernel(RoundArgs a)
 
 unsigned long long* g_stamps = nullptr;  // diagnostic phase stamps (ecg_tiny_set_stamps)
 
-// Diagnostic ablation (timing only, results are wrong): ECG_TINY_ABLATE=reduce|step|both replaces the slab
-// reduction and/or the step kernel by an empty kernel of the same grid and LDS (scripts/diag_ablate.py).
-__global__ void ablate_kernel(float* out) {
-  if (threadIdx.x == 0 && blockIdx.x == 0 && out) out[0] = 0.f;
-}
-inline int ablate_mode() {
-  static int m = -1;
-  if (m < 0) {
-    const char* e = getenv("ECG_TINY_ABLATE");
-    m = !e ? 0 : (strcmp(e, "reduce") == 0 ? 1 : strcmp(e, "step") == 0 ? 2 : strcmp(e, "both") == 0 ? 3 : 0);
-  }
-  return m;
-}
 
 template <int WAVES, int MODE, bool F32, bool PF>
 int launch_step(const float* X, int L, long ldx, const int* idx, const int* Y, const float* params, int nc,
@@ -1506,11 +1493,6 @@ int launch_step(const float* X, int L, long ldx, const int* idx, const int* Y, c
   auto kern = tiny_ecg_step_kernel<WAVES, MODE, F32, PF>;
   if (sm.bytes > 64 * 1024)
     ECG_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, sm.bytes));
-  if (MODE == 0 && (ablate_mode() & 2)) {
-    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)ablate_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, sm.bytes));
-    hipLaunchKernelGGL(ablate_kernel, dim3(B), dim3(WAVES * 64), sm.bytes, stream, nullptr);
-    return ecg::kOk;
-  }
   hipLaunchKernelGGL(kern, dim3(B), dim3(WAVES * 64), sm.bytes, stream, X, L, ldx, idx, Y, params, nc, out,
                      out_stride, inv_B, g_stamps, opt, wprep);
   ECG_HIP_CHECK(hipGetLastError());
@@ -1531,17 +1513,13 @@ int launch_prep(const float* params, unsigned char* wprep, const int* idx_src, i
 constexpr int kMaxLds = 160 * 1024;
 
 // 16 waves (one tile pair each at L=500) when the per-wave partial slots fit in LDS, else 8.
-// ECG_TINY_WAVES=8|16 overrides (tuning); the choice never changes results beyond fp32 summation order.
+// ecg_tiny_force_waves overrides it (tests); the choice never changes results beyond fp32 summation order.
 // Both precisions take 16 waves once there are >= 16 time tiles: bf16 12.57 vs 12.73 us/step at L=500 with the
 // MFMA conv1 (profiles/r1_round_kernel/ab_waves.log; 8 waves had been faster before conv1 moved to MFMA), fp32
 // has 4x more MFMA instructions per tile on v_mfma_f32_16x16x4_f32.
-int g_forced_waves = -1;  // ECG_TINY_WAVES, or ecg_tiny_force_waves (tests)
+int g_forced_waves = 0;  // ecg_tiny_force_waves (tests)
 int pick_waves(int L, bool f32) {
   const int Lp = (L + 31) / 32 * 32;
-  if (g_forced_waves < 0) {
-    const char* e = getenv("ECG_TINY_WAVES");
-    g_forced_waves = e ? atoi(e) : 0;
-  }
   const int forced = g_forced_waves;
   const bool fit16 = Lp <= 32 * 4 * 16 && make_smem(L, 16, MAX_CLASSES, f32).bytes <= kMaxLds;
   if (forced == 16 && fit16) return 16;
@@ -1600,14 +1578,10 @@ int step_dispatch(int mode, int prec, const float* X, int L, long ldx, const int
 
 FusedOpt no_fuse() {
   FusedOpt o{};
-  // Write-through gradient rows (default): the rows leave the XCD L2s while the step runs instead of in the
-  // boundary's write-back, and the reduce kernel finds them beyond L2: 11.1 vs 11.4 us/step (bench, A/B x2,
-  // profiles/r2/bench_slab_wt.txt).  ECG_TINY_SLAB_WT=0 restores plain stores.
-  static const int wt = [] {
-    const char* e = getenv("ECG_TINY_SLAB_WT");
-    return e && atoi(e) == 0 ? 0 : 1;
-  }();
-  o.slab_wt = wt;
+  // Write-through gradient rows: the rows leave the XCD L2s while the step runs instead of in the boundary's
+  // write-back, and the reduce kernel finds them beyond L2: 11.1 vs 11.4 us/step with plain stores (bench, A/B x2,
+  // profiles/r2/bench_slab_wt.txt).
+  o.slab_wt = 1;
   return o;
 }
 
@@ -1616,16 +1590,8 @@ int reduce_dispatch(const float* slab, int G, int stride, int P, float* params, 
                     unsigned char* wprep, hipStream_t stream, const GatherArgs* gather = nullptr) {
   if (G <= 0 || P <= 0 || stride < P + 1) return ecg::kBadArg;
   if (apply && (!params || (momentum != 0.f && !mom))) return ecg::kBadArg;
-  static const int cols = [] {  // ECG_RED_COLS in {4, 8, 16, 32, 64}: columns per reduction block (A/B knob)
-    const char* e = getenv("ECG_RED_COLS");
-    const int v = e ? atoi(e) : kRedColsDefault;
-    return (v == 4 || v == 8 || v == 16 || v == 32 || v == 64) ? v : kRedColsDefault;
-  }();
+  constexpr int cols = kRedColsDefault;  // columns per reduction block (A/B: profiles/r1_final/ab_red_cols.txt)
   const int blocks = (P + 1 + cols - 1) / cols;
-  if (ablate_mode() & 1) {
-    hipLaunchKernelGGL(ablate_kernel, dim3(blocks), dim3(cols * RED_ROWG), 0, stream, nullptr);
-    return ecg::kOk;
-  }
   GatherArgs ga{};
   ga.nred = INT_MAX;
   int grid = blocks;
@@ -1635,20 +1601,8 @@ int reduce_dispatch(const float* slab, int G, int stride, int P, float* params, 
     const int rpb = gather_rows_per_block(ga.L, ga.vec, cols * RED_ROWG);
     grid += (ga.B + rpb - 1) / rpb;
   }
-#define ECG_RED_LAUNCH(NC)                                                                                       \
-  hipLaunchKernelGGL(slab_reduce_sgd_kernel<NC>, dim3(grid), dim3(NC * RED_ROWG), 0, stream, slab, G, stride, P, \
-                     params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply, wprep, ga)
-  if (cols == 4)
-    ECG_RED_LAUNCH(4);
-  else if (cols == 8)
-    ECG_RED_LAUNCH(8);
-  else if (cols == 64)
-    ECG_RED_LAUNCH(64);
-  else if (cols == 32)
-    ECG_RED_LAUNCH(32);
-  else
-    ECG_RED_LAUNCH(16);
-#undef ECG_RED_LAUNCH
+  hipLaunchKernelGGL(slab_reduce_sgd_kernel<cols>, dim3(grid), dim3(cols * RED_ROWG), 0, stream, slab, G, stride, P,
+                     params, mom, grad_out, loss_acc, lr, momentum, wd, nesterov, apply, wprep, ga);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
@@ -1843,13 +1797,10 @@ static int train_step(const float* X, int L, long ldx, const int* idx, const int
   if (wprep && image == 0) st = launch_prep(params, wprep, nullptr, nullptr, 0, stream);
   if (st) return st;
   FusedOpt o = no_fuse();
-  // ECG_TINY_PREFETCH=1: warm-up loads of the next step's windows in the step kernel's tail (opt-in: 11.11 vs
-  // 11.08 us/step without, A/B x2 - the windows already sit in the Infinity Cache; profiles/r2/bench_prefetch.txt)
-  static const bool warm_next = [] {
-    const char* e = getenv("ECG_TINY_PREFETCH");
-    return e && atoi(e) == 1;
-  }();
-  o.idx_next = warm_next ? idx_next : nullptr;
+  // (Warm-up loads of the next step's windows in the step kernel's tail measured neutral - 11.11 vs 11.08 us/step,
+  // the windows already sit in the Infinity Cache; profiles/r2/bench_prefetch.txt - and were removed.)
+  (void)idx_next;
+  o.idx_next = nullptr;
   st = step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, o,
                      image == 2 ? nullptr : wprep, stream);
   if (st) return st;

@@ -46,15 +46,6 @@ for s in "$@"; do
       step convtest 600 python -u -m pytest tests/test_conv_mc_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     enginetest)
       step enginetest 900 python -u -m pytest tests/test_resnet_engine_gpu.py tests/test_resnet_trainer_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
-    wgab)
-      for g in 0 1; do ECG_WGRAD_G2=$g step probe_wg$g 300 python scripts/r4_conv_probe.py 30 1024; done
-      ECG_WGRAD_TARGET=256 step probe_wg1_t256 300 python scripts/r4_conv_probe.py 30 1024
-      for r in 1 2; do
-        ECG_WGRAD_G2=0 step resnet_wg0_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
-        ECG_WGRAD_G2=1 step resnet_wg1_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
-        ECG_WGRAD_TARGET=256 step resnet_wg1t256_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
-        ECG_WGRAD_TARGET=768 step resnet_wg1t768_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
-      done ;;
     tapab)
       for m in 0 2; do ECG_CONV_TAP=$m step probe_tap$m 300 python scripts/r4_conv_probe.py 30 1024; done
       for r in 1 2; do for m in 0 1 2; do

@@ -318,31 +318,9 @@ def test_prefrag_round_graph_bitwise_equal_lds_eager_with_external_updates(graph
     b.close()
 
 
-def test_split_round_graphs_bitwise_equal_one_graph():
-    """A PF round launched as a short head graph + the tail graph (ECG_TINY_HEAD) == the one-graph round, bit for
-    bit, over full and partial rounds (rounds not longer than the head take the one-graph path)."""
-    from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
-    plan = [7, 1, 2, 3, 7]
-    outs = []
-    for head in (2, 0):
-        dev, x, y, model, _ = _setup(B=128, N=1024)
-        tr = FusedTinyTrainer(model, x, y, 128, 7, seed=13, persistent=False, prefrag=True)
-        tr.head = head
-        tr.prepare(sorted(set(plan)))
-        for i, n in enumerate(plan):
-            tr.run_round(n, reset_loss=False, next_n=plan[i + 1] if i + 1 < len(plan) else None)
-        torch.cuda.synchronize()
-        outs.append((tr.params.clone(), tr.mom.clone(), tr.avg_loss()))
-        if head:
-            assert any(isinstance(k, tuple) and k[0] == "part" for k in tr._graphs)
-        tr.close()
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-    assert outs[0][2] == outs[1][2]
-
-
 @pytest.mark.parametrize("L,B", [(500, 128), (250, 96)])  # 16-byte rows / scalar rows (L % 4 != 0)
 def test_gather_round_graph_bitwise_equal_plain(L, B):
-    """PF round graphs whose reduce launches gather the next step's windows and labels (ECG_TINY_GATHER) == the
+    """PF round graphs whose reduce launches gather the next step's windows and labels (``gather``) == the
     plain PF graph and the eager C++ step loop, bit for bit, over full and partial rounds (1-step rounds gather
     nothing; odd and even step counts end on either ping-pong buffer)."""
     from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
