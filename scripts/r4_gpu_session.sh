@@ -42,6 +42,8 @@ for s in "$@"; do
       for i in 1 2 3; do step resnet_$i 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras; done ;;
     probe)
       step probe 300 python scripts/r4_conv_probe.py 30 1024,4096 ;;
+    bnprobe)
+      step bnprobe 300 python scripts/r4_bn_probe.py 50 ;;
     convtest)
       step convtest 600 python -u -m pytest tests/test_conv_mc_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     enginetest)
@@ -63,6 +65,12 @@ for s in "$@"; do
       export TMPDIR=/tmp
       step prof_tiny 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_tiny" -o tiny -- \
         python3 bench.py --steps 200 --warmup 50 --no-extras
+      step prof_resnet 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_resnet" -o resnet -- \
+        python3 bench.py --model resnet1d34 --steps 10 --warmup 3 --no-extras ;;
+    timeline)
+      export TMPDIR=/tmp
+      step timeline 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/timeline" -o tl -- \
+        python3 scripts/resnet_timeline.py run
       step prof_resnet 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_resnet" -o resnet -- \
         python3 bench.py --model resnet1d34 --steps 10 --warmup 3 --no-extras ;;
     tinypmc)

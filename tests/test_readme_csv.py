@@ -37,3 +37,34 @@ def test_render_marks_bar_and_spread(tmp_path):
     assert "+20 % (B=64)" in row and "+5 % (B=128)" in row and "bar at B=64." in row
     assert "Medians of 5 interleaved repetitions" in row and "B=64 90–110 / 90–110 / 108–132" in row
     assert "**4.00–4.50×**" in readme.module2_row(str(d))
+
+
+def test_readme_headline_matches_bench_runs():
+    """The headline rows are rendered from every recorded bench line (profiles/rN/bench_runs.jsonl)."""
+    ok, expected, found = readme.check_headline(os.path.join(ROOT, "README.md"), root=ROOT)
+    assert ok, "README headline is stale; run `python -m crossscale_ecg.report.readme --write`\n" + expected
+    assert f"<!-- runs: {readme.latest_runs_file(ROOT)} -->" in found
+
+
+def test_render_headline_median_over_boxes(tmp_path):
+    """Builder rows: median and range over all runs of the newest commit (older commits ignored), box count; the
+    driver column quotes the newest driver record."""
+    import json
+    recs = [
+        {"source": "builder", "session": "s0", "log": "bench20_1.log", "box": "A", "commit": "old", "model": "tiny_ecg",
+         "value": 30e6, "ms_per_step": 0.0085, "gpu_ms_per_step": 0.008, "steps": 20, "warmup": 5, "n_gpus": 1},
+        {"source": "driver", "session": "BENCH_r07.json", "log": "", "box": "x", "commit": "c7", "model": "tiny_ecg",
+         "round": 7, "value": 20e6, "ms_per_step": 0.0128, "gpu_ms_per_step": 0.0118, "steps": 20, "warmup": 5,
+         "n_gpus": 1},
+    ]
+    for i, (v, box) in enumerate(((18e6, "A"), (20e6, "B"), (19e6, "B"))):
+        recs.append({"source": "builder", "session": "s1", "log": f"bench20_{i}.log", "box": box, "commit": "new",
+                     "model": "tiny_ecg", "value": v, "ms_per_step": 256 / v * 1e3, "gpu_ms_per_step": None,
+                     "steps": 20, "warmup": 5, "n_gpus": 1})
+    p = tmp_path / "bench_runs.jsonl"
+    p.write_text("".join(json.dumps(r) + "\n" for r in recs))
+    text = readme.render_headline(str(p))
+    row = [ln for ln in text.splitlines() if "driver's command" in ln][0]
+    assert "round 7: **20.0 M/s**" in row
+    assert "median **19.0 M/s** (18.0 M/s–20.0 M/s) over 3 runs on 2 boxes, commit `new`" in row
+    assert "no run recorded" in [ln for ln in text.splitlines() if "ResNet1D-34" in ln][0]
