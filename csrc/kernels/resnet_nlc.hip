@@ -430,22 +430,27 @@ __global__ __launch_bounds__(TPB) void bn_act_kernel(const __bf16* __restrict__ 
                                                      long R, int C) {
   const int cg = C / 8;
   const long nv = R * cg;
+  int cur = -1;  // the thread's channel group, fixed under bn_pass_grid: coefficients loaded once
+  float sc[8], sh[8], sd[8], hd[8];
   for (long v = (long)blockIdx.x * TPB + threadIdx.x; v < nv; v += (long)gridDim.x * TPB) {
     const int c0 = (int)(v % cg) * 8;
     const long o = v * 8;
-    float zf[8], sc[8], sh[8], y[8];
+    float zf[8], y[8], rf[8];
     ld8(z + o, zf);
-    ldf8(scale + c0, sc);
-    ldf8(shift + c0, sh);
+    if (MODE >= 1) ld8(res + o, rf);
+    if (c0 != cur) {
+      cur = c0;
+      ldf8(scale + c0, sc);
+      ldf8(shift + c0, sh);
+      if (MODE == 2) {
+        ldf8(scale_d + c0, sd);
+        ldf8(shift_d + c0, hd);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) y[i] = fmaf(zf[i], sc[i], sh[i]);  // (the data-grad epilogue's mask re-derives it)
     if (MODE >= 1) {
-      float rf[8];
-      ld8(res + o, rf);
       if (MODE == 2) {
-        float sd[8], hd[8];
-        ldf8(scale_d + c0, sd);
-        ldf8(shift_d + c0, hd);
 #pragma unroll
         for (int i = 0; i < 8; ++i) rf[i] = rf[i] * sd[i] + hd[i];
       }
@@ -532,7 +537,11 @@ __global__ __launch_bounds__(TPB) void bn_bwd_reduce_kernel(
   }
 }
 
-// dzz = scale*(dz - c1 - xhat*c2) with dz = gy*(mask > 0); DS: also dzd = scale_d*(dz - c1 - xhat_d*c2_d)
+// dzz = scale*(dz - c1 - xhat*c2) with dz = gy*(mask > 0); DS: also dzd = scale_d*(dz - c1 - xhat_d*c2_d).
+// Grid-stride with a stride that is a multiple of C/8 (bn_pass_grid), so a thread's channel group is the same in
+// every iteration: its per-channel coefficients are loaded ONCE (the one-vector-per-thread form re-read 5 coefficient
+// vectors - 160 B of L1/L2 traffic - per 16-B element vector: 4.4-4.5 TB/s of tensor traffic at the B=1024 stage
+// shapes against 8 TB/s for a plain copy, scripts/r4_bn_probe.py).  Same expression, bitwise the same output.
 template <bool DS>
 __global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(
     const __bf16* __restrict__ gy, const __bf16* __restrict__ msk, const __bf16* __restrict__ z,
@@ -542,42 +551,59 @@ __global__ __launch_bounds__(TPB) void bn_bwd_apply_kernel(
     const float* __restrict__ scale_d, const float* __restrict__ c2_d, __bf16* __restrict__ out_d, long R, int C) {
   const int cg = C / 8;
   const long nv = R * cg;
+  int cur = -1;
+  float mu[8], rs[8], sc[8], k1[8], k2[8], mud[8], rsd[8], scd[8], k2d[8];
   for (long v = (long)blockIdx.x * TPB + threadIdx.x; v < nv; v += (long)gridDim.x * TPB) {
     const int c0 = (int)(v % cg) * 8;
     const long o = v * 8;
-    float g[8], m[8], zf[8], mu[8], rs[8], sc[8], k1[8], k2[8], y[8];
+    float g[8], zf[8], y[8];
     ld8(gy + o, g);
-    if (msk) {
-      ld8(msk + o, m);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) m[i] = 1.f;
-    }
     ld8(z + o, zf);
-    ldf8(mean + c0, mu);
-    ldf8(rstd + c0, rs);
-    ldf8(scale + c0, sc);
-    ldf8(c1 + c0, k1);
-    ldf8(c2 + c0, k2);
+    if (DS) ld8(zd + o, y);  // (y holds zd until the first output is computed)
+    if (c0 != cur) {  // first iteration (and any grid whose stride is not a multiple of C/8)
+      cur = c0;
+      ldf8(mean + c0, mu);
+      ldf8(rstd + c0, rs);
+      ldf8(scale + c0, sc);
+      ldf8(c1 + c0, k1);
+      ldf8(c2 + c0, k2);
+      if (DS) {
+        ldf8(mean_d + c0, mud);
+        ldf8(rstd_d + c0, rsd);
+        ldf8(scale_d + c0, scd);
+        ldf8(c2_d + c0, k2d);
+      }
+    }
+    if (msk) {
+      float m[8];
+      ld8(msk + o, m);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = m[i] > 0.f ? g[i] : 0.f;
+    }
+    float zdv[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      g[i] = m[i] > 0.f ? g[i] : 0.f;
+      zdv[i] = y[i];
       y[i] = sc[i] * (g[i] - k1[i] - (zf[i] - mu[i]) * rs[i] * k2[i]);
     }
     st8(out + o, y);
     if (DS) {
-      ld8(zd + o, zf);
-      ldf8(mean_d + c0, mu);
-      ldf8(rstd_d + c0, rs);
-      ldf8(scale_d + c0, sc);
-      ldf8(c2_d + c0, k2);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) y[i] = sc[i] * (g[i] - k1[i] - (zf[i] - mu[i]) * rs[i] * k2[i]);
+      for (int i = 0; i < 8; ++i) y[i] = scd[i] * (g[i] - k1[i] - (zdv[i] - mud[i]) * rsd[i] * k2d[i]);
       st8(out_d + o, y);
     }
   }
 }
 
+// Grid of the per-element BatchNorm passes: enough 256-thread blocks for ~4 element vectors per thread (capped at
+// 8 resident blocks per CU) and a thread count that is a multiple of C/8, so each thread keeps one channel group.
+inline unsigned bn_pass_grid(long R, int C) {
+  const long nv = R * (C / 8);
+  long g = (nv + 4L * TPB - 1) / (4L * TPB);
+  if (g < 256) g = std::min<long>(256, (nv + TPB - 1) / TPB);
+  if (g > 2048) g = 2048;
+  return (unsigned)std::max<long>(1, g);
+}
 
 // ------------------------------------------------------------------------------------------------ head
 // One block per sample: feat = mean_t h[b,t,:]; logits = W feat + bias; CE loss; g = (softmax - onehot)/B;
@@ -999,7 +1025,7 @@ int run_op(const int64_t* o, hipStream_t st) {
       const long R = o[9];
       const int C = (int)o[10];
       if (C % 8) return ecg::kBadArg;
-      const dim3 g(grid_for(R * C / 8));
+      const dim3 g(bn_pass_grid(R, C));
       if (mode == 0)
         hipLaunchKernelGGL(bn_act_kernel<0>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]), P<const float>(o[3]),
                            P<const float>(o[4]), nullptr, nullptr, nullptr, P<__bf16>(o[8]), R, C);
@@ -1033,7 +1059,8 @@ int run_op(const int64_t* o, hipStream_t st) {
       const bool ds = o[1] != 0;
       const long R = o[17];
       const int C = (int)o[18];
-      const dim3 g(grid_for(R * C / 8));
+      if (C % 8) return ecg::kBadArg;
+      const dim3 g(bn_pass_grid(R, C));
       if (!ds)
         hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]),
                            P<const __bf16>(o[3]), P<const __bf16>(o[4]), P<const float>(o[5]), P<const float>(o[6]),
