@@ -48,6 +48,31 @@ for s in "$@"; do
       step convtest 600 python -u -m pytest tests/test_conv_mc_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     enginetest)
       step enginetest 900 python -u -m pytest tests/test_resnet_engine_gpu.py tests/test_resnet_trainer_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    pipeab)
+      ECG_TAP_PIPE=1 step convtest_rp 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_mc_gpu.py -k tap
+      for v in 0 1; do ECG_TAP_NB=3 ECG_TAP_PIPE=$v step probe_pipe$v 300 python scripts/r4_conv_probe.py 30 1024; done
+      ECG_TAP_PIPE=1 ECG_TAP_ABL=1 step probe_pipe1_abl1 300 python scripts/r4_conv_probe.py 30 1024
+      ECG_TAP_PIPE=1 step enginetest_rp 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_resnet_engine_gpu.py
+      for r in 1 2; do for v in 0 1; do
+        ECG_TAP_NB=3 ECG_TAP_PIPE=$v step resnet_pipe${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+      done; done
+      ECG_RESNET_SIDE=0 step resnet_side0 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras ;;
+    tappmc)
+      export TMPDIR=/tmp
+      step pmc_tap1 120 timeout -s KILL 100 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES \
+        SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE \
+        --kernel-trace --output-format csv -d "$OUT/pmc_tap1" -o p -- python3 scripts/r4_conv_probe.py 5 1024
+      step pmc_tap2 120 timeout -s KILL 100 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+        SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD --kernel-trace --output-format csv \
+        -d "$OUT/pmc_tap2" -o p -- python3 scripts/r4_conv_probe.py 5 1024 ;;
+    tapabl)
+      for v in 0 1 2; do ECG_TAP_NB=3 ECG_TAP_ABL=$v step probe_abl$v 300 python scripts/r4_conv_probe.py 30 1024; done ;;
+    nbab)
+      for n in 3 5; do ECG_TAP_NB=$n step probe_nb$n 300 python scripts/r4_conv_probe.py 30 1024; done
+      ECG_TAP_NB=3 step convtest_nb3 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_mc_gpu.py -k tap
+      for r in 1 2; do for n in 3 5; do
+        ECG_TAP_NB=$n step resnet_nb${n}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+      done; done ;;
     tapab)
       for m in 0 2; do ECG_CONV_TAP=$m step probe_tap$m 300 python scripts/r4_conv_probe.py 30 1024; done
       for r in 1 2; do for m in 0 1 2; do
