@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Kernel-level timing of the ResNet1D-34 conv shapes at the bench batch (B=1024) and at B=4096: forward (no
 statistics), forward with the BatchNorm-statistics epilogue, data-grad (unstrided and strided) and the weight-gradient
-split-K kernel (partials only, the engine's split plan), each as the mean of back-to-back launches between HIP
-events.  Prints one JSON line per (shape, batch).
+split-K kernel (partials only, the engine's split plan), each as the mean GPU time of back-to-back launches
+replayed from a captured graph.  Prints one JSON line per (shape, batch).
 
     python scripts/r4_conv_probe.py [reps=30] [batches=1024,4096]
 """
@@ -23,16 +23,28 @@ SHAPES = [("l1", 125, 64, 64, 3, 1, 1), ("l2", 63, 128, 128, 3, 1, 1), ("l3", 32
 
 
 def timeit(fn, reps):
+    """Mean GPU time per call: ``reps`` calls captured into one hipGraph and replayed, so the host-side launch cost
+    of the Python/ctypes path (~10 us, more than the smaller kernels) does not starve the GPU between kernels."""
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(reps):
+                fn()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(reps):
-        fn()
+    for _ in range(3):
+        g.replay()
     b.record()
     torch.cuda.synchronize()
-    return a.elapsed_time(b) / reps * 1e3  # us
+    return a.elapsed_time(b) / (3 * reps) * 1e3  # us
 
 
 def main():
@@ -61,11 +73,9 @@ def main():
                 target = lib.ecg_conv1d_nlc_wgrad_target_wgs(Co, K, Ci)
                 splits = max(1, min(256, max(1, chunks // 8), max(1, target // max(1, tiles))))
             part = torch.empty((splits, Co, K * Ci), dtype=torch.float32, device=dev)
-            strm = _lib.stream_ptr(dev)
-
             def wg():
                 _lib.check(lib.ecg_conv1d_nlc_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr(), splits, B, L, Ci, Lo,
-                                                    Co, K, s, p, strm), "wgrad")
+                                                    Co, K, s, p, _lib.stream_ptr(dev)), "wgrad")
             rec["wgrad_us"] = timeit(wg, reps)
             rec["wgrad_splits"] = splits
             rec["wgrad_part_mb"] = round(part.numel() * 4 / 2**20, 1)

@@ -48,6 +48,14 @@ for s in "$@"; do
       step convtest 600 python -u -m pytest tests/test_conv_mc_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     enginetest)
       step enginetest 900 python -u -m pytest tests/test_resnet_engine_gpu.py tests/test_resnet_trainer_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    redab)
+      for r in 1 2 3; do for v in prev new; do
+        ECG_LIB_DIR=$PWD/_ablib/$v step resnet_red${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+      done; done ;;
+    epiab)
+      step convtest 600 python -u -m pytest tests/test_conv_mc_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread
+      step probe_epi 300 python scripts/r4_conv_probe.py 30 1024
+      for r in 1 2 3; do step resnet_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras; done ;;
     pipeab)
       ECG_TAP_PIPE=1 step convtest_rp 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_mc_gpu.py -k tap
       for v in 0 1; do ECG_TAP_NB=3 ECG_TAP_PIPE=$v step probe_pipe$v 300 python scripts/r4_conv_probe.py 30 1024; done
@@ -66,7 +74,7 @@ for s in "$@"; do
         SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD --kernel-trace --output-format csv \
         -d "$OUT/pmc_tap2" -o p -- python3 scripts/r4_conv_probe.py 5 1024 ;;
     tapabl)
-      for v in 0 1 2; do ECG_TAP_NB=3 ECG_TAP_ABL=$v step probe_abl$v 300 python scripts/r4_conv_probe.py 30 1024; done ;;
+      for v in 0 1 2 4 6 7; do ECG_TAP_PIPE=0 ECG_TAP_NB=3 ECG_TAP_ABL=$v step probe_abl$v 300 python scripts/r4_conv_probe.py 30 1024; done ;;
     nbab)
       for n in 3 5; do ECG_TAP_NB=$n step probe_nb$n 300 python scripts/r4_conv_probe.py 30 1024; done
       ECG_TAP_NB=3 step convtest_nb3 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_mc_gpu.py -k tap
@@ -92,6 +100,10 @@ for s in "$@"; do
         python3 bench.py --steps 200 --warmup 50 --no-extras
       step prof_resnet 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_resnet" -o resnet -- \
         python3 bench.py --model resnet1d34 --steps 10 --warmup 3 --no-extras ;;
+    timeline0)
+      export TMPDIR=/tmp
+      ECG_RESNET_SIDE=0 step timeline0 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/timeline0" -o tl -- \
+        python3 scripts/resnet_timeline.py run ;;
     timeline)
       export TMPDIR=/tmp
       step timeline 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/timeline" -o tl -- \
