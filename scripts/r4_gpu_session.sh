@@ -48,6 +48,17 @@ for s in "$@"; do
       step convtest 600 python -u -m pytest tests/test_conv_mc_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     enginetest)
       step enginetest 900 python -u -m pytest tests/test_resnet_engine_gpu.py tests/test_resnet_trainer_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    module1)
+      step shard_prep 300 python shard_prep.py --dataset synthetic
+      step module1 1000 python bench_locality.py --batch-sizes 64 128 256 512 --reps 5 --results-dir "$OUT/modules" ;;
+    module2)
+      step module2 900 python benchmark_part_2.py --results-dir "$OUT/modules" ;;
+    module3)
+      [ -d data/shards ] || step shard_prep 300 python shard_prep.py --dataset synthetic
+      step pseudo_fl 600 python part3_mpi_gpu_train.py --steps 200 --results-csv "$OUT/modules/part3_mpi_cuda_results.csv"
+      step fedavg 600 python part3_fedavg_overlap_mpi_gpu.py --data-root data/shards --rounds 5 --local-steps 50 \
+        --config both --results-csv "$OUT/modules/fedavg_results_w1.csv"
+      step plots 300 python plot_results.py --results-dir "$OUT/modules" ;;
     redab)
       for r in 1 2 3; do for v in prev new; do
         ECG_LIB_DIR=$PWD/_ablib/$v step resnet_red${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
