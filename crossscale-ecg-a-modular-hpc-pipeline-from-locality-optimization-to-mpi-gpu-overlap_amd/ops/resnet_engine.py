@@ -286,7 +286,7 @@ class ResNetStepEngine:
                self._gptr(bn.weight), self._gptr(bn.bias), P(st.c1), P(st.c2), G)
 
         # ---- BatchNorm finalize fused into the statistics-producing conv (csrc/include/bn_tail.h): replaces the
-        # BN_FIN op (two launches) after each conv forward and data-grad conv.  ECG_BN_TAIL=0: separate BN_FIN ops.
+        # BN_FIN op after each conv forward and data-grad conv.  ECG_BN_TAIL=0: separate (one-launch) BN_FIN ops.
         use_tail = os.environ.get("ECG_BN_TAIL", "1") != "0"
         self.bn_tail = use_tail
         tail_blobs: List[bytes] = []

@@ -382,43 +382,42 @@ __device__ __forceinline__ void bn_fin_outputs(const FinArgs& a, int c, double v
   }
 }
 
-// Two launches: phase 1 writes the G level-2 partials with plain stores, the kernel boundary makes
-// them visible, phase 2 (one block per 64 channels) reduces them - no fences on the critical path.
-__global__ __launch_bounds__(TPB) void bn_partial_kernel(FinArgs a) {
-  __shared__ double red[4][2][64];
-  const int tid = threadIdx.x, cl = tid & 63, g4 = tid >> 6;
+// One launch: a 1024-thread block per 64 channels sums the T partial rows of both statistics (16 row groups x 64
+// channels; each thread's rows t = rg, rg + 16, ... issued 16 at a time, so T <= 256 is ONE memory round trip),
+// combines the row groups in a fixed order (fp64, bitwise reproducible) and finalizes.  The producing conv stores
+// its partial rows with plain stores; the kernel boundary makes them visible.
+__global__ __launch_bounds__(1024) void bn_fin1_kernel(FinArgs a) {
+  __shared__ double red[16][2][64];
+  const int tid = threadIdx.x, cl = tid & 63, rg = tid >> 6;
   const int c = blockIdx.x * 64 + cl;
-  const int G = gridDim.y;
-  const int t0 = (int)((long)a.T * blockIdx.y / G), t1 = (int)((long)a.T * (blockIdx.y + 1) / G);
   double s1 = 0.0, s2 = 0.0;
-  for (int t = t0 + g4; t < t1; t += 4) {
-    s1 += (double)a.sA[(long)t * a.C + c];
-    s2 += (double)a.sB[(long)t * a.C + c];
+  for (int t0 = rg; t0 < a.T; t0 += 16 * 16) {
+    float v1[16], v2[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int t = min(t0 + 16 * u, a.T - 1);  // clamped: no branch, the extra rows are not added
+      v1[u] = a.sA[(long)t * a.C + c];
+      v2[u] = a.sB[(long)t * a.C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (t0 + 16 * u < a.T) {
+        s1 += (double)v1[u];
+        s2 += (double)v2[u];
+      }
   }
-  red[g4][0][cl] = s1;
-  red[g4][1][cl] = s2;
+  red[rg][0][cl] = s1;
+  red[rg][1][cl] = s2;
   __syncthreads();
   if (tid < 64) {
-    a.scratch[((long)blockIdx.y * 2 + 0) * a.C + c] = red[0][0][cl] + red[1][0][cl] + red[2][0][cl] + red[3][0][cl];
-    a.scratch[((long)blockIdx.y * 2 + 1) * a.C + c] = red[0][1][cl] + red[1][1][cl] + red[2][1][cl] + red[3][1][cl];
+    double v1 = 0.0, v2 = 0.0;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      v1 += red[g][0][cl];
+      v2 += red[g][1][cl];
+    }
+    bn_fin_outputs(a, c, v1, v2);
   }
-}
-
-__global__ __launch_bounds__(TPB) void bn_final_kernel(FinArgs a, int G) {
-  __shared__ double red[4][2][64];
-  const int tid = threadIdx.x, cl = tid & 63, g4 = tid >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  double v1 = 0.0, v2 = 0.0;
-  for (int g = g4; g < G; g += 4) {
-    v1 += a.scratch[((long)g * 2 + 0) * a.C + c];
-    v2 += a.scratch[((long)g * 2 + 1) * a.C + c];
-  }
-  red[g4][0][cl] = v1;
-  red[g4][1][cl] = v2;
-  __syncthreads();
-  if (tid < 64)
-    bn_fin_outputs(a, c, red[0][0][cl] + red[1][0][cl] + red[2][0][cl] + red[3][0][cl],
-                   red[0][1][cl] + red[1][1][cl] + red[2][1][cl] + red[3][1][cl]);
 }
 
 // MODE 0: out = relu(z*scale + shift); 1: out = relu(z*scale + shift + res); 2: + (zd*scale_d + shift_d)
@@ -1016,8 +1015,10 @@ int run_op(const int64_t* o, hipStream_t st) {
       a.c2 = P<float>(o[22]);
       const int G = (int)o[23];
       if (a.C % 64 || G < 1 || G > 1024) return ecg::kBadArg;
-      hipLaunchKernelGGL(bn_partial_kernel, dim3(a.C / 64, G), dim3(TPB), 0, st, a);
-      hipLaunchKernelGGL(bn_final_kernel, dim3(a.C / 64), dim3(TPB), 0, st, a, G);
+      // one launch (ResNet1D-34 B=1024 with ECG_BN_TAIL=0: 3.48 ms/step vs 3.76 for the former two-launch
+      // partial + final form; the fused tail stays the default at 3.39, profiles/r4/bn_fin_ab.txt)
+      hipLaunchKernelGGL(bn_fin1_kernel, dim3(a.C / 64), dim3(1024), 0, st, a);
+      (void)G;
       break;
     }
     case OP_BN_ACT: {

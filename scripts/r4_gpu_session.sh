@@ -59,6 +59,20 @@ for s in "$@"; do
       step fedavg 600 python part3_fedavg_overlap_mpi_gpu.py --data-root data/shards --rounds 5 --local-steps 50 \
         --config both --results-csv "$OUT/modules/fedavg_results_w1.csv"
       step plots 300 python plot_results.py --results-dir "$OUT/modules" ;;
+    libab)  # LIBS="a b c": interleaved ResNet runs against _ablib/<a>, _ablib/<b>, ...
+      for r in 1 2 3; do for v in ${LIBS}; do
+        ECG_LIB_DIR=$PWD/_ablib/$v step resnet_lib${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+      done; done ;;
+    wgafter)
+      for r in 1 2 3; do for v in 0 1; do
+        ECG_WG_AFTER=$v step resnet_wga${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+      done; done ;;
+    finab)
+      for r in 1 2 3; do
+        ECG_BN_TAIL=1 step resnet_tail1_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+        ECG_BN_TAIL=0 ECG_BN_FIN1=1 step resnet_fin1_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+        ECG_BN_TAIL=0 ECG_BN_FIN1=0 step resnet_fin2_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+      done ;;
     redab)
       for r in 1 2 3; do for v in prev new; do
         ECG_LIB_DIR=$PWD/_ablib/$v step resnet_red${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
