@@ -73,6 +73,11 @@ for s in "$@"; do
         ECG_BN_TAIL=0 ECG_BN_FIN1=1 step resnet_fin1_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
         ECG_BN_TAIL=0 ECG_BN_FIN1=0 step resnet_fin2_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
       done ;;
+    envab)  # ENVS="A=1 B=2" pairs: interleaved runs, default vs each setting
+      for r in 1 2 3; do
+        step resnet_env0_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+        for e in ${ENVS}; do env $e python -c pass && step "resnet_env_${e}_$r" 300 env $e python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras; done
+      done ;;
     redab)
       for r in 1 2 3; do for v in prev new; do
         ECG_LIB_DIR=$PWD/_ablib/$v step resnet_red${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
