@@ -78,6 +78,12 @@ for s in "$@"; do
         step resnet_env0_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
         for e in ${ENVS}; do env $e python -c pass && step "resnet_env_${e}_$r" 300 env $e python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras; done
       done ;;
+    headab)
+      ECG_TINY_HEAD_DIRECT=1 step tinytest_h1 600 python -u -m pytest tests/test_fused_tiny_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread
+      for r in 1 2 3 4; do for h in 0 1 2; do
+        ECG_TINY_HEAD_DIRECT=$h step tiny20_h${h}_$r 300 python bench.py --steps 20 --warmup 5 --no-extras
+      done; done
+      for h in 0 1; do ECG_TINY_HEAD_DIRECT=$h step tiny500_h$h 300 python bench.py --steps 500 --warmup 100 --no-extras; done ;;
     redab)
       for r in 1 2 3; do for v in prev new; do
         ECG_LIB_DIR=$PWD/_ablib/$v step resnet_red${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
