@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-4 GPU measurement session on one MI355X (run by gpurun from the repo root):
 #   bash scripts/r4_gpu_session.sh <tag> <steps...>
-# steps: tests | bench | resnet | probe | pmc | stats | tinypmc   (any subset, in order)
+# steps (any subset, in order): tests smoke bench bench20 resnet | probe bnprobe convtest enginetest |
+#   module1 module2 module3 | libab (LIBS=...) envab (ENVS=...) finab tapab | pmc tappmc tinypmc stats timeline timeline0
 # Every GPU step runs under its own time limit; a crash, abort or timeout ends the session.
 set -u
 cd "$(dirname "$0")/.."
@@ -63,44 +64,16 @@ for s in "$@"; do
       for r in 1 2 3; do for v in ${LIBS}; do
         ECG_LIB_DIR=$PWD/_ablib/$v step resnet_lib${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
       done; done ;;
-    wgafter)
-      for r in 1 2 3; do for v in 0 1; do
-        ECG_WG_AFTER=$v step resnet_wga${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
-      done; done ;;
-    finab)
+    finab)  # fused BatchNorm finalize vs the separate one-launch finalize
       for r in 1 2 3; do
         ECG_BN_TAIL=1 step resnet_tail1_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
-        ECG_BN_TAIL=0 ECG_BN_FIN1=1 step resnet_fin1_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
-        ECG_BN_TAIL=0 ECG_BN_FIN1=0 step resnet_fin2_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
+        ECG_BN_TAIL=0 step resnet_fin1_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
       done ;;
     envab)  # ENVS="A=1 B=2" pairs: interleaved runs, default vs each setting
       for r in 1 2 3; do
         step resnet_env0_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
         for e in ${ENVS}; do env $e python -c pass && step "resnet_env_${e}_$r" 300 env $e python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras; done
       done ;;
-    headab)
-      ECG_TINY_HEAD_DIRECT=1 step tinytest_h1 600 python -u -m pytest tests/test_fused_tiny_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread
-      for r in 1 2 3 4; do for h in 0 1 2; do
-        ECG_TINY_HEAD_DIRECT=$h step tiny20_h${h}_$r 300 python bench.py --steps 20 --warmup 5 --no-extras
-      done; done
-      for h in 0 1; do ECG_TINY_HEAD_DIRECT=$h step tiny500_h$h 300 python bench.py --steps 500 --warmup 100 --no-extras; done ;;
-    redab)
-      for r in 1 2 3; do for v in prev new; do
-        ECG_LIB_DIR=$PWD/_ablib/$v step resnet_red${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
-      done; done ;;
-    epiab)
-      step convtest 600 python -u -m pytest tests/test_conv_mc_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread
-      step probe_epi 300 python scripts/r4_conv_probe.py 30 1024
-      for r in 1 2 3; do step resnet_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras; done ;;
-    pipeab)
-      ECG_TAP_PIPE=1 step convtest_rp 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_mc_gpu.py -k tap
-      for v in 0 1; do ECG_TAP_NB=3 ECG_TAP_PIPE=$v step probe_pipe$v 300 python scripts/r4_conv_probe.py 30 1024; done
-      ECG_TAP_PIPE=1 ECG_TAP_ABL=1 step probe_pipe1_abl1 300 python scripts/r4_conv_probe.py 30 1024
-      ECG_TAP_PIPE=1 step enginetest_rp 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_resnet_engine_gpu.py
-      for r in 1 2; do for v in 0 1; do
-        ECG_TAP_NB=3 ECG_TAP_PIPE=$v step resnet_pipe${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
-      done; done
-      ECG_RESNET_SIDE=0 step resnet_side0 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras ;;
     tappmc)
       export TMPDIR=/tmp
       step pmc_tap1 120 timeout -s KILL 100 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES \
@@ -109,14 +82,6 @@ for s in "$@"; do
       step pmc_tap2 120 timeout -s KILL 100 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
         SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD --kernel-trace --output-format csv \
         -d "$OUT/pmc_tap2" -o p -- python3 scripts/r4_conv_probe.py 5 1024 ;;
-    tapabl)
-      for v in 0 1 2 4 6 7; do ECG_TAP_PIPE=0 ECG_TAP_NB=3 ECG_TAP_ABL=$v step probe_abl$v 300 python scripts/r4_conv_probe.py 30 1024; done ;;
-    nbab)
-      for n in 3 5; do ECG_TAP_NB=$n step probe_nb$n 300 python scripts/r4_conv_probe.py 30 1024; done
-      ECG_TAP_NB=3 step convtest_nb3 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_mc_gpu.py -k tap
-      for r in 1 2; do for n in 3 5; do
-        ECG_TAP_NB=$n step resnet_nb${n}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
-      done; done ;;
     tapab)
       for m in 0 2; do ECG_CONV_TAP=$m step probe_tap$m 300 python scripts/r4_conv_probe.py 30 1024; done
       for r in 1 2; do for m in 0 1 2; do
