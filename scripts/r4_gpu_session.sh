@@ -64,6 +64,11 @@ for s in "$@"; do
       for r in 1 2 3; do for v in ${LIBS}; do
         ECG_LIB_DIR=$PWD/_ablib/$v step resnet_lib${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
       done; done ;;
+    tinyenv)  # ENVS="A=1 ...": interleaved TinyECG K=20 runs, default vs each setting
+      for r in 1 2 3 4; do
+        step tiny20_env0_$r 300 python bench.py --steps 20 --warmup 5 --no-extras
+        for e in ${ENVS}; do step "tiny20_env_${e}_$r" 300 env $e python bench.py --steps 20 --warmup 5 --no-extras; done
+      done ;;
     finab)  # fused BatchNorm finalize vs the separate one-launch finalize
       for r in 1 2 3; do
         ECG_BN_TAIL=1 step resnet_tail1_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
