@@ -47,6 +47,8 @@ for s in "$@"; do
       step bnprobe 300 python scripts/r4_bn_probe.py 50 ;;
     convtest)
       step convtest 600 python -u -m pytest tests/test_conv_mc_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    tailtest)
+      step tailtest 300 python -u -m pytest tests/test_resnet_engine_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "large_batch or depth34_well" ;;
     enginetest)
       step enginetest 900 python -u -m pytest tests/test_resnet_engine_gpu.py tests/test_resnet_trainer_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     module1)
