@@ -1020,6 +1020,8 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     ECG_STAMP(3)
     S.template head_and_M<TRAIN>(ylab, inv_B, out, out_stride, b);
     if (!TRAIN) return;
+    if (MODE == 0 && stamps && (tid & 63) == 0 && (S.w <= 1 || S.w == WAVES - 1))  // diagnostic: head / M wave ends
+      stamps[(long)b * 16 + 8 + (S.w == 0 ? 0 : S.w == 1 ? 1 : 2)] = __builtin_amdgcn_s_memtime();
     __syncthreads();
     ECG_STAMP(4)
     S.dgrad();

@@ -43,6 +43,10 @@ for s in "$@"; do
       for i in 1 2 3; do step resnet_$i 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras; done ;;
     probe)
       step probe 300 python scripts/r4_conv_probe.py 30 1024,4096 ;;
+    diag)
+      step diag 300 python scripts/diag_step_phases.py ;;
+    headm)
+      step headm 120 python scripts/diag_head_m.py ;;
     bnprobe)
       step bnprobe 300 python scripts/r4_bn_probe.py 50 ;;
     convtest)
