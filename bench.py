@@ -394,10 +394,16 @@ def main(argv=None):
     tbar = HostBarrier(ctx)
 
     timed_plan = round_plan(a.steps, S)
-    if a.warmup > 0:
-        runner.run(round_plan(a.warmup, S), then=timed_plan[0])
-    if hasattr(trainer, "prepare"):  # capture + upload every graph the timed plan replays, outside the timing
-        trainer.prepare(sorted(set(timed_plan)))
+    warm_plan = round_plan(a.warmup, S) if a.warmup > 0 else []
+    # One-time host work first - capture + upload of every round graph the warm-up and timed plans replay (the
+    # warm-up replay inside prepare() is rolled back) and a full GC pass - THEN the warm-up rounds, so the timed
+    # region starts right behind real training steps instead of after ~0.1 s of GPU idle (clocks and caches had
+    # cooled: TinyECG K=20 13.1 -> 11.9 us/step wall, ResNet1D-34 3.44 -> 3.41 ms; profiles/r4/bench_order_ab.txt).
+    if hasattr(trainer, "prepare"):
+        trainer.prepare(sorted(set(timed_plan) | set(warm_plan)))
+    gc.collect()
+    if warm_plan:
+        runner.run(warm_plan, then=timed_plan[0])
     runner.syncs = 0
 
     def bracket():  # synchronize + barrier (+ synchronize again only when the barrier itself enqueued GPU work)
@@ -415,8 +421,8 @@ def main(argv=None):
     # the timed collectives' span and the compute stream's stall on them (events; resolved after the region)
     runner.timer = CommTimer(on_gpu, dev) if ctx.distributed else None
     # no cyclic-GC pass inside the timed region (a collection there is host jitter, not work: one K=20 run measured
-    # 15.7 us/step wall at 11.4 us/step of GPU time); the same work runs, the collector resumes right after
-    gc.collect()
+    # 15.7 us/step wall at 11.4 us/step of GPU time); the full pass ran before the warm-up, the collector resumes
+    # right after the region
     gc.disable()
     try:
         bracket()

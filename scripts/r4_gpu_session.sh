@@ -45,6 +45,9 @@ for s in "$@"; do
       step probe 300 python scripts/r4_conv_probe.py 30 1024,4096 ;;
     diag)
       step diag 300 python scripts/diag_step_phases.py ;;
+    roundfix)  # ENVS="A=1 ...": fixed vs per-step cost of a round replay, default and each setting
+      step roundfix0 120 python scripts/diag_round_fixed.py
+      for e in ${ENVS:-}; do step "roundfix_${e}" 120 env $e python scripts/diag_round_fixed.py; done ;;
     headm)
       step headm 120 python scripts/diag_head_m.py ;;
     bnprobe)
