@@ -23,6 +23,9 @@ def main():
     x = torch.randn(N, L, device=dev)
     y = torch.zeros(N, dtype=torch.long, device=dev)
     ns = (1, 2, 5, 10, 20, 50)
+    if os.environ.get("DIAG_WAVES"):  # force the step kernel's wave count (8 or 16) before any graph is captured
+        from crossscale_ecg.ops import _lib
+        _lib.kernels().ecg_tiny_force_waves(int(os.environ["DIAG_WAVES"]))
     tr = FusedTinyTrainer(TinyECG().to(dev), x, y, B, 50, lr=1e-2, momentum=0.9, seed=0)
     tr.prepare(list(ns))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
