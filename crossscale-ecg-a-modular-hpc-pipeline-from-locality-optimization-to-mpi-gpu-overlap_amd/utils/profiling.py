@@ -21,8 +21,12 @@ def _lib():
         return _roctx
     _tried = True
     import torch
-    cands = [os.path.join(os.path.dirname(torch.__file__), "lib", "libroctx64.so"),
-             "/opt/rocm/lib/libroctx64.so", "/opt/rocm/lib/librocprofiler-sdk-roctx.so"]
+    # rocprofv3 (rocprofiler-sdk) records the markers of its own roctx library; the legacy roctracer libroctx64
+    # (also the copy torch ships) is only seen by the old tracer, so the SDK library comes first
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    cands = [os.path.join(rocm, "lib", "librocprofiler-sdk-roctx.so"),
+             os.path.join(os.path.dirname(torch.__file__), "lib", "libroctx64.so"),
+             os.path.join(rocm, "lib", "libroctx64.so")]
     for c in cands:
         if os.path.exists(c):
             try:

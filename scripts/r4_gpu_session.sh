@@ -48,6 +48,11 @@ for s in "$@"; do
     roundfix)  # ENVS="A=1 ...": fixed vs per-step cost of a round replay, default and each setting
       step roundfix0 120 python scripts/diag_round_fixed.py
       for e in ${ENVS:-}; do step "roundfix_${e}" 120 env $e python scripts/diag_round_fixed.py; done ;;
+    m1trace)  # Module 1 B=128: A0 vs A3 compute ranges under a kernel + HIP API + marker trace
+      export TMPDIR=/tmp
+      step m1trace 400 rocprofv3 --kernel-trace --hip-trace --marker-trace --output-format csv -d "$OUT/m1trace" \
+        -o t -- python3 scripts/trace_module1_b128.py run
+      step m1parse 120 python scripts/trace_module1_b128.py parse "$OUT/m1trace" ;;
     headm)
       step headm 120 python scripts/diag_head_m.py ;;
     bnprobe)
