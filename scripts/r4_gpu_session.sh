@@ -59,6 +59,8 @@ for s in "$@"; do
       step bnprobe 300 python scripts/r4_bn_probe.py 50 ;;
     convtest)
       step convtest 600 python -u -m pytest tests/test_conv_mc_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    tinytest)
+      step tinytest 400 python -u -m pytest tests/test_fused_tiny_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     tailtest)
       step tailtest 300 python -u -m pytest tests/test_resnet_engine_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "large_batch or depth34_well" ;;
     enginetest)
