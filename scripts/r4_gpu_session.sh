@@ -80,6 +80,13 @@ for s in "$@"; do
       for r in 1 2 3; do for v in ${LIBS}; do
         ECG_LIB_DIR=$PWD/_ablib/$v step resnet_lib${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
       done; done ;;
+    tinylib)  # LIBS="a b": interleaved TinyECG K=20 / K=500 runs against _ablib/<a>, _ablib/<b>
+      for r in 1 2 3 4; do for v in ${LIBS}; do
+        ECG_LIB_DIR=$PWD/_ablib/$v step tiny20_lib${v}_$r 300 python bench.py --steps 20 --warmup 5 --no-extras
+      done; done
+      for v in ${LIBS}; do
+        ECG_LIB_DIR=$PWD/_ablib/$v step tiny500_lib${v} 300 python bench.py --steps 500 --warmup 100 --no-extras
+      done ;;
     tinyenv)  # ENVS="A=1 ...": interleaved TinyECG K=20 runs, default vs each setting
       for r in 1 2 3 4; do
         step tiny20_env0_$r 300 python bench.py --steps 20 --warmup 5 --no-extras
