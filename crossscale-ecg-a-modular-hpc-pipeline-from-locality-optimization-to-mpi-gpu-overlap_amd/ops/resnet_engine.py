@@ -173,6 +173,8 @@ class ResNetStepEngine:
         self.x = self._t(B, L, dtype=torch.float32)
         self.y = self._t(B, dtype=torch.int32)
         self.z0 = self._t(B, Lz, 64)
+        # the stem max-pool's argmax per output (0..2 within its window), written by the forward for the backward
+        self.pool_am = torch.zeros(B * Lp * 64, dtype=torch.uint8, device=dev)
         self.h0 = self._t(B, Lp, 64)
         acts = []
         for (Li, Ci, Lo, Co, s), blk in zip(shapes, blocks):
@@ -354,7 +356,7 @@ class ResNetStepEngine:
            tail(T0, 64, [fin_fwd_words(bn0, B * Lz)]))
         if not use_tail:
             fin_fwd(bn0, T0, B * Lz)
-        op("STEM_POOL", P(self.z0), P(bn0.scale), P(bn0.shift), P(self.h0), B, Lz, Lp, 64)
+        op("STEM_POOL", P(self.z0), P(bn0.scale), P(bn0.shift), P(self.h0), B, Lz, Lp, 64, P(self.pool_am))
         xin = self.h0
         # side lane (with fused finalizes): a block's downsample conv runs beside conv1 -> BN_ACT -> conv2, on BN
         # partials of its own; the BN_ACT that adds it joins the lanes
@@ -487,7 +489,7 @@ class ResNetStepEngine:
         # =============================== stem backward
         Tb0 = (B * Lz + stem_chunk_b - 1) // stem_chunk_b
         op("STEM_BWD_REDUCE", P(gcur), P(self.z0), P(bn0.scale), P(bn0.shift), P(bn0.mean), P(bn0.rstd), P(dz0),
-           P(bpart), B, Lz, Lp, 64, stem_chunk_b, tail(Tb0, 64, [fin_bwd_words(bn0, B * Lz, 1)]))
+           P(bpart), B, Lz, Lp, 64, stem_chunk_b, tail(Tb0, 64, [fin_bwd_words(bn0, B * Lz, 1)]), P(self.pool_am))
         if not use_tail:
             fin_bwd(bn0, Tb0, B * Lz, 1)
         op("STEM_WGRAD", P(dz0), P(self.z0), P(bn0.mean), P(bn0.rstd), P(bn0.scale), P(bn0.c1), P(bn0.c2),

@@ -151,10 +151,11 @@ __global__ __launch_bounds__(TPB) void stem_fwd_kernel(const float* __restrict__
     ecg::bn_tail<TPB>(tail, stats, 2, gridDim.x, 64, blockIdx.x, 0, 64, reinterpret_cast<unsigned char*>(&xs[0][0]));
 }
 
-// out[b,o,c] = max_{j in {2o-1,2o,2o+1}} relu(z[b,j,c]*scale[c] + shift[c])   (MaxPool1d(3, 2, 1))
+// out[b,o,c] = max_{j in {2o-1,2o,2o+1}} relu(z[b,j,c]*scale[c] + shift[c])   (MaxPool1d(3, 2, 1)); am[b,o,c]
+// (optional) = j - (2o-1) of the first maximum, for the backward
 __global__ __launch_bounds__(TPB) void stem_pool_kernel(const __bf16* __restrict__ z, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, __bf16* __restrict__ out,
-                                                        int B, int Lz, int Lp, int C) {
+                                                        uint8_t* __restrict__ am, int B, int Lz, int Lp, int C) {
   const int cg = C / 8;
   const long nv = (long)B * Lp * cg;
   for (long v = (long)blockIdx.x * TPB + threadIdx.x; v < nv; v += (long)gridDim.x * TPB) {
@@ -162,10 +163,14 @@ __global__ __launch_bounds__(TPB) void stem_pool_kernel(const __bf16* __restrict
     const long bo = v / cg;
     const int o = (int)(bo % Lp), b = (int)(bo / Lp);
     float sc[8], sh[8], mx[8];
+    uint32_t ix[8];
     ldf8(scale + c0, sc);
     ldf8(shift + c0, sh);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) mx[i] = -INFINITY;
+    for (int i = 0; i < 8; ++i) {
+      mx[i] = -INFINITY;
+      ix[i] = 0u;
+    }
 #pragma unroll
     for (int d = -1; d <= 1; ++d) {
       const int j = 2 * o + d;
@@ -173,19 +178,34 @@ __global__ __launch_bounds__(TPB) void stem_pool_kernel(const __bf16* __restrict
       float zf[8];
       ld8(z + ((long)b * Lz + j) * C + c0, zf);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) mx[i] = fmaxf(mx[i], fmaxf(zf[i] * sc[i] + sh[i], 0.f));
+      for (int i = 0; i < 8; ++i) {
+        const float av = fmaxf(zf[i] * sc[i] + sh[i], 0.f);
+        if (av > mx[i]) {  // strict: the first maximum wins (the order the backward has always used)
+          mx[i] = av;
+          ix[i] = (uint32_t)(d + 1);
+        }
+      }
     }
     st8(out + bo * C + c0, mx);
+    if (am) {
+      uint2 w;
+      w.x = ix[0] | ix[1] << 8 | ix[2] << 16 | ix[3] << 24;
+      w.y = ix[4] | ix[5] << 8 | ix[6] << 16 | ix[7] << 24;
+      *reinterpret_cast<uint2*>(am + bo * C + c0) = w;
+    }
   }
 }
 
 // Backward of ReLU(BN(z)) -> MaxPool: dz[b,j,c] = (a_j > 0) * sum_{windows o whose first argmax is j} gp[b,o,c]
-// (written bf16) and BN partials sum(dz), sum(dz * xhat) per block of rows.
+// (written bf16) and BN partials sum(dz), sum(dz * xhat) per block of rows.  The argmax comes from the forward
+// (stem_pool_kernel's ``am``, as PyTorch's max_pool1d backward uses the forward's indices): one z row per output
+// row instead of recomputing both windows from five (round 4: 3.363-3.370 vs 3.369-3.377 ms/step, r4_stemam1).
 __global__ __launch_bounds__(TPB) void stem_bwd_reduce_kernel(
     const __bf16* __restrict__ gp, const __bf16* __restrict__ z, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ mean, const float* __restrict__ rstd,
     __bf16* __restrict__ dz, float* __restrict__ part, int B, int Lz, int Lp, int C, int chunk,
-    const ecg::BnTail* __restrict__ tail) {  // tail: the stem BatchNorm's backward finalize fused here, or null
+    const ecg::BnTail* __restrict__ tail,  // tail: the stem BatchNorm's backward finalize fused here, or null
+    const uint8_t* __restrict__ am) {      // am: the forward's argmax per pooled output (stem_pool_kernel)
   __shared__ __attribute__((aligned(16))) float red[TPB * 16];
   const int cg = C / 8, tid = threadIdx.x;
   const int rpp = TPB / cg, roff = tid / cg, c0 = (tid % cg) * 8;
@@ -201,51 +221,27 @@ __global__ __launch_bounds__(TPB) void stem_bwd_reduce_kernel(
   const long r1 = active ? min(R, (long)(blockIdx.x + 1) * chunk) : 0;
   for (long r = (long)blockIdx.x * chunk + roff; r < r1; r += rpp) {
     const int b = (int)(r / Lz), j = (int)(r % Lz);
-    const __bf16* zb = z + (long)b * Lz * C + c0;
-    // the windows containing j are o0 = j>>1 and o1 = (j+1)>>1 (equal for even j); together they cover the rows
-    // p0 .. p0+4, p0 = 2*o0 - 1.  All seven loads (five z rows, two gradient rows) are issued unconditionally from
-    // clamped addresses, so they are in flight together; validity is applied to the values.
-    const int o0 = j >> 1, o1 = (j + 1) >> 1, p0 = 2 * o0 - 1;
+    // the windows containing j are o0 = j>>1 (rows p0 .. p0+2, p0 = 2*o0 - 1) and, for odd j, o1 = o0 + 1 (rows
+    // j .. j+2): row j is window o0's first maximum when am = 1 + (j & 1), window o1's when am = 0.  All loads are
+    // issued from clamped addresses, validity applied to the values.
+    const int o0 = j >> 1, o1 = (j + 1) >> 1;
     const bool has1 = o1 != o0 && o1 < Lp;
-    float zq[5][8], g0[8], g1[8];
-#pragma unroll
-    for (int u = 0; u < 5; ++u) ld8(zb + (long)min(max(p0 + u, 0), Lz - 1) * C, zq[u]);
+    float zj[8], g0[8], g1[8];
+    ld8(z + ((long)b * Lz + j) * C + c0, zj);
     ld8(gp + ((long)b * Lp + o0) * C + c0, g0);
     ld8(gp + ((long)b * Lp + min(o1, Lp - 1)) * C + c0, g1);
-    float g[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      // window o0: rows p0, p0+1, p0+2 (first maximum wins, out-of-range rows skipped)
-      float best = -INFINITY;
-      int arg = -1;
-#pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        const int p = p0 + d;
-        const float av = fmaxf(zq[d][i] * sc[i] + sh[i], 0.f);
-        if (p >= 0 && p < Lz && av > best) { best = av; arg = p; }
-      }
-      float gi = arg == j ? g0[i] : 0.f;
-      if (has1) {  // window o1 = o0 + 1: rows p0+2 .. p0+4
-        float best1 = -INFINITY;
-        int arg1 = -1;
-#pragma unroll
-        for (int d = 2; d < 5; ++d) {
-          const int p = p0 + d;
-          const float av = fmaxf(zq[d][i] * sc[i] + sh[i], 0.f);
-          if (p >= 0 && p < Lz && av > best1) { best1 = av; arg1 = p; }
-        }
-        if (arg1 == j) gi += g1[i];
-      }
-      g[i] = gi;
-    }
-    float zj[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) zj[i] = (j & 1) ? zq[2][i] : zq[1][i];  // row j = p0 + 1 + (j & 1)
+    const uint2 a0 = *reinterpret_cast<const uint2*>(am + ((long)b * Lp + o0) * C + c0);
+    const uint2 a1w = *reinterpret_cast<const uint2*>(am + ((long)b * Lp + min(o1, Lp - 1)) * C + c0);
+    const uint32_t want0 = 1u + (uint32_t)(j & 1);
     float d[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+      const uint32_t m0 = ((i < 4 ? a0.x : a0.y) >> (8 * (i & 3))) & 0xffu;
+      const uint32_t m1 = ((i < 4 ? a1w.x : a1w.y) >> (8 * (i & 3))) & 0xffu;
+      float gi = m0 == want0 ? g0[i] : 0.f;
+      if (has1 && m1 == 0u) gi += g1[i];
       const float av = zj[i] * sc[i] + sh[i];
-      d[i] = av > 0.f ? g[i] : 0.f;
+      d[i] = av > 0.f ? gi : 0.f;
     }
     st8(dz + r * C + c0, d);
 #pragma unroll
@@ -1088,18 +1084,18 @@ int run_op(const int64_t* o, hipStream_t st) {
     case OP_STEM_POOL: {
       const int B = (int)o[5], Lz = (int)o[6], Lp = (int)o[7], C = (int)o[8];
       hipLaunchKernelGGL(stem_pool_kernel, dim3(grid_for((long)B * Lp * C / 8)), dim3(TPB), 0, st,
-                         P<const __bf16>(o[1]), P<const float>(o[2]), P<const float>(o[3]), P<__bf16>(o[4]), B, Lz, Lp,
-                         C);
+                         P<const __bf16>(o[1]), P<const float>(o[2]), P<const float>(o[3]), P<__bf16>(o[4]),
+                         P<uint8_t>(o[9]), B, Lz, Lp, C);
       break;
     }
     case OP_STEM_BWD_REDUCE: {
       const int B = (int)o[9], Lz = (int)o[10], Lp = (int)o[11], C = (int)o[12], chunk = (int)o[13];
-      if (C % 8 || 2 * C * (TPB / (C / 8)) > TPB * 16 || (o[14] && (C % 64 || C > 256))) return ecg::kBadArg;
+      if (C % 8 || 2 * C * (TPB / (C / 8)) > TPB * 16 || (o[14] && (C % 64 || C > 256)) || !o[15]) return ecg::kBadArg;
       const long R = (long)B * Lz;
       hipLaunchKernelGGL(stem_bwd_reduce_kernel, dim3((unsigned)((R + chunk - 1) / chunk)), dim3(TPB), 0, st,
                          P<const __bf16>(o[1]), P<const __bf16>(o[2]), P<const float>(o[3]), P<const float>(o[4]),
                          P<const float>(o[5]), P<const float>(o[6]), P<__bf16>(o[7]), P<float>(o[8]), B, Lz, Lp, C,
-                         chunk, P<const ecg::BnTail>(o[14]));
+                         chunk, P<const ecg::BnTail>(o[14]), P<const uint8_t>(o[15]));
       break;
     }
     case OP_STEM_WGRAD: {
