@@ -29,8 +29,6 @@ i64p = C.POINTER(C.c_int64)
 
 STATUS = {0: "ok", 1: "bad argument", 2: "problem too large for the fused kernel", 3: "HIP runtime error",
           4: "I/O error", 5: "timeout", 6: "end of data"}
-# give-up codes of the persistent TinyECG round kernel (csrc/kernels/tiny_ecg_step.hip)
-ROUND_GIVE_UP = {1: "parameter granules never arrived", 2: "gradient-row granules never arrived"}
 
 
 class NativeError(RuntimeError):
@@ -74,24 +72,14 @@ def _bind_kernels(lib: C.CDLL) -> None:
     _sig(lib, "ecg_tiny_prep", [vp, vp, vp])
     _sig(lib, "ecg_slab_reduce_sgd", [vp, i32, i32, i32, vp, vp, vp, vp, f32, f32, f32, i32, i32, vp, vp])
     _sig(lib, "ecg_tiny_train_step", [vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, vp, f32, f32, f32, i32,
-                                      vp, vp, i32, vp, vp])
+                                      i32, vp, vp])
     _sig(lib, "ecg_round_graph_create", [C.POINTER(vp), vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, i32, vp,
-                                         f32, f32, f32, i32, vp, vp, i32, vp, vp])
-    _sig(lib, "ecg_round_graph_create_part", [C.POINTER(vp), vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, i32,
-                                              vp, f32, f32, f32, i32, vp, i32, i32])
+                                         f32, f32, f32, i32, i32, vp, vp])
     _sig(lib, "ecg_round_graph_create_pf", [C.POINTER(vp), vp, i32, i64, vp, vp, vp, vp, i32, vp, i32, i32, i32,
                                             vp, f32, f32, f32, i32, vp, i32, i32, vp, vp])
     _sig(lib, "ecg_tiny_gather_floats", [i32, i32], i64)
     _sig(lib, "ecg_tiny_step_grads_twice", [vp, i32, i64, vp, vp, vp, i32, vp, i32, i32, f32, i32, vp, vp])
-    _sig(lib, "ecg_tiny_round_ws_bytes", [i32, i32], i64)
-    _sig(lib, "ecg_tiny_round_fits", [i32, i32, i32, i32])
-    _sig(lib, "ecg_tiny_train_round", [vp, i32, i64, vp, vp, vp, vp, i32, i32, i32, vp, f32, f32, f32, i32, vp, i64,
-                                       vp, i32, vp, vp])
-    _sig(lib, "ecg_round_graph_create_persistent", [C.POINTER(vp), vp, i32, i64, vp, vp, vp, vp, i32, i32, i32, vp,
-                                                    f32, f32, f32, i32, vp, i64, vp, i32, vp])
     _sig(lib, "ecg_tiny_force_waves", [i32])
-    _sig(lib, "ecg_tiny_ctl_ints", [])
-    _sig(lib, "ecg_tiny_gslab_rows", [])
     _sig(lib, "ecg_tiny_set_stamps", [vp])
     _sig(lib, "ecg_round_graph_launch", [vp, vp])
     _sig(lib, "ecg_round_graph_destroy", [vp])

@@ -1,17 +1,9 @@
 """Fused TinyECG training / inference on gfx950 (Python side of csrc/kernels/tiny_ecg_step.hip).
 
 Each workgroup computes one sample's forward+backward out of LDS.  ``FusedTinyTrainer`` runs a whole FedAvg
-local round as
-
-* ONE persistent launch (``persistent=True``; needs every workgroup of the batch resident at once): the step
-  loop runs inside the kernel, per-sample gradient rows and the updated parameters move between
-  workgroups as tagged write-through granules, every workgroup owns (reduces + SGD-updates) one column
-  slice of the flat parameters; or
-* two launches per step (gradient slab, then slab reduction + SGD; the default, fastest measured), or one
-  launch per step with an in-kernel reduction tree (``single_launch``),
-
-captured into one native hipGraph and replayed with a single ``hipGraphLaunch`` per round.  All three
-paths sum in a fixed order: the persistent round reproduces the two-launch path bit for bit.
+local round as two launches per step (gradient slab, then slab reduction + SGD), captured into one native hipGraph
+and replayed with a single ``hipGraphLaunch`` per round.  (A one-launch step with an in-kernel reduction tree and a
+persistent one-launch round were measured slower on MI355X and removed in round 5: profiles/r4/tiny_phase_diag.txt.)
 
 Reference semantics per step: Module_3/TRUE_FL_M3/part3_fedavg_overlap_mpi_gpu.py:103-132
 (train_step_G0/G1), batches as Module_3/shard_dataset.py:118-136, optimizer SGD(lr=1e-2, momentum=0.9).
@@ -156,8 +148,7 @@ class FusedTinyTrainer:
     def __init__(self, model: TinyECG, x_gpu: torch.Tensor, y_gpu: torch.Tensor, batch_size: int,
                  steps_per_round: int, lr: float = 1e-2, momentum: float = 0.9, weight_decay: float = 0.0,
                  nesterov: bool = False, seed: Optional[int] = None, use_graph: Optional[bool] = None,
-                 single_launch: bool = False, precision: str = "bf16", persistent: Optional[bool] = None,
-                 prefrag: Optional[bool] = None):
+                 precision: str = "bf16", prefrag: Optional[bool] = None):
         self.device = x_gpu.device
         self.precision = precision
         self.prec = prec_id(precision)
@@ -188,27 +179,14 @@ class FusedTinyTrainer:
         self._graphs = {}  # n_steps -> native hipGraphExec handle
         self.steps_done = 0
         lib = _lib.kernels()
-        # single-launch steps: arrival counters (zero on entry, reset by the kernel) + group partial rows.
-        # Measured on MI355X (profiles/r1_fused_step_v3): the in-kernel write-through reduction tree costs
-        # ~7 us of hand-off latency vs ~5.5 us for slab-reduce kernel + boundary, so two launches is the default.
-        self.single_launch = bool(single_launch)
-        self.ctl = torch.zeros(lib.ecg_tiny_ctl_ints(), dtype=torch.int32, device=self.device)
-        self.gslab = torch.empty((lib.ecg_tiny_gslab_rows(), self.stride), dtype=torch.float32, device=self.device)
         smem = lib.ecg_tiny_smem_bytes(self.x.shape[1], self.prec)
         if smem > 160 * 1024:
             raise ValueError(f"window length {self.x.shape[1]} too long for the fused kernel ({smem} B LDS)")
-        # persistent round: one launch per local round.  Opt-in: measured on MI355X at B=256 it runs 14.7 us/step
-        # against 13.7 for the two-launch graph - its two granule hand-offs per step cost more than the two kernel
-        # boundaries and the reduce launch they replace (profiles/r1_round_kernel/).
-        fits = bool(lib.ecg_tiny_round_fits(self.x.shape[1], self.nc, self.B, self.prec))
-        if persistent and not fits:
-            raise ValueError(f"persistent round needs all {self.B} workgroups resident at once (B <= #CUs)")
-        self.persistent = bool(persistent) and fits and not self.single_launch
         # prepared fragments (two-launch bf16 steps): a round's first step runs on the LDS path (the weights may
         # have been rewritten since: FedAvg, broadcast, checkpoint) and its SGD epilogue rewrites the whole image;
         # every later step of the round reads it
         pf = prefrag_default() if prefrag is None else bool(prefrag)
-        self.prefrag = pf and precision == "bf16" and not self.single_launch and not self.persistent
+        self.prefrag = pf and precision == "bf16"
         self.wprep = new_wprep(self.device) if self.prefrag else None
         self.gather = gather_default() if self.prefrag else False
         self.xg = self.yg = None
@@ -216,10 +194,6 @@ class FusedTinyTrainer:
             self.xg = torch.zeros(lib.ecg_tiny_gather_floats(self.x.shape[1], self.B), dtype=torch.float32,
                                   device=self.device)
             self.yg = torch.zeros(2 * self.B, dtype=torch.int32, device=self.device)
-        self.status = torch.zeros(4, dtype=torch.int32, device=self.device)  # sticky give-up code
-        self.ws = None
-        if self.persistent:
-            self.ws = torch.empty(lib.ecg_tiny_round_ws_bytes(self.nc, self.B), dtype=torch.uint8, device=self.device)
 
     # ------------------------------------------------------------------ graph management
     def _graph_for(self, n: int) -> C.c_void_p:
@@ -232,13 +206,7 @@ class FusedTinyTrainer:
         g = C.c_void_p()
         lib = _lib.kernels()
         torch.cuda.synchronize(self.device)
-        if self.persistent:
-            st = lib.ecg_round_graph_create_persistent(
-                C.byref(g), self.x.data_ptr(), self.x.shape[1], self.x.stride(0), self.idx_table.data_ptr(),
-                self.y32.data_ptr(), self.params.data_ptr(), self.mom.data_ptr(), self.nc, self.B, n,
-                self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd, int(self.nesterov), self.ws.data_ptr(),
-                self.ws.numel(), self.status.data_ptr(), self.prec, self.idx_stage.data_ptr())
-        elif self.prefrag and self.gather:
+        if self.prefrag and self.gather:
             return self._part_graph(n, 0, key)
         else:
             tab, stage = (self.idx_stage, None) if self.prefrag else (self.idx_table, self.idx_stage)
@@ -246,7 +214,7 @@ class FusedTinyTrainer:
                                             tab.data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
                                             self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
                                             n, self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd,
-                                            int(self.nesterov), *self._fuse_ptrs(), self.prec,
+                                            int(self.nesterov), self.prec,
                                             _lib.ptr(stage), _lib.ptr(self.wprep))
         _lib.check(st, "ecg_round_graph_create")
         self._graphs[key] = g
@@ -295,9 +263,6 @@ class FusedTinyTrainer:
             pass
 
     # ------------------------------------------------------------------ execution
-    def _fuse_ptrs(self):
-        return (self.ctl.data_ptr(), self.gslab.data_ptr()) if self.single_launch else (None, None)
-
     def _eager_step(self, s: int):
         lib = _lib.kernels()
         if self.prefrag:
@@ -313,25 +278,9 @@ class FusedTinyTrainer:
                                      self.idx_table[s].data_ptr(), self.y32.data_ptr(), self.params.data_ptr(),
                                      self.mom.data_ptr(), self.nc, self.slab.data_ptr(), self.stride, self.B,
                                      self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd, int(self.nesterov),
-                                     *self._fuse_ptrs(), self.prec, _lib.ptr(self.wprep),
+                                     self.prec, _lib.ptr(self.wprep),
                                      _lib.stream_ptr(self.device))
         _lib.check(st, "ecg_tiny_train_step")
-
-    def _eager_round(self, n: int, stamps: Optional[torch.Tensor] = None):
-        """The persistent round as a direct launch (``stamps``: diagnostic phase clock of step 1)."""
-        lib = _lib.kernels()
-        st = lib.ecg_tiny_train_round(self.x.data_ptr(), self.x.shape[1], self.x.stride(0), self.idx_table.data_ptr(),
-                                      self.y32.data_ptr(), self.params.data_ptr(), self.mom.data_ptr(), self.nc,
-                                      self.B, n, self.loss_acc.data_ptr(), self.lr, self.momentum, self.wd,
-                                      int(self.nesterov), self.ws.data_ptr(), self.ws.numel(), self.status.data_ptr(),
-                                      self.prec, _lib.ptr(stamps), _lib.stream_ptr(self.device))
-        _lib.check(st, "ecg_tiny_train_round")
-
-    def check_status(self) -> None:
-        """Raise if a persistent round gave up (a bounded spin timed out: workgroups not co-resident)."""
-        code = int(self.status[0].item())
-        if code:
-            raise _lib.NativeError(f"persistent TinyECG round gave up: {_lib.ROUND_GIVE_UP.get(code, code)}")
 
     def prepare(self, sizes) -> None:
         """Draw the sampler's first permutation block, then capture, upload and warm every round graph whose step
@@ -342,7 +291,7 @@ class FusedTinyTrainer:
             return
         lib = _lib.kernels()
         sizes = [self._check_n(n) for n in sizes]
-        state = (self.params, self.mom, self.loss_acc, self.idx_stage, self.idx_table, self.status)
+        state = (self.params, self.mom, self.loss_acc, self.idx_stage, self.idx_table)
         snap = [t.clone() for t in state]
         stream = _lib.stream_ptr(self.device)
         for n in sizes:
@@ -408,11 +357,8 @@ class FusedTinyTrainer:
             self._swap_tables()
         else:
             self.idx_table[:n].copy_(self.idx_stage[:n])
-            if self.persistent:
-                self._eager_round(n)
-            else:
-                for s in range(n):
-                    self._eager_step(s)
+            for s in range(n):
+                self._eager_step(s)
         self.steps_done += n
         self._loss_steps = getattr(self, "_loss_steps", 0) + n
         if next_n is not None:
@@ -420,7 +366,6 @@ class FusedTinyTrainer:
 
     def avg_loss(self) -> float:
         """Mean per-step loss since the last reset (synchronises)."""
-        self.check_status()
         return float(self.loss_acc.item()) / (self.B * max(1, getattr(self, "_loss_steps", self.S)))
 
     def reset_momentum(self):

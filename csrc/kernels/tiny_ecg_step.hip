@@ -7,11 +7,10 @@
 //   accumulator layout and used directly as the A operand; h1 read as the B operand with the gfx950
 //   transposing LDS read ds_read_b64_tr_b16)  ->  dconv2 dgrad (MFMA)  ->  ReLU mask  ->  dconv1 wgrad.
 // The sample's parameter gradient (1,458 floats for C=2) plus its loss form one row.  The rows of a step are
-// summed and SGD+momentum is applied to the flat fp32 master weights in one of three ways:
-//   * two launches per step: rows -> slab, then ``slab_reduce_sgd_kernel``; graph-replayed per local round;
-//   * one launch per step: an in-kernel last-arriver reduction tree (``FusedOpt``);
-//   * one launch per local ROUND (``tiny_ecg_round_kernel``, the default whenever the batch's workgroups fit
-//     on the device at once): see the comment above that kernel.
+// summed and SGD+momentum is applied to the flat fp32 master weights by a second launch
+// (``slab_reduce_sgd_kernel``); a local round's launches are captured into one hipGraph and replayed.
+// (One launch per step with an in-kernel last-arriver reduction tree and one persistent launch per round were
+// measured slower - 13.23 and 16.33 vs 10.62 us/step, profiles/r4/tiny_phase_diag.txt - and were removed in round 5.)
 //
 // Reference semantics being reproduced (per step): Module_3/TRUE_FL_M3/part3_fedavg_overlap_mpi_gpu.py:103-132
 // (train_step_G0/G1: fwd, cross_entropy(mean), backward, SGD(lr=1e-2, momentum=0.9).step()) on the
@@ -59,26 +58,11 @@ struct Smem {
 // (deterministic; no LDS float atomics).
 constexpr int RED_G = 0;       // [16] dL/dh2 scale per channel (dpooled / L), written by the head
 constexpr int RED_POOLED = 16; // [16] pooled features
-constexpr int RED_FLAG = 32;   // [16] broadcast slot for the last-arriver decision (ints)
 constexpr int RED_POOL = 48;   // [WAVES][16] pooled partials
 
-// In-kernel cross-sample reduction + SGD (one launch per training step).  Deterministic two-level
-// last-arriver tree: the G per-sample rows are summed by NG <= 16 group reducers (group g = b % NG, i.e.
-// one XCD-affine group under round-robin dispatch; correctness never depends on placement), then by the
-// last group reducer, which applies SGD.  Publication follows the agent-scope release -> ticket ->
-// acquire protocol; counters are zero on entry and reset by the final reducer.
-constexpr int kMaxGroups = 16;
+// Per-launch options of the step kernel.
 struct FusedOpt {
-  int* ctl;          // [kMaxGroups + 1] arrival counters (nullptr: no in-kernel reduction, slab only)
-  float* gslab;      // [kMaxGroups][out_stride] group partial rows
-  float* params;     // flat fp32 params updated in place by the final reducer
-  float* mom;        // momentum buffer
-  float* loss_acc;   // += sum of per-sample losses
-  float lr, momentum, wd;
-  int nesterov;
-  int G;             // number of workgroups (= batch)
-  int slab_wt;       // two-launch path: store the gradient rows write-through (ECG_TINY_SLAB_WT, default on)
-  const int* idx_next;  // next step's batch rows: touch this sample's next window on the way out (L2/MALL warm-up)
+  int slab_wt;  // store the gradient rows write-through (sc1): they leave the XCD L2s while the step runs
 };
 // conv2 wgrad work split: 5 taps x msplit(WAVES) pair ranges, one (tap, range) per wave 1.. (wave 0 runs the head)
 __host__ __device__ constexpr int msplit(int waves) { return (waves - 1) / 5 < 1 ? 1 : (waves - 1) / 5; }
@@ -220,7 +204,7 @@ __device__ __forceinline__ float row16_sum(float v) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// The per-sample computation (phases 0-5), shared by the per-step kernel and the persistent round kernel.
+// The per-sample computation (phases 0-5) of the per-step kernel.
 //
 // Backward algebra used (h2 = relu(conv2(h1)), pooled = mean_t h2, g[co] = dL/dpooled[co] / L):
 //   dh2[t][co]       = g[co] * m[t][co]          with m = relu'(h2) in {0, 1} (exact in bf16)
@@ -299,8 +283,8 @@ struct TinySample {
   }
 
   // ---- phase 0: window, parameters, constant pads
-  // The window goes global -> registers (load_x) -> LDS (put_x), so the persistent round can issue the loads of
-  // the next step's window early: xs elements i = tid + k*NT, one coalesced load each.
+  // The window goes global -> registers (load_x) -> LDS (put_x): xs elements i = tid + k*NT, one coalesced load
+  // each.
   static constexpr int XK = (32 * MAX_PAIRS_PER_WAVE * WAVES + 16 + NT - 1) / NT;
   struct XRegs {
     float v[XK];
@@ -1027,11 +1011,10 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     S.dgrad();
     __syncthreads();
     ECG_STAMP(5)
-    // phase 5: combine partials, scale by g, write this sample's gradient row.  The single-launch reduction
-    // below reads it inside this launch (write-through stores); otherwise the kernel boundary publishes it.
-    if (WAVES == 16 && opt.ctl == nullptr && opt.slab_wt && S.lay.P - S.lay.b2 + 1 <= S.NT - 448) {
+    // phase 5: combine partials, scale by g, write this sample's gradient row (published by the kernel boundary).
+    if (WAVES == 16 && opt.slab_wt && S.lay.P - S.lay.b2 + 1 <= S.NT - 448) {
       S.row_store(slab_r, rowbase);
-    } else if (opt.ctl != nullptr || opt.slab_wt) {
+    } else if (opt.slab_wt) {
       for (int i = tid; i <= S.lay.P; i += S.NT) st_wt(slab_r, rowbase + i, S.row_value(i));
     } else {
       for (int i = tid; i <= S.lay.P; i += S.NT) out[rowbase + i] = S.row_value(i);
@@ -1041,116 +1024,6 @@ __global__ __launch_bounds__(WAVES * 64) void tiny_ecg_step_kernel(
     if (MODE == 2) __syncthreads();  // the second pass reuses the LDS
   }
   if (stamps && tid == 0) stamps[(long)b * 16 + 14] = __builtin_amdgcn_s_memrealtime();
-  if (MODE == 0 && opt.idx_next != nullptr) {
-    // Fire-and-forget loads of the next step's window (one dword per 64-byte line) so the next launch's phase 0
-    // finds it in cache: nothing waits for them (the values are unused), the workgroup just retires.
-    const long row = opt.idx_next[b];
-    const int i = tid * 16;
-    if (i < L) (void)*reinterpret_cast<const volatile float*>(X + row * ldx + i);
-  }
-  if (MODE == 0 && opt.ctl != nullptr) {
-    // ---------------- phase 6: two-level deterministic cross-sample reduction + SGD --------------
-    const Layout& lay = S.lay;
-    int* flag = reinterpret_cast<int*>(S.red + RED_FLAG);
-    const int G = opt.G;
-    const int NG = G < kMaxGroups ? G : kMaxGroups;
-    const int g = b % NG;
-    const int members = (G - 1 - g) / NG + 1;  // rows b' < G with b' % NG == g
-    const int ncols = lay.P + 1;               // gradient + loss column
-    // Hand-off protocol (guide Guideline 16, R1 form): rows are stored write-through (sc1) by every
-    // wave and drained (vmcnt(0)) before the barrier; ONE lane then takes a relaxed agent-scope ticket.
-    // Reducers read the handed-off rows ONLY with sc1 loads, so neither a release nor an acquire fence
-    // (each ~1-2 us at agent scope) is needed.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const int t = __hip_atomic_fetch_add(&opt.ctl[g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      flag[0] = (t == members - 1);
-    }
-    __syncthreads();
-    if (!flag[0]) return;
-    // group reducer: sum the group's rows in a fixed order (bitwise reproducible)
-    const __amdgpu_buffer_rsrc_t g_r = make_rsrc(opt.gslab, (long)kMaxGroups * out_stride * 4);
-    // (no per-element "load or zero" selects inside the unrolled block: hipcc would serialise them)
-    constexpr int NT = WAVES * 64;
-    constexpr int CPT = (1 + C * K1 + C + C * C * K2 + C + MAX_CLASSES * C + MAX_CLASSES + NT - 1) / NT;
-    if (members == 16) {
-      // fast path (B = 256): every thread issues all CPT x 16 row loads before the first add -> one round trip
-      float v[CPT][16];
-#pragma unroll
-      for (int cc = 0; cc < CPT; ++cc) {
-        const int col = min(tid + cc * NT, ncols - 1);  // clamped: no branches around the loads
-#pragma unroll
-        for (int u = 0; u < 16; ++u) v[cc][u] = ld_wt(slab_r, (g + u * NG) * out_stride + col);
-      }
-#pragma unroll
-      for (int cc = 0; cc < CPT; ++cc) {
-        float sum = 0.f;
-#pragma unroll
-        for (int u = 0; u < 16; u += 2) sum += v[cc][u] + v[cc][u + 1];
-        if (tid + cc * NT < ncols) st_wt(g_r, g * out_stride + tid + cc * NT, sum);
-      }
-    }
-    for (int i = members == 16 ? ncols : tid; i < ncols; i += WAVES * 64) {
-      float sum = 0.f;
-      int m = 0;
-      for (; m + 8 <= members; m += 8) {
-        float v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = ld_wt(slab_r, (g + (m + u) * NG) * out_stride + i);
-        sum += ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
-      }
-      for (; m < members; ++m) sum += ld_wt(slab_r, (g + m * NG) * out_stride + i);
-      st_wt(g_r, g * out_stride + i, sum);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const int t = __hip_atomic_fetch_add(&opt.ctl[kMaxGroups], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      flag[1] = (t == NG - 1);
-    }
-    __syncthreads();
-    if (!flag[1]) return;
-    // final reducer: sum the NG group rows, SGD(+momentum) on the flat master weights, reset counters
-    float gv[CPT][kMaxGroups];
-    if (NG == kMaxGroups) {
-#pragma unroll
-      for (int cc = 0; cc < CPT; ++cc) {
-        const int col = min(tid + cc * NT, ncols - 1);
-#pragma unroll
-        for (int u = 0; u < kMaxGroups; ++u) gv[cc][u] = ld_wt(g_r, u * out_stride + col);
-      }
-    }
-#pragma unroll
-    for (int cc = 0; cc < CPT; ++cc) {
-      const int i = tid + cc * NT;
-      if (i >= ncols) continue;
-      float sum = 0.f;
-      if (NG == kMaxGroups) {
-#pragma unroll
-        for (int u = 0; u < kMaxGroups; u += 2) sum += gv[cc][u] + gv[cc][u + 1];
-      } else {
-        for (int m = 0; m < NG; ++m) sum += ld_wt(g_r, m * out_stride + i);
-      }
-      if (i == lay.P) {
-        if (opt.loss_acc) opt.loss_acc[0] += sum;
-      } else {
-        const float p = opt.params[i];
-        float d = sum + opt.wd * p;
-        if (opt.momentum != 0.f) {
-          const float bm = opt.momentum * opt.mom[i] + d;
-          opt.mom[i] = bm;
-          d = opt.nesterov ? d + opt.momentum * bm : bm;
-        }
-        opt.params[i] = p - opt.lr * d;
-      }
-    }
-    if (tid <= kMaxGroups) __hip_atomic_store(&opt.ctl[tid], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (stamps && tid == 0) {
-      stamps[(long)b * 16 + 7] = __builtin_amdgcn_s_memtime();
-      stamps[(long)b * 16 + 13] = __builtin_amdgcn_s_memrealtime();
-    }
-  }
 }
 
 // Sum the per-sample gradient rows and apply SGD (+momentum, weight decay, nesterov) in place.
@@ -1257,233 +1130,6 @@ __global__ __launch_bounds__(RED_COLS * RED_ROWG) void slab_reduce_sgd_kernel(
   }
 }
 
-// ------------------------------------------------------------------------------------------------------------
-// Persistent round: ONE launch runs ``steps`` training steps of one FedAvg client, B workgroups (one per
-// sample of a step) that are all resident at once (the host takes this path only when B <= #CUs).
-//   * A step's code runs with warm instruction / scalar caches: a fresh launch pays the cold fetch of the
-//     whole step body again in every phase (scripts/diag_step_phases.py: cold vs warm passes).
-//   * Per step, workgroup b publishes its gradient row as {tag = step + 1, value} 8-byte granules (MI355X
-//     guide, Guideline 16 R2: the data is the flag; two granules per 16-byte write-through store).  It then
-//     OWNS the column slice [b*cw, b*cw + cw): it sweeps those granules of all B rows until every tag
-//     matches, sums each column in exactly the order of slab_reduce_sgd_kernel (so parameters, momentum and
-//     loss are bitwise those of the two-launch path), applies SGD to its slice (the authoritative parameter
-//     and momentum values of the slice stay in its LDS for the whole round) and publishes the new parameters
-//     as granules.  Every workgroup sweeps the parameter granules before its next step.  No counters, no
-//     fences, no grid barrier: two one-hop hand-offs per step.
-//   * The next step's window and label are loaded into registers before the exchange and land under it.
-//   * Every spin is bounded: after kSpinTicks the workgroup records a give-up code in ``status`` (sticky,
-//     read by the host) and leaves; its peers then time out too, so the launch always drains.
-//   * Tags are zeroed by a memset of the granule workspace before every launch (a memset node in the
-//     captured round graph); the slice owners write params / momentum / loss back when the round ends.
-typedef unsigned long long u64;
-typedef __attribute__((address_space(1))) u64 gu64;
-typedef __attribute__((address_space(1))) int gi32;
-
-constexpr unsigned long long kSpinTicks = 50000000ull;  // 0.5 s of s_memrealtime (100 MHz); a round takes ~1 ms
-constexpr int kGiveUpParams = 1, kGiveUpRows = 2;
-
-struct RoundArgs {
-  const float* X;
-  long ldx;
-  const int* idx_table;  // [steps][G] dataset rows of every step
-  const int* Y;          // [N] int32 labels
-  float* params;         // flat fp32 master weights: read at entry, each slice written back by its owner
-  float* mom;            // momentum (nullptr when momentum == 0)
-  float* loss_acc;       // += sum over the round's samples of the loss
-  u64* rowg;             // [G][gstride] gradient-row granules
-  u64* parg;             // [gstride] parameter granules
-  int* status;           // [0]: sticky give-up code (0 = ok)
-  unsigned long long* stamps;  // diagnostic: phase clock of step 1 (warm), [G][16]; nullptr = off
-  int L, nc, G, steps, gstride;
-  float inv_B, lr, momentum, wd;
-  int nesterov;
-};
-
-__host__ __device__ inline int round_gstride(int nc) { return (make_layout(nc).P + 1 + 15) / 16 * 16; }
-__host__ __device__ inline int round_cols(int nc, int G) { return (make_layout(nc).P + 1 + G - 1) / G; }
-// extra LDS of the round kernel: vals [cw][G], part [cw][16], own params [cw], own momentum [cw], give-up flag
-__host__ __device__ inline int round_ext_bytes(int nc, int G) {
-  const int cw = round_cols(nc, G);
-  return ((G * cw + cw * 16 + 2 * cw + 4) * 4 + 15) / 16 * 16;
-}
-inline long round_ws_bytes(int nc, int G) { return ((long)G + 1) * round_gstride(nc) * 8; }
-
-__device__ __forceinline__ u64 get_granule(const u64* g) {
-  return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void put_granule(u64* g, unsigned tag, float v) {
-  __hip_atomic_store((gu64*)g, ((u64)tag << 32) | __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Sweep granules at(e), e = tid + k*NT (clamped to n-1, so no branch around a load), until every tag equals
-// ``tag``; the values land in v[k].  Wave-uniform result; false when the spin ran out of time.
-template <int NT, int KMAX, typename At>
-__device__ __forceinline__ bool sweep(At at, int n, unsigned tag, float (&v)[KMAX], unsigned long long t0) {
-  const int tid = threadIdx.x;
-  for (int spins = 0;; ++spins) {
-    bool ok = true;
-#pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      const u64 x = get_granule(at(min(tid + k * NT, n - 1)));
-      v[k] = __builtin_bit_cast(float, (unsigned)x);
-      ok = ok && (unsigned)(x >> 32) == tag;
-    }
-    if (__all(ok)) return true;
-    if ((spins & 31) == 31 && __builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) return false;
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-template <int WAVES, bool F32>
-__global__ __launch_bounds__(WAVES * 64) void tiny_ecg_round_kernel(RoundArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  using TS = TinySample<WAVES, F32>;
-  constexpr int NT = TS::NT;
-  constexpr int KMAX = (2048 + NT - 1) / NT;                                 // granules per thread per sweep
-  TS S(smem, a.L, a.nc);
-  const int tid = threadIdx.x, b = blockIdx.x, G = a.G;
-  const int P = S.lay.P, ncols = P + 1;
-  const int cw0 = round_cols(a.nc, G);
-  const int col0 = min(ncols, b * cw0), cw = min(ncols, col0 + cw0) - col0;  // owned columns (may be 0)
-  float* vals = reinterpret_cast<float*>(smem + S.sm.bytes);  // [cw0][G] owned columns of every row
-  float* part = vals + G * cw0;                                // [cw0][16] ordered partial sums
-  float* ownp = part + cw0 * 16;                               // [cw0] owned parameters (loss sum for col P)
-  float* ownm = ownp + cw0;                                    // [cw0] owned momentum
-  int* gflag = reinterpret_cast<int*>(ownm + cw0);             // [0]: give-up code of this workgroup
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  const __amdgpu_buffer_rsrc_t row_r = make_rsrc(a.rowg, (long)G * a.gstride * 8);
-
-  S.zero_pads();
-  for (int i = tid; i < cw; i += NT) {
-    const int col = col0 + i;
-    ownp[i] = col < P ? a.params[col] : a.loss_acc[0];
-    ownm[i] = (col < P && a.mom) ? a.mom[col] : 0.f;
-  }
-  if (tid == 0) gflag[0] = 0;
-
-  typename TS::XRegs xr;
-  int ynext = 0;
-  auto prefetch = [&](int s) {  // window + label of step s into registers
-    const long row = a.idx_table[(long)s * G + b];
-    ynext = a.Y[row];
-    S.load_x(a.X + row * a.ldx, xr);
-  };
-  auto give_up = [&]() -> bool {  // block-uniform after a barrier
-    if (gflag[0] == 0) return false;
-    if (tid == 0) __hip_atomic_store((gi32*)a.status, gflag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return true;
-  };
-  prefetch(0);
-  for (int s = 0; s < a.steps; ++s) {
-    const bool stamp = a.stamps != nullptr && s == 1 && tid == 0;
-#define ECG_RSTAMP(k) \
-  if (stamp) a.stamps[(long)b * 16 + (k)] = __builtin_amdgcn_s_memtime();
-    ECG_RSTAMP(0)
-    // ---- parameters of this step: the launch's input (step 0) or the granules the slice owners published
-    if (s == 0) {
-      for (int i = tid; i < P; i += NT) S.put_param(i, a.params[i]);
-    } else {
-      float v[KMAX];
-      if (!sweep<NT, KMAX>([&](int e) { return a.parg + e; }, P, (unsigned)s, v, t0)) gflag[0] = kGiveUpParams;
-#pragma unroll
-      for (int k = 0; k < KMAX; ++k) {
-        const int i = tid + k * NT;
-        if (i < P) S.put_param(i, v[k]);
-      }
-    }
-    S.put_x(xr);
-    const int ylab = ynext;
-    __syncthreads();
-    if (give_up()) return;
-    ECG_RSTAMP(1)
-    S.conv1();
-    __syncthreads();
-    ECG_RSTAMP(2)
-    S.conv2();
-    __syncthreads();
-    ECG_RSTAMP(3)
-    S.template head_and_M<true>(ylab, a.inv_B, nullptr, 0, b);
-    __syncthreads();
-    ECG_RSTAMP(4)
-    S.dgrad();
-    if (s + 1 < a.steps) prefetch(s + 1);  // lands under the exchange below
-    __syncthreads();
-    ECG_RSTAMP(5)
-    // ---- publish this sample's gradient row: granules {s+1, value}, two per 16-byte write-through store
-    for (int p = tid; 2 * p < ncols; p += NT) {
-      const int i = 2 * p;
-      const float v0 = S.row_value(i), v1 = i + 1 < ncols ? S.row_value(i + 1) : 0.f;
-      typedef int i32x4 __attribute__((ext_vector_type(4)));
-      const i32x4 q = {__builtin_bit_cast(int, v0), s + 1, __builtin_bit_cast(int, v1), s + 1};
-      __builtin_amdgcn_raw_buffer_store_b128(q, row_r, (b * a.gstride + i) * 8, 0, 16);
-    }
-    // ---- gather the owned columns of every row
-    const int n = G * cw;
-    if (n > 0) {  // block-uniform
-      float v[KMAX];
-      auto at = [&](int e) { return a.rowg + (long)(e / cw) * a.gstride + col0 + e % cw; };
-      if (!sweep<NT, KMAX>(at, n, (unsigned)(s + 1), v, t0)) gflag[0] = kGiveUpRows;
-#pragma unroll
-      for (int k = 0; k < KMAX; ++k) {
-        const int e = tid + k * NT;
-        if (e < n) vals[(e % cw) * G + e / cw] = v[k];
-      }
-    }
-    __syncthreads();
-    if (give_up()) return;
-    ECG_RSTAMP(6)
-    // ---- column sums in slab_reduce_sgd_kernel's order: 16 row groups (rows rg, rg+16, ... in chunks of 16,
-    // pairwise), then the 16 group sums in order
-    for (int q = tid; q < cw * 16; q += NT) {
-      const int cl = q >> 4, rg = q & 15;
-      const float* colv = vals + cl * G;
-      float acc = 0.f;
-      int r = rg;
-      for (; r + 16 * 15 < G; r += 16 * 16) {
-#pragma unroll
-        for (int j = 0; j < 16; j += 2) acc += colv[r + 16 * j] + colv[r + 16 * (j + 1)];
-      }
-      for (; r < G; r += 16) acc += colv[r];
-      part[q] = acc;
-    }
-    __syncthreads();
-    // ---- SGD on the owned slice, publish the new parameters for the next step
-    for (int cl = tid; cl < cw; cl += NT) {
-      float gsum = 0.f;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) gsum += part[cl * 16 + j];
-      const int col = col0 + cl;
-      if (col == P) {
-        ownp[cl] += gsum;  // the round's loss sum (loss_acc)
-      } else {
-        const float p = ownp[cl];
-        float d = gsum + a.wd * p;
-        if (a.momentum != 0.f) {
-          const float bm = a.momentum * ownm[cl] + d;
-          ownm[cl] = bm;
-          d = a.nesterov ? d + a.momentum * bm : bm;
-        }
-        const float pn = p - a.lr * d;
-        ownp[cl] = pn;
-        if (s + 1 < a.steps) put_granule(a.parg + col, (unsigned)(s + 1), pn);
-      }
-    }
-    ECG_RSTAMP(7)
-#undef ECG_RSTAMP
-  }
-  // ---- the round's result: each owner writes back its slice (same thread that updated it)
-  for (int cl = tid; cl < cw; cl += NT) {
-    const int col = col0 + cl;
-    if (col < P) {
-      a.params[col] = ownp[cl];
-      if (a.mom) a.mom[col] = ownm[cl];
-    } else {
-      a.loss_acc[0] = ownp[cl];
-    }
-  }
-}
-
 unsigned long long* g_stamps = nullptr;  // diagnostic phase stamps (ecg_tiny_set_stamps)
 
 
@@ -1565,8 +1211,7 @@ int step_dispatch(int mode, int prec, const float* X, int L, long ldx, const int
   if (prec != 0 && prec != 1) return ecg::kBadArg;
   int st = check_step_args(L, nc, B, out_stride, mode, prec == 1);
   if (st) return st;
-  if (opt.ctl && (!opt.gslab || !opt.params || (opt.momentum != 0.f && !opt.mom) || opt.G != B)) return ecg::kBadArg;
-  if (wprep && (prec == 1 || opt.ctl)) return ecg::kBadArg;
+  if (wprep && prec == 1) return ecg::kBadArg;
   const int waves = pick_waves(L, prec == 1);
   if (prec == 1)
     return dispatch_cfg<true, false>(mode, waves, X, L, ldx, idx, Y, params, nc, out, out_stride, B, inv_B, opt,
@@ -1609,90 +1254,6 @@ int reduce_dispatch(const float* slab, int G, int stride, int P, float* params, 
   return ecg::kOk;
 }
 
-// ---- persistent round: residency check and launch
-template <int WAVES, bool F32>
-int round_smem(int L, int nc, int G) {
-  return make_smem(L, WAVES, nc, F32).bytes + round_ext_bytes(nc, G);
-}
-
-template <int WAVES, bool F32>
-bool round_fits_cfg(int L, int nc, int G) {
-  const int smem = round_smem<WAVES, F32>(L, nc, G);
-  if (smem > kMaxLds) return false;
-  auto kern = tiny_ecg_round_kernel<WAVES, F32>;
-  if (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)
-    return false;
-  int dev = 0, cus = 0, per_cu = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, WAVES * 64, smem) != hipSuccess)
-    return false;
-  // The protocol needs every workgroup resident at once.  The occupancy answer can be one block per CU too
-  // high (MI355X guide, residency), so only grids of at most one workgroup per CU take this path.
-  return per_cu >= 1 && G <= cus;
-}
-
-// The persistent round keeps 8 waves in bf16 (14.0 vs 18.5 us/step at 16: its per-step hand-offs are spun on
-// by every wave, profiles/r1_round_kernel/diag_*).
-int round_waves(int L, bool f32) { return f32 ? pick_waves(L, true) : 8; }
-
-bool round_fits(int L, int nc, int G, bool f32) {
-  if (check_step_args(L, nc, G, make_layout(nc).P + 1, 0, f32) != ecg::kOk) return false;
-  const int waves = round_waves(L, f32);
-  if (f32) return waves == 8 ? round_fits_cfg<8, true>(L, nc, G) : round_fits_cfg<16, true>(L, nc, G);
-  return waves == 8 ? round_fits_cfg<8, false>(L, nc, G) : round_fits_cfg<16, false>(L, nc, G);
-}
-
-template <int WAVES, bool F32>
-int launch_round_cfg(const RoundArgs& a, hipStream_t stream) {
-  const int smem = round_smem<WAVES, F32>(a.L, a.nc, a.G);
-  auto kern = tiny_ecg_round_kernel<WAVES, F32>;
-  ECG_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
-  hipLaunchKernelGGL(kern, dim3(a.G), dim3(WAVES * 64), smem, stream, a);
-  ECG_HIP_CHECK(hipGetLastError());
-  return ecg::kOk;
-}
-
-// memset of the granule tags + the round kernel (both captured when called under stream capture)
-int round_dispatch(const RoundArgs& a, void* ws, long ws_bytes, int prec, hipStream_t stream) {
-  if (prec != 0 && prec != 1) return ecg::kBadArg;
-  if (!ws || !a.status || !a.loss_acc || !a.params || (a.momentum != 0.f && !a.mom) || a.steps <= 0)
-    return ecg::kBadArg;
-  if (ws_bytes < round_ws_bytes(a.nc, a.G) || !round_fits(a.L, a.nc, a.G, prec == 1)) return ecg::kBadArg;
-  ECG_HIP_CHECK(hipMemsetAsync(ws, 0, round_ws_bytes(a.nc, a.G), stream));
-  const int waves = round_waves(a.L, prec == 1);
-  if (prec == 1) return waves == 8 ? launch_round_cfg<8, true>(a, stream) : launch_round_cfg<16, true>(a, stream);
-  return waves == 8 ? launch_round_cfg<8, false>(a, stream) : launch_round_cfg<16, false>(a, stream);
-}
-
-RoundArgs make_round_args(const float* X, int L, long ldx, const int* idx_table, const int* Y, float* params,
-                          float* mom, int nc, int B, int steps, float* loss_acc, float lr, float momentum, float wd,
-                          int nesterov, void* ws, int* status, unsigned long long* stamps) {
-  RoundArgs a{};
-  a.X = X;
-  a.ldx = ldx;
-  a.idx_table = idx_table;
-  a.Y = Y;
-  a.params = params;
-  a.mom = mom;
-  a.loss_acc = loss_acc;
-  a.gstride = round_gstride(nc);
-  a.rowg = static_cast<u64*>(ws);
-  a.parg = a.rowg + (long)B * a.gstride;
-  a.status = status;
-  a.stamps = stamps;
-  a.L = L;
-  a.nc = nc;
-  a.G = B;
-  a.steps = steps;
-  a.inv_B = 1.0f / (float)B;
-  a.lr = lr;
-  a.momentum = momentum;
-  a.wd = wd;
-  a.nesterov = nesterov;
-  return a;
-}
-
 struct RoundGraph {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
@@ -1705,7 +1266,7 @@ struct RoundGraph {
 ECG_API int ecg_tiny_param_count(int nc) { return make_layout(nc).P; }
 
 // Diagnostic: when set, every fused-step workgroup b writes s_memtime at each phase boundary to
-// stamps[b*16 + k] (k = 0..6; MODE 2's second pass: 7..13; single-launch final reducer: 7) and
+// stamps[b*16 + k] (k = 0..6; MODE 2's second pass: 7..13) and
 // s_memrealtime at entry/exit to [b*16+15] / [b*16+14].
 ECG_API int ecg_tiny_set_stamps(unsigned long long* stamps) {
   g_stamps = stamps;
@@ -1768,11 +1329,6 @@ ECG_API int ecg_tiny_forward(const float* X, int L, long ldx, const int* idx, co
   return prep_then(1, prec, X, L, ldx, idx, nullptr, params, nc, logits, nc, B, 0.f, wprep, stream);
 }
 
-// Size of the control block (int32 counters, must be zero before the first fused step) and of the
-// group-partial buffer (floats) needed by the single-launch step.
-ECG_API int ecg_tiny_ctl_ints(void) { return kMaxGroups + 1; }
-ECG_API int ecg_tiny_gslab_rows(void) { return kMaxGroups; }
-
 ECG_API int ecg_slab_reduce_sgd(const float* slab, int G, int stride, int P, float* params, float* mom,
                                 float* grad_out, float* loss_acc, float lr, float momentum, float wd, int nesterov,
                                 int apply, void* wprep, hipStream_t stream) {
@@ -1787,22 +1343,14 @@ ECG_API int ecg_slab_reduce_sgd(const float* slab, int G, int stride, int P, flo
 // zero-initialised allocation), which is how a round starts without a prep launch.
 static int train_step(const float* X, int L, long ldx, const int* idx, const int* Y, float* params, float* mom,
                       int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr, float momentum, float wd,
-                      int nesterov, int* ctl, float* gslab, int prec, unsigned char* wprep, int image,
-                      hipStream_t stream, const int* idx_next = nullptr, const GatherArgs* gather = nullptr) {
-  if (ctl) {
-    if (wprep) return ecg::kBadArg;
-    FusedOpt o{ctl, gslab, params, mom, loss_acc, lr, momentum, wd, nesterov, B};
-    return step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, o, nullptr,
-                         stream);
-  }
+                      int nesterov, int prec, unsigned char* wprep, int image, hipStream_t stream,
+                      const GatherArgs* gather = nullptr) {
   int st = ecg::kOk;
   if (wprep && image == 0) st = launch_prep(params, wprep, nullptr, nullptr, 0, stream);
   if (st) return st;
   FusedOpt o = no_fuse();
   // (Warm-up loads of the next step's windows in the step kernel's tail measured neutral - 11.11 vs 11.08 us/step,
   // the windows already sit in the Infinity Cache; profiles/r2/bench_prefetch.txt - and were removed.)
-  (void)idx_next;
-  o.idx_next = nullptr;
   st = step_dispatch(0, prec, X, L, ldx, idx, Y, params, nc, slab, slab_stride, B, 1.0f / (float)B, o,
                      image == 2 ? nullptr : wprep, stream);
   if (st) return st;
@@ -1810,15 +1358,13 @@ static int train_step(const float* X, int L, long ldx, const int* idx, const int
                          nesterov, 1, wprep, stream, gather);
 }
 
-// Full training step.  With ``ctl``/``gslab`` (see ecg_tiny_ctl_ints) it is ONE launch: per-sample
-// gradients, the in-kernel deterministic reduction tree and SGD.  Without them it is two launches
-// (gradient slab, then slab_reduce_sgd_kernel) - three with ``wprep`` (the PF image is rebuilt first).
+// Full training step: two launches (gradient slab, then slab_reduce_sgd_kernel) - three with ``wprep`` (the PF
+// image is rebuilt first).
 ECG_API int ecg_tiny_train_step(const float* X, int L, long ldx, const int* idx, const int* Y, float* params,
                                 float* mom, int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr,
-                                float momentum, float wd, int nesterov, int* ctl, float* gslab, int prec, void* wprep,
-                                hipStream_t stream) {
+                                float momentum, float wd, int nesterov, int prec, void* wprep, hipStream_t stream) {
   return train_step(X, L, ldx, idx, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr, momentum, wd, nesterov,
-                    ctl, gslab, prec, static_cast<unsigned char*>(wprep), 0, stream);
+                    prec, static_cast<unsigned char*>(wprep), 0, stream);
 }
 
 // Two-launch training step that keeps a zero-initialised PF image current without prep launches: ``image_current``
@@ -1830,7 +1376,7 @@ ECG_API int ecg_tiny_train_step_pf(const float* X, int L, long ldx, const int* i
                                    hipStream_t stream) {
   if (!wprep) return ecg::kBadArg;
   return train_step(X, L, ldx, idx, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr, momentum, wd, nesterov,
-                    nullptr, nullptr, 0, static_cast<unsigned char*>(wprep), image_current ? 1 : 2, stream);
+                    0, static_cast<unsigned char*>(wprep), image_current ? 1 : 2, stream);
 }
 
 // ``steps`` two-launch PF steps (batch s reads idx_table + s*B) enqueued directly from C++: the same kernels and
@@ -1843,34 +1389,14 @@ ECG_API int ecg_tiny_train_steps_pf(const float* X, int L, long ldx, const int* 
   int st = ecg::kOk;
   for (int s = 0; s < steps && st == 0; ++s)
     st = train_step(X, L, ldx, idx_table + (long)s * B, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr,
-                    momentum, wd, nesterov, nullptr, nullptr, 0, static_cast<unsigned char*>(wprep),
-                    (s > 0 || image_current) ? 1 : 2, stream,
-                    s + 1 < steps ? idx_table + (long)(s + 1) * B : nullptr);
+                    momentum, wd, nesterov, 0, static_cast<unsigned char*>(wprep), (s > 0 || image_current) ? 1 : 2,
+                    stream);
   return st;
 }
 
-// ---- persistent round (tiny_ecg_round_kernel)
-// Bytes of the granule workspace (tags zeroed by the launcher before every launch).
-ECG_API long ecg_tiny_round_ws_bytes(int nc, int B) { return round_ws_bytes(nc, B); }
-
-// 1 when a round of batch B can run as one persistent launch on the current device (every workgroup resident).
-ECG_API int ecg_tiny_round_fits(int L, int nc, int B, int prec) { return round_fits(L, nc, B, prec == 1) ? 1 : 0; }
-
-// ``steps`` training steps (batch s reads idx_table + s*B) as ONE launch (+ the workspace memset).  ``status``
-// (int32, zero-initialised by the caller) receives a sticky non-zero code if a bounded spin gave up.
-ECG_API int ecg_tiny_train_round(const float* X, int L, long ldx, const int* idx_table, const int* Y, float* params,
-                                 float* mom, int nc, int B, int steps, float* loss_acc, float lr, float momentum,
-                                 float wd, int nesterov, void* ws, long ws_bytes, int* status, int prec,
-                                 unsigned long long* stamps, hipStream_t stream) {
-  const RoundArgs a = make_round_args(X, L, ldx, idx_table, Y, params, mom, nc, B, steps, loss_acc, lr, momentum, wd,
-                                      nesterov, ws, status, stamps);
-  return round_dispatch(a, ws, ws_bytes, prec, stream);
-}
-
-static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws, long ws_bytes, int prec,
-                         const float* X, int L, long ldx, const int* idx_table, const int* Y, float* params,
-                         float* mom, int nc, float* slab, int slab_stride, int B, float* loss_acc, float lr,
-                         float momentum, float wd, int nesterov, int* ctl, float* gslab, const int* idx_stage,
+static int capture_round(void** handle, int steps, int prec, const float* X, int L, long ldx, const int* idx_table,
+                         const int* Y, float* params, float* mom, int nc, float* slab, int slab_stride, int B,
+                         float* loss_acc, float lr, float momentum, float wd, int nesterov, const int* idx_stage,
                          unsigned char* wprep, int step_offset = 0, int image_current = 0, float* xg = nullptr,
                          int* yg = nullptr) {
   hipStream_t cap;
@@ -1895,10 +1421,7 @@ static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws
                                          hipMemcpyDeviceToDevice, cap) != hipSuccess) {
     st = ecg::kHipError;
   }
-  if (st) {
-  } else if (pa) {
-    st = round_dispatch(*pa, ws, ws_bytes, prec, cap);
-  } else {
+  if (st == 0) {
     // Gathered steps (xg/yg): step s > 0 reads ping-pong buffer s & 1, which the reduce launch of step s - 1 filled
     // (stream order: that buffer's previous reader, step s - 2's kernel, finished before that reduce started).
     const int ldg = (L + 3) / 4 * 4;
@@ -1915,9 +1438,8 @@ static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws
       }
       st = train_step(gathered ? xg + (long)(s & 1) * B * ldg : X, L, gathered ? (long)ldg : ldx,
                       gathered ? nullptr : tab + row, gathered ? yg + (long)(s & 1) * B : Y, params, mom, nc, slab,
-                      slab_stride, B, loss_acc, lr, momentum, wd, nesterov, ctl, gslab, prec, wprep,
-                      (s == 0 && !image_current) ? 2 : 1, cap, s + 1 < steps ? tab + row + B : nullptr,
-                      gather_next ? &ga : nullptr);
+                      slab_stride, B, loss_acc, lr, momentum, wd, nesterov, prec, wprep,
+                      (s == 0 && !image_current) ? 2 : 1, cap, gather_next ? &ga : nullptr);
     }
   }
   e = hipStreamEndCapture(cap, &rg->graph);
@@ -1944,25 +1466,18 @@ static int capture_round(void** handle, int steps, const RoundArgs* pa, void* ws
 ECG_API int ecg_round_graph_create(void** handle, const float* X, int L, long ldx, const int* idx_table,
                                    const int* Y, float* params, float* mom, int nc, float* slab, int slab_stride,
                                    int B, int steps, float* loss_acc, float lr, float momentum, float wd,
-                                   int nesterov, int* ctl, float* gslab, int prec, const int* idx_stage,
-                                   void* wprep) {
+                                   int nesterov, int prec, const int* idx_stage, void* wprep) {
   if (!handle || steps <= 0) return ecg::kBadArg;
   int st = check_step_args(L, nc, B, slab_stride, 0, prec == 1);
   if (st) return st;
-  if (wprep && (prec != 0 || ctl)) return ecg::kBadArg;
-  return capture_round(handle, steps, nullptr, nullptr, 0, prec, X, L, ldx, idx_table, Y, params, mom, nc, slab,
-                       slab_stride, B, loss_acc, lr, momentum, wd, nesterov, ctl, gslab, idx_stage,
-                       static_cast<unsigned char*>(wprep));
+  if (wprep && prec != 0) return ecg::kBadArg;
+  return capture_round(handle, steps, prec, X, L, ldx, idx_table, Y, params, mom, nc, slab, slab_stride, B, loss_acc,
+                       lr, momentum, wd, nesterov, idx_stage, static_cast<unsigned char*>(wprep));
 }
 
-// A PF round split in two graphs (``ecg_round_graph_create`` with ``wprep`` and ``idx_stage``): this one captures
-// steps [step_offset, step_offset + steps) of the staged table; ``image_current`` = 1 when an earlier graph of the
-// same round already ran the LDS-path first step that rewrites the PF image.  Launching a short head graph first
-// lets the GPU start while the runtime still submits the long tail graph: a graph's launch latency grows with its
-// node count and sits in front of its first kernel.
-// ``xg``/``yg`` (optional, both or neither): ping-pong gather buffers, floats [2][B][round_up(L, 4)] and int32
-// [2][B] (ecg_tiny_gather_floats): every step after the round's first reads its batch from the buffer its
-// predecessor's reduce launch gathered (see GatherArgs) - bitwise the same step on the same data.
+// A PF round (``ecg_round_graph_create`` with ``wprep`` and ``idx_stage``): captures steps [step_offset,
+// step_offset + steps) of the staged table; ``image_current`` = 1 when the PF image is already current (else the
+// first captured step runs on the LDS path, whose SGD epilogue rewrites the image).
 ECG_API int ecg_round_graph_create_pf(void** handle, const float* X, int L, long ldx, const int* idx_stage,
                                       const int* Y, float* params, float* mom, int nc, float* slab, int slab_stride,
                                       int B, int steps, float* loss_acc, float lr, float momentum, float wd,
@@ -1971,35 +1486,13 @@ ECG_API int ecg_round_graph_create_pf(void** handle, const float* X, int L, long
   if (!handle || steps <= 0 || step_offset < 0 || !wprep || !idx_stage || (!xg) != (!yg)) return ecg::kBadArg;
   int st = check_step_args(L, nc, B, slab_stride, 0, false);
   if (st) return st;
-  return capture_round(handle, steps, nullptr, nullptr, 0, 0, X, L, ldx, idx_stage, Y, params, mom, nc, slab,
-                       slab_stride, B, loss_acc, lr, momentum, wd, nesterov, nullptr, nullptr, idx_stage,
-                       static_cast<unsigned char*>(wprep), step_offset, image_current, xg, yg);
-}
-
-ECG_API int ecg_round_graph_create_part(void** handle, const float* X, int L, long ldx, const int* idx_stage,
-                                        const int* Y, float* params, float* mom, int nc, float* slab, int slab_stride,
-                                        int B, int steps, float* loss_acc, float lr, float momentum, float wd,
-                                        int nesterov, void* wprep, int step_offset, int image_current) {
-  return ecg_round_graph_create_pf(handle, X, L, ldx, idx_stage, Y, params, mom, nc, slab, slab_stride, B, steps,
-                                   loss_acc, lr, momentum, wd, nesterov, wprep, step_offset, image_current, nullptr,
-                                   nullptr);
+  return capture_round(handle, steps, 0, X, L, ldx, idx_stage, Y, params, mom, nc, slab, slab_stride, B, loss_acc, lr,
+                       momentum, wd, nesterov, idx_stage, static_cast<unsigned char*>(wprep), step_offset, image_current,
+                       xg, yg);
 }
 
 // Floats of the gather buffer ``xg`` of ecg_round_graph_create_pf (its ``yg`` holds 2 * B int32).
 ECG_API long ecg_tiny_gather_floats(int L, int B) { return 2L * B * ((L + 3) / 4 * 4); }
-
-// The persistent round (workspace memset + one launch) captured as a hipGraph, replayed once per round.
-ECG_API int ecg_round_graph_create_persistent(void** handle, const float* X, int L, long ldx, const int* idx_table,
-                                              const int* Y, float* params, float* mom, int nc, int B, int steps,
-                                              float* loss_acc, float lr, float momentum, float wd, int nesterov,
-                                              void* ws, long ws_bytes, int* status, int prec,
-                                              const int* idx_stage) {
-  if (!handle || steps <= 0) return ecg::kBadArg;
-  const RoundArgs a = make_round_args(X, L, ldx, idx_table, Y, params, mom, nc, B, steps, loss_acc, lr, momentum, wd,
-                                      nesterov, ws, status, nullptr);
-  return capture_round(handle, steps, &a, ws, ws_bytes, prec, X, L, ldx, idx_table, Y, params, mom, nc, nullptr, 0,
-                       B, loss_acc, lr, momentum, wd, nesterov, nullptr, nullptr, idx_stage, nullptr);
-}
 
 ECG_API int ecg_round_graph_launch(void* handle, hipStream_t stream) {
   if (!handle) return ecg::kBadArg;

@@ -3,11 +3,9 @@
 
 Phases: 0 stage x/params | 1 conv1 | 2 conv2 fwd + mask | 3 head || mask-weighted wgrad | 4 dgrad2 + wgrad1 |
 5 row store.  Reports
-  * hipEvent times of the gradient-only kernel, the two-launch and single-launch rounds and the persistent round;
+  * hipEvent times of the gradient-only kernel and the two-launch round (LDS-built and prepared operands);
   * the per-step kernel's phases cold (first pass of a launch) and warm (MODE 2: the same workgroup computes
     its sample again right after, with warm instruction / scalar / data caches);
-  * the persistent round kernel's phases in a warm step (step 1): 0 param sweep + stage | 1..4 as above |
-    5 row publish + owned-column sweep | 6 ordered sums + SGD + publish.
 Stamped runs are slower than real ones: read shares, not totals.
 """
 import os
@@ -23,8 +21,6 @@ from crossscale_ecg.ops import _lib  # noqa: E402
 from crossscale_ecg.ops.fused_tiny import tiny_step_grads, labels_int32, slab_stride, FusedTinyTrainer  # noqa: E402
 
 NAMES = ["stage", "conv1", "conv2+mask", "head||M", "dgrad2+wgrad1", "row store"]
-ROUND_NAMES = ["params+stage", "conv1", "conv2+mask", "head||M", "dgrad2+wgrad1", "publish+gather",
-               "col sums+sgd"]
 
 
 def ev_time(fn, n):
@@ -63,9 +59,7 @@ def main():
     for pf in (False, True):
         t = ev_time(lambda: tiny_step_grads(flat, x, y32, idx, B, 2, slab, prefrag=pf), 200)
         print(f"gradient-only kernel (eager loop, prefrag={pf}, PF adds the prep launch): {t:.2f} us")
-    for name, kw in (("two-launch LDS", dict(persistent=False, prefrag=False)),
-                     ("two-launch PF ", dict(persistent=False, prefrag=True)),
-                     ("single-launch", dict(single_launch=True)), ("persistent  ", dict(persistent=True))):
+    for name, kw in (("two-launch LDS", dict(prefrag=False)), ("two-launch PF ", dict(prefrag=True))):
         m = TinyECG().to(dev)
         tr = FusedTinyTrainer(m, x, y, B, 50, seed=0, **kw)
         tr.run_round()
@@ -73,7 +67,6 @@ def main():
         t = ev_time(lambda: tr.run_round(), 20) / 50
         tr.use_graph = False
         te = ev_time(lambda: tr.run_round(), 4) / 50
-        tr.check_status()
         print(f"{name} round: graph {t:.2f} us/step, eager {te:.2f} us/step")
         tr.close()
 
@@ -109,19 +102,6 @@ def main():
         phase_table(s, 0, NAMES, f"[{label}] per-step kernel, COLD pass (fresh launch):")
         phase_table(s, 7, NAMES, f"[{label}] per-step kernel, WARM pass (same workgroup, immediately after):")
         print(f"  cold total median {statistics.median(cyc.tolist()):.0f} cyc")
-
-    # persistent round, warm step 1
-    m = TinyECG().to(dev)
-    tr = FusedTinyTrainer(m, x, y, B, 4, seed=0, use_graph=False, persistent=True)
-    tr.sampler.fill(tr.idx_table)
-    rs = torch.zeros(B * 16, dtype=torch.int64, device=dev)
-    for _ in range(5):
-        rs.zero_()
-        tr._eager_round(4, stamps=rs)
-    torch.cuda.synchronize()
-    tr.check_status()
-    phase_table(rs.view(B, 16).cpu(), 0, ROUND_NAMES, "persistent round kernel, step 1 (warm):")
-    tr.close()
 
 
 if __name__ == "__main__":

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-4 GPU measurement session on one MI355X (run by gpurun from the repo root):
-#   bash scripts/r4_gpu_session.sh <tag> <steps...>
+# GPU measurement session on one MI355X (run by gpurun from the repo root):
+#   bash scripts/gpu_session.sh <tag> <steps...>
 # steps (any subset, in order): tests smoke bench bench20 resnet | probe bnprobe convtest enginetest |
 #   module1 module2 module3 | libab (LIBS=...) envab (ENVS=...) finab tapab | pmc tappmc tinypmc stats timeline timeline0
 # Every GPU step runs under its own time limit; a crash, abort or timeout ends the session.
@@ -8,7 +8,7 @@ set -u
 cd "$(dirname "$0")/.."
 TAG=${1:-base}
 shift
-OUT=gpurun_out/r4_$TAG
+OUT=gpurun_out/${ECG_ROUND:-r5}_$TAG
 mkdir -p "$OUT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {  # step <name> <timeout_s> <cmd...>

@@ -18,7 +18,7 @@ def main():
     x = torch.randn(20000, 500, device=dev)
     y = torch.zeros(20000, dtype=torch.long, device=dev)
     torch.manual_seed(0)
-    tr = FusedTinyTrainer(TinyECG().to(dev), x, y, 256, 50, seed=0, use_graph=False, persistent=False)
+    tr = FusedTinyTrainer(TinyECG().to(dev), x, y, 256, 50, seed=0, use_graph=False)
     for _ in range(6):
         tr.run_round(50)
     torch.cuda.synchronize()

@@ -100,39 +100,18 @@ def test_train_step_and_graph_match_torch_sgd(precision):
     tr.close()
 
 
-@pytest.mark.parametrize("B", [7, 16, 100, 256])
-def test_single_launch_step_matches_two_launch(B):
-    """In-kernel reduction tree + SGD (one launch) == slab + reduce kernel (two launches), any batch size,
-    and the arrival counters are reset between launches (many consecutive steps)."""
-    from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
-    dev, x, y, model, _ = _setup(B=B, N=max(4 * B, 64))
-    m2 = TinyECG().to(dev)
-    m2.load_state_dict(model.state_dict())
-    a = FusedTinyTrainer(model, x, y, B, 6, seed=3, use_graph=True, single_launch=True)
-    b = FusedTinyTrainer(m2, x, y, B, 6, seed=3, use_graph=False, single_launch=False, persistent=False)
-    for _ in range(3):
-        a.run_round()
-        b.run_round()
-    torch.cuda.synchronize()
-    assert int(a.ctl.abs().sum()) == 0, "arrival counters not reset"
-    assert torch.allclose(a.params, b.params, rtol=1e-5, atol=1e-6), (a.params - b.params).abs().max()
-    assert abs(a.avg_loss() - b.avg_loss()) < 1e-4
-    a.close()
-    b.close()
-
-
-def test_single_launch_is_deterministic():
+def test_two_launch_round_is_deterministic():
     from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
     outs = []
-    for single in (True, True, False, False):
+    for _ in range(2):
         dev, x, y, model, _ = _setup(B=256, N=2048)
-        tr = FusedTinyTrainer(model, x, y, 256, 10, seed=11, single_launch=single, persistent=False)
+        tr = FusedTinyTrainer(model, x, y, 256, 10, seed=11)
         tr.run_round()
         torch.cuda.synchronize()
         outs.append(tr.params.clone())
         tr.close()
-    # both paths are atomics-free: bitwise reproducible run to run
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[2], outs[3])
+    # atomics-free fixed-order reduction: bitwise reproducible run to run
+    assert torch.equal(outs[0], outs[1])
 
 
 def test_fp32_window_limit_is_reported():
@@ -149,8 +128,8 @@ def test_graph_equals_eager():
     dev, x, y, model, _ = _setup(B=64, N=640)
     m2 = TinyECG().to(dev)
     m2.load_state_dict(model.state_dict())
-    a = FusedTinyTrainer(model, x, y, 64, 5, seed=7, use_graph=True, persistent=False)
-    b = FusedTinyTrainer(m2, x, y, 64, 5, seed=7, use_graph=False, persistent=False)
+    a = FusedTinyTrainer(model, x, y, 64, 5, seed=7, use_graph=True)
+    b = FusedTinyTrainer(m2, x, y, 64, 5, seed=7, use_graph=False)
     for _ in range(3):
         a.run_round()
         b.run_round()
@@ -175,73 +154,6 @@ def test_training_reduces_loss_on_learnable_labels():
         tr.run_round()
     last = tr.avg_loss()
     assert last < first * 0.9, (first, last)
-    tr.close()
-
-
-@pytest.mark.parametrize("precision", ["bf16", "fp32"])
-@pytest.mark.parametrize("B", [7, 64, 256])
-def test_persistent_round_matches_two_launch(B, precision):
-    """One persistent launch per round (granule hand-offs, column-slice owners apply SGD) == two launches per
-    step: every owner sums its columns in the slab-reduce kernel's order, so weights, momentum and loss agree
-    bit for bit, over several rounds (the granule tags are re-zeroed before every launch)."""
-    from crossscale_ecg.ops import _lib
-    from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
-    dev, x, y, model, _ = _setup(B=B, N=max(4 * B, 64))
-    m2 = TinyECG().to(dev)
-    m2.load_state_dict(model.state_dict())
-    lib = _lib.kernels()
-    # the per-step kernel at the persistent kernel's wave count (bf16: 8), so per-sample sums match bit for bit
-    prev = lib.ecg_tiny_force_waves(8 if precision == "bf16" else 0)
-    try:
-        a = FusedTinyTrainer(model, x, y, B, 6, seed=3, use_graph=True, persistent=True, precision=precision)
-        b = FusedTinyTrainer(m2, x, y, B, 6, seed=3, use_graph=False, persistent=False, precision=precision)
-        assert a.persistent and not b.persistent
-        for _ in range(3):
-            a.run_round()
-            b.run_round()
-        torch.cuda.synchronize()
-    finally:
-        lib.ecg_tiny_force_waves(prev)
-    a.check_status()
-    assert torch.equal(a.params, b.params), (a.params - b.params).abs().max()
-    assert torch.equal(a.mom, b.mom), (a.mom - b.mom).abs().max()
-    assert a.avg_loss() == b.avg_loss()
-    a.close()
-    b.close()
-
-
-def test_persistent_round_graph_equals_eager_partial_rounds():
-    """Graph replay == direct launch of the persistent round, for full and partial rounds."""
-    from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
-    dev, x, y, model, _ = _setup(B=128, N=1024)
-    m2 = TinyECG().to(dev)
-    m2.load_state_dict(model.state_dict())
-    a = FusedTinyTrainer(model, x, y, 128, 5, seed=5, use_graph=True, persistent=True)
-    b = FusedTinyTrainer(m2, x, y, 128, 5, seed=5, use_graph=False, persistent=True)
-    for n in (5, 1, 3, 5):
-        a.run_round(n)
-        b.run_round(n)
-        torch.cuda.synchronize()
-        assert a.avg_loss() == b.avg_loss()
-    assert torch.equal(a.params, b.params) and torch.equal(a.mom, b.mom)
-    a.close()
-    b.close()
-
-
-def test_persistent_round_is_opt_in_and_checked():
-    from crossscale_ecg.ops import _lib
-    from crossscale_ecg.ops.fused_tiny import FusedTinyTrainer
-    dev, x, y, model, _ = _setup(B=256, N=1024)
-    assert not FusedTinyTrainer(TinyECG().to(dev), x, y, 256, 4, seed=1).persistent  # two-launch is the default
-    tr = FusedTinyTrainer(model, x, y, 256, 4, seed=1, persistent=True)
-    assert tr.persistent, "B=256 fits one workgroup per CU on MI355X"
-    n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-    assert _lib.kernels().ecg_tiny_round_fits(500, 2, n_cu + 1, 0) == 0  # more workgroups than CUs: not offered
-    with pytest.raises(ValueError):
-        FusedTinyTrainer(TinyECG().to(dev), torch.randn(2 * (n_cu + 1), 500, device=dev),
-                         torch.zeros(2 * (n_cu + 1), dtype=torch.long, device=dev), n_cu + 1, 2, persistent=True)
-    tr.run_round()
-    assert tr.avg_loss() == tr.avg_loss()
     tr.close()
 
 
@@ -298,8 +210,8 @@ def test_prefrag_round_graph_bitwise_equal_lds_eager_with_external_updates(graph
     dev, x, y, model, _ = _setup(B=128, N=1024)
     m2 = TinyECG().to(dev)
     m2.load_state_dict(model.state_dict())
-    a = FusedTinyTrainer(model, x, y, 128, 7, seed=9, use_graph=graph, persistent=False, prefrag=True)
-    b = FusedTinyTrainer(m2, x, y, 128, 7, seed=9, use_graph=False, persistent=False, prefrag=False)
+    a = FusedTinyTrainer(model, x, y, 128, 7, seed=9, use_graph=graph, prefrag=True)
+    b = FusedTinyTrainer(m2, x, y, 128, 7, seed=9, use_graph=False, prefrag=False)
     assert a.prefrag and not b.prefrag
     g = torch.Generator(device=dev)
     g.manual_seed(5)
@@ -328,7 +240,7 @@ def test_gather_round_graph_bitwise_equal_plain(L, B):
     outs = []
     for gather, graph in ((True, True), (False, True), (False, False)):
         dev, x, y, model, _ = _setup(B=B, L=L, N=1024, nc=5)
-        tr = FusedTinyTrainer(model, x, y, B, 7, seed=21, persistent=False, prefrag=True, use_graph=graph)
+        tr = FusedTinyTrainer(model, x, y, B, 7, seed=21, prefrag=True, use_graph=graph)
         tr.gather = gather
         if gather and tr.xg is None:
             tr.xg = torch.zeros(2 * B * ((L + 3) // 4 * 4), dtype=torch.float32, device=dev)
