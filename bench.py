@@ -251,6 +251,12 @@ class FedAvgRunner:
             self._pending = None
 
 
+def weights_digest(flat):
+    """float64 sum and abs-sum of the flat weights plus their first and last 8 values (18 numbers)."""
+    f = flat.detach().double()
+    return [float(f.sum()), float(f.abs().sum())] + f[:8].tolist() + f[-8:].tolist()
+
+
 def torch_eager_rate(x, y, B, steps, device):
     import torch
     import torch.nn.functional as F
@@ -339,8 +345,14 @@ def main(argv=None):
     sys.path.insert(0, ROOT)
     import crossscale_ecg  # noqa: F401
     from crossscale_ecg.models.tiny_ecg import TinyECG, num_params
-    from crossscale_ecg.parallel.env import init_distributed, barrier, shutdown_distributed
+    from crossscale_ecg.parallel.env import (init_distributed, barrier, shutdown_distributed, rccl_init_log,
+                                             rccl_transports, peer_access)
 
+    # RCCL runs: its INIT log (channel -> transport) goes to a per-rank file read back after the run
+    rccl_log = None
+    if a.device == "gpu" and os.environ.get("ECG_DIST_BACKEND", "nccl") == "nccl" and \
+            int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        rccl_log = rccl_init_log()
     ctx = init_distributed(prefer_gpu=a.device == "gpu")
     if ctx.world_size != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={ctx.world_size}")
@@ -438,11 +450,14 @@ def main(argv=None):
         gc.enable()
     gpu_s = ev0.elapsed_time(ev1) / 1e3 if ev0 is not None else float("nan")
     comm_ms, exposed_ms = runner.timer.summary() if runner.timer is not None else (0.0, 0.0)
+    digest = weights_digest(flat)  # after the last FedAvg all-reduce every rank must hold these exact weights
     tbar_kind = tbar.kind
     tbar.close()
     world_seen, dist_backend = 1, "none"
     per_rank = [[elapsed, gpu_s, comm_ms, exposed_ms]]
     placements = [placement]
+    digests = [digest]
+    links = None
     if ctx.distributed:
         import torch.distributed as dist
         world_seen, dist_backend = dist.get_world_size(), dist.get_backend()
@@ -453,6 +468,12 @@ def main(argv=None):
         per_rank = [[float(v) for v in t.tolist()] for t in allv]
         placements = [None] * world_seen
         dist.all_gather_object(placements, placement)
+        dig = torch.tensor(digest, dtype=torch.float64, device=dev if dist_backend == "nccl" else "cpu")
+        digs = [torch.zeros_like(dig) for _ in range(world_seen)]
+        dist.all_gather(digs, dig)
+        digests = [[float(v) for v in t.tolist()] for t in digs]
+        links = [None] * world_seen
+        dist.all_gather_object(links, {"transports": rccl_transports(rccl_log), "peer_access": peer_access(dev)})
         elapsed = max(r[0] for r in per_rank)
         gpu_s = max(r[1] for r in per_rank)
     total = a.gpus * B * a.steps
@@ -517,12 +538,18 @@ def main(argv=None):
             "per_rank_gpu_ms_per_step": [round(r[1] * 1e3 / a.steps, 5) if r[1] == r[1] else None for r in per_rank],
             "comm_ms": [round(r[2], 4) for r in per_rank],
             "comm_exposed_ms": [round(r[3], 4) for r in per_rank],
+            # rank -> NUMA node : CPU slice [split basis: kfd = planned over every GPU of the machine]
             "rank_cpus": [f"node{p.get('numa_node', -1)}:{p.get('cpus', '')}" + ("" if p.get("bound") else " (unbound)")
-                          for p in placements],
+                          + (f" [{p['basis']}]" if p.get("basis") else "") for p in placements],
             # timing method: the cyclic GC is paused inside the timed region (restarted right after); the first
             # timed round's batch indices were drawn behind the last warmup round (later rounds' staging is timed)
             "gc_paused_in_timed_region": True,
             "first_round_staged_in_warmup": a.warmup > 0,
+            # self-check of the FedAvg result: float64 sum / abs-sum and the first and last 8 weights of every rank
+            # after the final all-reduce (must be bit-identical across ranks)
+            "fedavg_weights_identical": all(d == digests[0] for d in digests),
+            "fedavg_weights_checksum": digests[0][0],
+            **({"rccl_links": links} if links is not None else {}),
             **extras,
         }
         print(json.dumps(rec), flush=True)

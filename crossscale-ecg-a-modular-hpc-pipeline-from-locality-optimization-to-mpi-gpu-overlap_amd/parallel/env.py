@@ -132,3 +132,44 @@ def barrier(ctx: Optional[DistContext] = None) -> None:
             dist.barrier(device_ids=[ctx.device.index])
         else:
             dist.barrier()
+
+
+# ----------------------------------------------------------------------------------- RCCL transport record
+def rccl_init_log(directory: Optional[str] = None) -> Optional[str]:
+    """Route RCCL's INIT-subsystem log to a per-process file, so the transport RCCL chose for every ring / tree
+    channel (``via P2P/IPC`` over xGMI, ``via SHM``, ``via NET``) can be read back after the run
+    (``rccl_transports``).  Must run before the first communicator is created; leaves a user's own NCCL_DEBUG
+    setting alone (returns None then)."""
+    if "NCCL_DEBUG" in os.environ:
+        return None
+    directory = directory or os.environ.get("TMPDIR", "/tmp")
+    path = os.path.join(directory, f"ecg_rccl_init.{os.getpid()}.log")
+    os.environ["NCCL_DEBUG"] = "INFO"
+    os.environ["NCCL_DEBUG_SUBSYS"] = "INIT"
+    os.environ["NCCL_DEBUG_FILE"] = path
+    return path
+
+
+def rccl_transports(path: Optional[str]) -> dict:
+    """Count the channel connections per transport in an RCCL INIT log (``rccl_init_log``): e.g.
+    ``{"P2P/IPC": 24}`` when every ring/tree neighbour is reached over xGMI peer-to-peer."""
+    out: dict = {}
+    if not path or not os.path.exists(path):
+        return out
+    import re
+    pat = re.compile(r"\bvia (P2P/[\w ]+?|SHM(?:/\w+)?|NET/[\w/]+|NVLS|CollNet\w*)(?:\s|$|/read|/direct)")
+    with open(path, errors="replace") as f:
+        for line in f:
+            m = pat.search(line)
+            if m:
+                key = m.group(1).strip()
+                out[key] = out.get(key, 0) + 1
+    return out
+
+
+def peer_access(device: torch.device) -> list:
+    """Per visible GPU j != this rank's: whether HIP reports direct peer access (xGMI) from ``device`` to j."""
+    if device.type != "cuda":
+        return []
+    n = torch.cuda.device_count()
+    return [bool(torch.cuda.can_device_access_peer(device.index, j)) for j in range(n) if j != device.index]

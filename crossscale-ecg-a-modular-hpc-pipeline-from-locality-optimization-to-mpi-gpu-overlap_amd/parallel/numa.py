@@ -8,7 +8,12 @@ its GPU, to a disjoint slice of the CPUs of that GPU's NUMA node:
 
     GPU PCI address (torch device properties) -> /sys/bus/pci/devices/<bdf>/numa_node
     -> /sys/devices/system/node/node<n>/cpulist  (intersected with the CPUs this process may use)
-    -> ranks on the same node split that list into contiguous, equal slices (in device order).
+    -> the GPUs on the same NUMA node split that list into contiguous, equal slices (in PCI-address order).
+
+The GPUs that share a node are taken from the KFD topology (``/sys/class/kfd/kfd/topology/nodes``: every GPU of
+the machine, whatever ``HIP_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES`` or ``srun --gpus-per-task=1`` let this
+process see), so ranks that each see only their own GPU still get disjoint slices; only when the topology is
+unreadable does the split fall back to the visible devices.  The basis used is part of the returned record.
 
 Everything reads a ``sysfs`` root argument so the mapping is unit-tested on a fake tree.
 """
@@ -89,6 +94,34 @@ def plan_affinity(bdfs: Sequence[str], index: int, allowed: Iterable[int],
     return node, cpus[k * per:(k + 1) * per]
 
 
+def kfd_gpu_bdfs(kfd_root: str = "/sys/class/kfd/kfd/topology/nodes") -> List[str]:
+    """PCI addresses of EVERY GPU of the machine from the KFD topology (``gpu_id`` != 0; ``location_id`` =
+    bus << 8 | device << 3 | function, ``domain``), sorted - independent of the *_VISIBLE_DEVICES masks."""
+    out = []
+    try:
+        nodes = os.listdir(kfd_root)
+    except OSError:
+        return out
+    for n in nodes:
+        gid = _read(os.path.join(kfd_root, n, "gpu_id"))
+        try:
+            if gid is None or int(gid.strip() or 0) == 0:
+                continue
+        except ValueError:
+            continue
+        props = {}
+        for line in (_read(os.path.join(kfd_root, n, "properties")) or "").splitlines():
+            parts = line.split()
+            if len(parts) == 2:
+                props[parts[0]] = parts[1]
+        try:
+            loc, dom = int(props["location_id"]), int(props.get("domain", "0"))
+        except (KeyError, ValueError):
+            continue
+        out.append(f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}")
+    return sorted(set(out))
+
+
 def device_bdfs() -> List[str]:
     """PCI addresses (``dddd:bb:dd.0``) of the visible GPUs, in device order (initialises the HIP runtime)."""
     import torch
@@ -99,20 +132,44 @@ def device_bdfs() -> List[str]:
     return out
 
 
-def bind_to_gpu_numa(device_index: int, sysfs: str = "/sys", bdfs: Optional[Sequence[str]] = None) -> Dict:
-    """Pin this process to its slice of the CPUs of GPU ``device_index``'s NUMA node.  Returns a record
-    {"numa_node", "cpus", "bound"} for the bench JSON; never raises (placement is a performance measure)."""
-    rec: Dict = {"numa_node": -1, "cpus": "", "bound": False}
+def _set_process_affinity(cpus: Sequence[int]) -> None:
+    """Apply the mask to every thread of the process (``sched_setaffinity(0)`` moves only the calling thread; the
+    HIP runtime's own threads, started when the device was selected, would keep the old mask)."""
+    os.sched_setaffinity(0, cpus)
+    try:
+        tids = [int(t) for t in os.listdir("/proc/self/task")]
+    except OSError:
+        return
+    for t in tids:
+        try:
+            os.sched_setaffinity(t, cpus)
+        except OSError:
+            pass
+
+
+def bind_to_gpu_numa(device_index: int, sysfs: str = "/sys", bdfs: Optional[Sequence[str]] = None,
+                     kfd_root: str = "/sys/class/kfd/kfd/topology/nodes") -> Dict:
+    """Pin this process to its slice of the CPUs of GPU ``device_index``'s NUMA node (``device_index`` indexes the
+    VISIBLE devices, ``bdfs``).  The slice is planned over every GPU of the machine (KFD topology) so that ranks
+    with narrowed visibility still split disjointly.  Returns a record {"numa_node", "cpus", "bound", "basis"} for
+    the bench JSON; never raises (placement is a performance measure)."""
+    rec: Dict = {"numa_node": -1, "cpus": "", "bound": False, "basis": "none"}
     try:
         allowed = os.sched_getaffinity(0)
         if bdfs is None:
             bdfs = device_bdfs()
         if not 0 <= device_index < len(bdfs):
             return rec
-        node, cpus = plan_affinity(bdfs, device_index, allowed, sysfs)
+        mine = bdfs[device_index]
+        every = kfd_gpu_bdfs(kfd_root)
+        if mine in every:
+            plan_bdfs, idx, rec["basis"] = every, every.index(mine), "kfd"
+        else:  # topology unreadable (or a device it does not list): split among the visible GPUs
+            plan_bdfs, idx, rec["basis"] = list(bdfs), device_index, "visible"
+        node, cpus = plan_affinity(plan_bdfs, idx, allowed, sysfs)
         rec["numa_node"] = node
         if cpus:
-            os.sched_setaffinity(0, cpus)
+            _set_process_affinity(cpus)
             rec["cpus"], rec["bound"] = format_cpulist(cpus), True
         else:
             rec["cpus"] = format_cpulist(allowed)
