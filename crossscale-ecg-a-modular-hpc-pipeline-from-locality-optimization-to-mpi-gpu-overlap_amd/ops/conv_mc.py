@@ -32,7 +32,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_fwd", [vp, vp, vp, vp] + [i32] * 10 + [vp])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad", [vp, vp, vp] + [i32] * 9 + [vp])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_tiles", [i32, i32, i32])
-    _lib._sig(lib, "ecg_conv1d_nlc_wgrad_target_wgs", [i32, i32, i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_wgrad_target_wgs", [i32] * 6)
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_splits", [i32] * 8)
     _lib._sig(lib, "ecg_conv1d_nlc_set_big", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_set_mt", [i32])
@@ -76,9 +76,12 @@ def set_multi_tile(mode: int) -> int:
     return _lib_k().ecg_conv1d_nlc_set_mt(int(mode))
 
 
-def stat_rows(M: int, c_out: int) -> int:
-    """Rows of BatchNorm partials the forward kernel writes for M output rows and c_out channels."""
-    return _lib_k().ecg_conv1d_nlc_fwd_stat_tiles(int(M), int(c_out))
+def stat_rows(B: int, L_in: int, c_in: int, L_out: int, c_out: int, k: int = 3, stride: int = 1, pad: int = 1,
+              in_dil: int = 1) -> int:
+    """Rows of BatchNorm partials the forward kernel writes for that exact conv (the kernel family - tap-shared,
+    multi-tile, one-tile - and its tile size depend on the whole shape, not just M and c_out)."""
+    return _lib_k().ecg_conv1d_nlc_fwd_stat_rows(int(B), int(L_in), int(c_in), int(L_out), int(c_out), int(k),
+                                                 int(stride), int(pad), int(in_dil))
 
 
 def fwd_stats_raw(x: torch.Tensor, w_t: torch.Tensor, stride: int, pad: int, L_out: int):
@@ -130,7 +133,7 @@ def wgrad_raw(dy: torch.Tensor, x: torch.Tensor, K: int, stride: int, pad: int,
     if splits is None:  # the tap-shared kernel's plan, else: target workgroups, >= 8 chunks each, <= 256 slices
         splits = lib.ecg_conv1d_nlc_wgrad_splits(B, Lin, Cin, Lout, Cout, K, stride, pad)
     if not splits:
-        target = lib.ecg_conv1d_nlc_wgrad_target_wgs(Cout, K, Cin)
+        target = lib.ecg_conv1d_nlc_wgrad_target_wgs(Cout, K, Cin, B, Lin, Lout)
         splits = max(1, min(256, max(1, chunks // 8), max(1, target // max(1, tiles))))
     part = torch.empty((splits, Cout, K * Cin), dtype=torch.float32, device=dy.device)
     st = _lib_k().ecg_conv1d_nlc_wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr(), splits, B, Lin, Cin, Lout, Cout, K,

@@ -54,7 +54,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_plan_stem_rows", [])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles", [ctypes.c_long, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_tiles", [i32, i32, i32])
-    _lib._sig(lib, "ecg_conv1d_nlc_wgrad_target_wgs", [i32, i32, i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_wgrad_target_wgs", [i32] * 6)
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_splits", [i32] * 8)
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles_ex", [i32, i32, i32, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_rows", [i32] * 9)
@@ -219,7 +219,7 @@ class ResNetStepEngine:
             # S x |dW|)
             chunks = (R + 63) // 64
             tiles = self.lib.ecg_conv1d_nlc_wgrad_tiles(Cout, K, Cin)
-            target = self.lib.ecg_conv1d_nlc_wgrad_target_wgs(Cout, K, Cin)
+            target = self.lib.ecg_conv1d_nlc_wgrad_target_wgs(Cout, K, Cin, B, Lin or 0, Lout or 0)
             # A/B knob: capping the splits shrinks the reduce (S x |dW|) but starves the wgrad kernel of workgroups
             # (B=1024: cap 16 -> 5.86, cap 8 -> 7.66 ms/step vs 4.61 uncapped, profiles/r2/resnet_conv_ab.txt)
             cap = 64

@@ -831,7 +831,9 @@ struct TapCfg {
 };
 
 template <int BN, int EPI>
-__global__ __launch_bounds__(512, 2) void conv1d_nlc_fwd_tap_kernel(FwdArgs a, int MT, int NT) {
+// (launch bounds: one workgroup per CU is all the ~115 KB of LDS allows; the code object is identical to the one
+// built with a min-blocks hint of 2 - 103-161 VGPRs, no scratch - so the hint now states the real residency)
+__global__ __launch_bounds__(512, 1) void conv1d_nlc_fwd_tap_kernel(FwdArgs a, int MT, int NT) {
   constexpr int BM = TAP_BM, NWR = 4, NW = 8;
   using Cfg = FwdCfg<BM, BN, NWR>;
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
@@ -1483,7 +1485,7 @@ __global__ __launch_bounds__(128 * NWR, NWR == 2 ? 2 : 1) void conv1d_nlc_wgrad_
 // split-K partial traffic (written here, re-read by the reduce) halves at equal occupancy, and the launch needs half
 // the workgroups for the same depth of work per CU.
 template <int NG>
-__global__ __launch_bounds__(256 * NG, NG == 2 ? 2 : 1) void conv1d_nlc_wgrad_dma2_kernel(WgradArgs a, int TM, int TN,
+__global__ __launch_bounds__(256 * NG, 1) void conv1d_nlc_wgrad_dma2_kernel(WgradArgs a, int TM, int TN,
                                                                                           int splits) {
   constexpr int BM = 128, BN = 128, NWR = 2;
   using Cfg = WgCfg<BM, BN, NWR>;
@@ -1996,6 +1998,12 @@ ECG_API int ecg_conv1d_nlc_fwd(const void* x, const void* w, const float* bias, 
                                in_dil, relu, nullptr, nullptr, stream);
 }
 
+// LDS-DMA weight-gradient loops: 32-bit buffer offsets from the split's first row / sample (cps row chunks of 64).
+inline bool wgrad_dma_ok(long cps, int Lin, int Cin, int Lout, int Cout) {
+  const long rows = cps * 64;
+  return rows * Cout * 2 < 0x7fff0000L && (rows / Lout + 2) * (long)Lin * Cin * 2 < 0x7fff0000L;
+}
+
 // Partial weight gradients: part[splits][Cout][Kw*Cin] fp32 (sum over dim 0 = dw in [Cout][Kw][Cin]).
 // ``splits`` workgroup slices of the (b,t) reduction; returns kBadArg unless Cin, Cout % 64 == 0.
 ECG_API int ecg_conv1d_nlc_wgrad(const void* dy, const void* x, float* part, int splits, int B, int Lin, int Cin,
@@ -2009,10 +2017,7 @@ ECG_API int ecg_conv1d_nlc_wgrad(const void* dy, const void* x, float* part, int
               stride, pad, cps, make_fastdiv(Lout)};
   if (wgrad_ts_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad)) return launch_wgrad_ts(a, splits, stream);
   const bool bm128 = Cout % 128 == 0, bn128 = Cin % 128 == 0;
-  // LDS-DMA loops: 32-bit buffer offsets from the split's first row / sample
-  const long rows = (long)cps * 64;
-  const bool dma_ok = rows * Cout * 2 < 0x7fff0000L &&
-                      (rows / Lout + 2) * (long)Lin * Cin * 2 < 0x7fff0000L;
+  const bool dma_ok = wgrad_dma_ok(cps, Lin, Cin, Lout, Cout);
   if (wgrad_big(Cout, Cin)) return dma_ok ? launch_wgrad_dma<256, 256>(a, splits, stream)
                                           : launch_wgrad<256, 256>(a, splits, stream);
   if (bm128 && bn128 && dma_ok) return launch_wgrad_dma2(a, splits, stream);
@@ -2042,12 +2047,21 @@ ECG_API int ecg_conv1d_nlc_wgrad_splits(int B, int Lin, int Cin, int Lout, int C
 }
 
 // Workgroups the weight-gradient launch should aim for (tiles x splits): ~4 resident per CU for the 4-wave
-// register-staged tiles, ~2 rounds of one per CU for the 8-wave 256x256 tile.
-ECG_API int ecg_conv1d_nlc_wgrad_target_wgs(int Cout, int Kw, int Cin) {
-  (void)Kw;
+// register-staged tiles, ~2 rounds of one per CU for the 8-wave 256x256 tile.  (B, Lin, Lout) decide whether the
+// 128x128 shapes take the two-group LDS-DMA kernel at the split count that target implies; B = 0: assume it does.
+ECG_API int ecg_conv1d_nlc_wgrad_target_wgs(int Cout, int Kw, int Cin, int B, int Lin, int Lout) {
   if (wgrad_big(Cout, Cin)) return 512;
   // 128x128 tiles: the two-group 8-wave kernel, one workgroup per CU (B=1024 ResNet1D-34: 3.43 ms/step at 256
-  // workgroups vs 3.51 at 512 and 3.81 at 768; profiles/r4/wgrad_g2_ab.txt)
-  if (Cout % 128 == 0 && Cin % 128 == 0) return 256;
+  // workgroups vs 3.51 at 512 and 3.81 at 768; profiles/r4/wgrad_g2_ab.txt) - when its 32-bit offsets hold;
+  // otherwise the 4-wave register-staged 128x128 kernel, which wants ~4 workgroups per CU (advisor r4)
+  if (Cout % 128 == 0 && Cin % 128 == 0) {
+    if (B <= 0 || Lout <= 0) return 256;
+    const int tiles = ecg_conv1d_nlc_wgrad_tiles(Cout, Kw, Cin);
+    const long chunks = ((long)B * Lout + 63) / 64;
+    long splits = (256 + tiles - 1) / tiles;
+    splits = splits < 1 ? 1 : splits;
+    const long cps = (chunks + splits - 1) / splits;
+    return wgrad_dma_ok(cps, Lin, Cin, Lout, Cout) ? 256 : 1024;
+  }
   return 1024;
 }

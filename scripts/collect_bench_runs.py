@@ -4,7 +4,7 @@ on (GPU serial number from the session's host.txt) and the commit the session ra
 rendered from ALL measured lines - not the best box.  Driver records (BENCH_rNN.json at the repo
 root) are added with ``--driver``.
 
-    python scripts/collect_bench_runs.py --commit <sha> gpurun_out/r4_<tag> [...]
+    python scripts/collect_bench_runs.py --commit <sha> gpurun_out/r5_<tag> [...]
     python scripts/collect_bench_runs.py --driver BENCH_r03.json
 Only the default configurations are collected: ``bench20_<i>.log`` (the driver's command), ``bench500.log``
 (K=500) and ``resnet_<i>.log`` (ResNet1D-34 B=1024, K=20); A/B logs with knobs set carry other names.
@@ -15,7 +15,7 @@ import os
 import re
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DEFAULT_OUT = os.path.join(ROOT, "profiles", "r4", "bench_runs.jsonl")
+DEFAULT_OUT = os.path.join(ROOT, "profiles", "r5", "bench_runs.jsonl")
 KEEP = ("value", "ms_per_step", "gpu_ms_per_step", "steps", "warmup", "n_gpus")
 
 

@@ -35,7 +35,7 @@ def main():
             conv_mc.set_multi_tile(mode)
             t_plain = timeit(lambda: conv_mc.fwd_raw(x, w, None, 1, 1, L))
             t_stats = timeit(lambda: conv_mc.fwd_stats_raw(x, w, 1, 1, L))
-            rows = conv_mc.stat_rows(B * L, C)
+            rows = conv_mc.stat_rows(B, L, C, L, C)
             print(f"M={B * L:6d} C={C:3d} mt={mode}: plain {t_plain:6.2f} us  stats {t_stats:6.2f} us  "
                   f"({rows} partial rows)", flush=True)
     conv_mc.set_multi_tile(1)

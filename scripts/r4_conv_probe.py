@@ -70,7 +70,7 @@ def main():
             tiles = lib.ecg_conv1d_nlc_wgrad_tiles(Co, K, Ci)
             splits = lib.ecg_conv1d_nlc_wgrad_splits(B, L, Ci, Lo, Co, K, s, p)
             if not splits:
-                target = lib.ecg_conv1d_nlc_wgrad_target_wgs(Co, K, Ci)
+                target = lib.ecg_conv1d_nlc_wgrad_target_wgs(Co, K, Ci, B, L, Lo)
                 splits = max(1, min(256, max(1, chunks // 8), max(1, target // max(1, tiles))))
             part = torch.empty((splits, Co, K * Ci), dtype=torch.float32, device=dev)
             def wg():

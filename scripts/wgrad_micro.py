@@ -23,7 +23,7 @@ def splits_for(lib, B, L, C):
         return s, "ts"
     chunks = (B * L + 63) // 64
     tiles = lib.ecg_conv1d_nlc_wgrad_tiles(C, 3, C)
-    target = lib.ecg_conv1d_nlc_wgrad_target_wgs(C, 3, C)
+    target = lib.ecg_conv1d_nlc_wgrad_target_wgs(C, 3, C, B, L, L)
     return max(1, min(64, 256, max(1, chunks // 8), max(1, target // tiles))), "one-tap"
 
 

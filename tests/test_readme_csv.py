@@ -3,6 +3,8 @@ crossscale_ecg.report.readme renders from the CSV directory the block names, and
 committed profiles/rN/modules."""
 import os
 
+import pytest
+
 from crossscale_ecg.report import readme
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -40,15 +42,21 @@ def test_render_marks_bar_and_spread(tmp_path):
 
 
 def test_readme_headline_matches_bench_runs():
-    """The headline rows are rendered from every recorded bench line (profiles/rN/bench_runs.jsonl)."""
+    """The headline rows are rendered from every recorded bench line (profiles/rN/bench_runs.jsonl) of HEAD's code,
+    and the runs file holds the newest driver record (BENCH_rNN.json)."""
+    import json
+    runs_file = readme.latest_runs_file(ROOT)
+    commits = {json.loads(ln)["commit"] for ln in open(os.path.join(ROOT, runs_file)) if ln.strip()}
+    if not readme.git_ready(c for c in commits if c):
+        pytest.skip("git history (HEAD and the recorded commits) not available: code identity cannot be decided")
     ok, expected, found = readme.check_headline(os.path.join(ROOT, "README.md"), root=ROOT)
     assert ok, "README headline is stale; run `python -m crossscale_ecg.report.readme --write`\n" + expected
     assert f"<!-- runs: {readme.latest_runs_file(ROOT)} -->" in found
 
 
-def test_render_headline_median_over_boxes(tmp_path):
-    """Builder rows: median and range over all runs of the newest commit (older commits ignored), box count; the
-    driver column quotes the newest driver record."""
+def test_render_headline_median_over_boxes(tmp_path, monkeypatch):
+    """Builder rows: median and range over all runs of HEAD's code (other commits ignored), box count; the driver
+    column quotes the newest driver record."""
     import json
     recs = [
         {"source": "builder", "session": "s0", "log": "bench20_1.log", "box": "A", "commit": "old", "model": "tiny_ecg",
@@ -63,8 +71,14 @@ def test_render_headline_median_over_boxes(tmp_path):
                      "steps": 20, "warmup": 5, "n_gpus": 1})
     p = tmp_path / "bench_runs.jsonl"
     p.write_text("".join(json.dumps(r) + "\n" for r in recs))
+    # code identity: "new" carries HEAD's code, "old" does not
+    monkeypatch.setattr(readme, "_same_code", lambda a, b: a == "new" and b == "HEAD")
     text = readme.render_headline(str(p))
     row = [ln for ln in text.splitlines() if "driver's command" in ln][0]
     assert "round 7: **20.0 M/s**" in row
     assert "median **19.0 M/s** (18.0 M/s–20.0 M/s) over 3 runs on 2 boxes, commit `new`" in row
-    assert "no run recorded" in [ln for ln in text.splitlines() if "ResNet1D-34" in ln][0]
+    assert "no run of the current code" in [ln for ln in text.splitlines() if "ResNet1D-34" in ln][0]
+    # a code change without new runs: every builder row says so instead of quoting the old numbers
+    monkeypatch.setattr(readme, "_same_code", lambda a, b: False)
+    stale = readme.render_headline(str(p))
+    assert "median" not in [ln for ln in stale.splitlines() if "driver's command" in ln][0]

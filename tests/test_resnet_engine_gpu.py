@@ -127,22 +127,26 @@ def test_engine_multi_tile_forward_matches_one_tile(mode):
     towards the stem (the kernel-level equality is pinned by test_conv1d_nlc_stats_multi_tile)."""
     from crossscale_ecg.ops import conv_mc
     prev = conv_mc.set_multi_tile(0)
+    # the 128-channel stage convs go to the tap-shared kernel by default: off here, so mode 2 still covers their
+    # multi-tile path (advisor r4)
+    prev_tap = conv_mc.set_tap_shared(0)
     try:
-        one = conv_mc.stat_rows(1024 * 125, 64)
+        one = conv_mc.stat_rows(1024, 125, 64, 125, 64)
         m0, _, eng0, x, y = _setup(18, B=1024, use_graph=False, seed=5)
         eng0.forward_backward()
         torch.cuda.synchronize()
         conv_mc.set_multi_tile(mode)
-        multi = conv_mc.stat_rows(1024 * 125, 64)
+        multi = conv_mc.stat_rows(1024, 125, 64, 125, 64)
         assert multi < one == 1000, (multi, one)
         if mode == 2:
-            assert conv_mc.stat_rows(1024 * 63, 128) < (1024 * 63 + 127) // 128
+            assert conv_mc.stat_rows(1024, 63, 128, 63, 128) < (1024 * 63 + 127) // 128
         m1, _, eng1, _, _ = _setup(18, B=1024, use_graph=False, seed=5)
         eng1.set_batch(x, y)
         eng1.forward_backward()
         torch.cuda.synchronize()
     finally:
         conv_mc.set_multi_tile(prev)
+        conv_mc.set_tap_shared(prev_tap)
     assert abs(eng0.avg_loss() - eng1.avg_loss()) < 1e-3
     errs = {n: _rel(p1.grad, p0.grad) for (n, p0), (_, p1) in zip(m0.named_parameters(), m1.named_parameters())}
     assert errs["fc.weight"] < 1e-2 and errs["fc.bias"] < 1e-2, errs  # head: a few bf16 flips deep
