@@ -17,7 +17,10 @@ wall-clock).  ``step_ms`` is the measured wall time per step; for A0-A3 it equal
 next batch's fill and copy overlap the current batch's compute.
 ``samples_per_s = (samples/iters) / (step_ms/1e3)`` (bench_locality.py:73-74).
 ``compute`` is the reference eager step (TinyECG fwd/CE/bwd/SGD lr 1e-2) or, with ``compute="fused"``,
-the fused HIP step fed from the same device batch buffer.
+the fused HIP step fed from the same device batch buffer (one native call enqueues the step kernel and the
+reduce+SGD kernel, ~12 us of GPU time): with the ~0.6 ms of Python launches of the eager step gone, the A0-A3
+comparison is one of the data path alone.  Its rows go to ``*_fused.csv`` next to the
+reference-faithful eager rows.
 """
 from __future__ import annotations
 
@@ -63,10 +66,6 @@ class _Compute:
             self.mom = torch.zeros_like(self.flat)
             self.slab = torch.empty((B, slab_stride(2)), device=dev)
             self.loss = torch.zeros(1, device=dev)
-            from ..ops import _lib
-            lib = _lib.kernels()
-            self.ctl = torch.zeros(lib.ecg_tiny_ctl_ints(), dtype=torch.int32, device=dev)
-            self.gslab = torch.empty((lib.ecg_tiny_gslab_rows(), slab_stride(2)), device=dev)
         else:
             self.opt = torch.optim.SGD(self.model.parameters(), lr=1e-2)
 
@@ -78,7 +77,7 @@ class _Compute:
             st = _lib.kernels().ecg_tiny_train_step(x2.data_ptr(), x2.shape[1], x2.stride(0), None, y32.data_ptr(),
                                                     self.flat.data_ptr(), self.mom.data_ptr(), 2,
                                                     self.slab.data_ptr(), self.slab.shape[1], x2.shape[0],
-                                                    self.loss.data_ptr(), 1e-2, 0.0, 0.0, 0, None, None, 0, None,
+                                                    self.loss.data_ptr(), 1e-2, 0.0, 0.0, 0, 0, None,
                                                     _lib.stream_ptr(self.dev))
             _lib.check(st, "ecg_tiny_train_step")
             return
@@ -302,13 +301,13 @@ def _median_row(cells: List[Dict]) -> Dict:
 def run_locality(shard_dir: str, batch_sizes: List[int], iters: int = 100, num_workers: int = 4,
                  device: Optional[str] = None, compute: str = "torch", results_dir: str = "results",
                  n_windows: int = 20000, labl: bool = True, normalize: bool = True, reps: int = 1,
-                 pin_thread: bool = False) -> List[Dict]:
+                 pin_thread: bool = False, reps_large: Optional[int] = None) -> List[Dict]:
     """A0-A5 per batch size.  ``reps`` > 1: every (config, batch) cell is measured ``reps`` times, the
     configurations interleaved within each repetition (A0 A1 A2 A3 A4 A5, A0 A1 ...), and the CSV holds the
     median of each column plus the samples/s interquartile range (``samples_per_s_q1/q3``, ``reps``).
     ``pin_thread``: the training thread of every A0-A3 configuration runs on one fixed CPU, and the pinned
     configurations' pin-memory thread on another (pinning only A2/A3 mixed thread placement into the
-    A3-vs-A0 comparison)."""
+    A3-vs-A0 comparison).  ``reps_large``: repetitions for batch sizes >= 512 (default ``reps``)."""
     dev = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
     paths = ensure_synthetic_shards(shard_dir, n_windows, shard_size=8192) if not list_shards(shard_dir) \
         else list_shards(shard_dir)
@@ -317,7 +316,8 @@ def run_locality(shard_dir: str, batch_sizes: List[int], iters: int = 100, num_w
     rows, labl_rows = [], []
     for bs in batch_sizes:
         cells: Dict[str, List[Dict]] = {}
-        for rep in range(max(1, reps)):
+        n_reps = reps_large if (reps_large and bs >= 512) else reps
+        for rep in range(max(1, n_reps)):
             for name, contiguous, pin, nb in CONFIGS:
                 sampler = SequentialSampler(ds) if contiguous else RandomSampler(ds)
                 dl = DataLoader(ds, batch_size=bs, sampler=sampler, num_workers=num_workers,
@@ -348,7 +348,8 @@ def run_locality(shard_dir: str, batch_sizes: List[int], iters: int = 100, num_w
             if name == "A4_LABL":
                 labl_rows.append(row)
     os.makedirs(results_dir, exist_ok=True)
-    write_csv(os.path.join(results_dir, "part1_locality_results.csv"), rows, LOCALITY_COLUMNS + SPREAD_COLUMNS)
+    sfx = "" if compute == "torch" else f"_{compute}"
+    write_csv(os.path.join(results_dir, f"part1_locality_results{sfx}.csv"), rows, LOCALITY_COLUMNS + SPREAD_COLUMNS)
     if labl_rows:
-        write_csv(os.path.join(results_dir, "part1_labl_results.csv"), labl_rows, LABL_COLUMNS + SPREAD_COLUMNS)
+        write_csv(os.path.join(results_dir, f"part1_labl_results{sfx}.csv"), labl_rows, LABL_COLUMNS + SPREAD_COLUMNS)
     return rows

@@ -214,14 +214,15 @@ def run_part2(results_dir: str = "results", gpu: bool = True, cpu: bool = True, 
     out: Dict[str, List[Dict]] = {}
     nthreads = nthreads or usable_cpus()
     if gpu and torch.cuda.is_available():
-        # one untimed pass of the grid's first cell: its kernels, MIOpen's solver choice, the host flag page and
-        # the allocator are cold on the first call, which inflated the first timed cell (round 3: HIP 18.1 us at
-        # B=64, K=3 against 9.0-11.8 us in every other cell)
-        bench_pair_gpu(batch_sizes[0], kernel_sizes[0], np.random.default_rng(7), max(3, trials // 5))
+        # every cell gets an untimed pass of its own right before it is timed: its kernels, MIOpen's solver choice
+        # for that shape, the host flag page and the allocator are cold on a cell's first calls (round 3: HIP 18.1 us
+        # at B=64, K=3 against 9.0-11.8 us elsewhere; round 4, warming only the first cell: torch 77/84 us at B=64,
+        # K=3/5 against 33-37 us elsewhere - VERDICT r4 weak #5)
         rng = np.random.default_rng(1337)
         rows, raw = [], []
         for bs in batch_sizes:
             for K in kernel_sizes:
+                bench_pair_gpu(bs, K, np.random.default_rng(7), max(3, trials // 5))
                 row, r = bench_pair_gpu(bs, K, rng, trials)
                 rows.append(row)
                 raw += [{"batch_size": bs, "kernel_size": K, "trial": i, "torch_ms": a, "omp_ms": b}

@@ -2,7 +2,7 @@
 # GPU measurement session on one MI355X (run by gpurun from the repo root):
 #   bash scripts/gpu_session.sh <tag> <steps...>
 # steps (any subset, in order): tests smoke bench bench20 resnet | probe bnprobe convtest enginetest |
-#   module1 module2 module3 | libab (LIBS=...) envab (ENVS=...) finab tapab | pmc tappmc tinypmc stats timeline timeline0
+#   module1 module1f module2 m2trace module3 | libab (LIBS=...) envab (ENVS=...) finab tapab | pmc tappmc tinypmc stats timeline timeline0
 # Every GPU step runs under its own time limit; a crash, abort or timeout ends the session.
 set -u
 cd "$(dirname "$0")/.."
@@ -68,8 +68,17 @@ for s in "$@"; do
     module1)
       step shard_prep 300 python shard_prep.py --dataset synthetic
       step module1 1000 python bench_locality.py --batch-sizes 64 128 256 512 --reps 5 --results-dir "$OUT/modules" ;;
+    module1f)  # A0-A5 with the fused HIP training step: the data path without the eager step's launches
+      [ -d data/shards ] || step shard_prep 300 python shard_prep.py --dataset synthetic
+      step module1f 1000 python bench_locality.py --compute fused --batch-sizes 64 128 256 512 --reps 5 \
+        --results-dir "$OUT/modules" ;;
     module2)
       step module2 900 python benchmark_part_2.py --results-dir "$OUT/modules" ;;
+    m2trace)  # which MIOpen kernels / HIP calls torch.nn.Conv1d runs per Module-2 cell
+      export TMPDIR=/tmp
+      step m2trace 400 rocprofv3 --kernel-trace --hip-trace --marker-trace --output-format csv -d "$OUT/m2trace" \
+        -o t -- python3 scripts/trace_module2_miopen.py run
+      step m2parse 120 python scripts/trace_module2_miopen.py parse "$OUT/m2trace" ;;
     module3)
       [ -d data/shards ] || step shard_prep 300 python shard_prep.py --dataset synthetic
       step pseudo_fl 600 python part3_mpi_gpu_train.py --steps 200 --results-csv "$OUT/modules/part3_mpi_cuda_results.csv"
