@@ -207,6 +207,29 @@ HIP_COLUMNS = ["batch_size", "kernel_size", "backend", "torch_ms_median", "torch
                "hip_ev_ms", "speedup_ev", "max_abs_err"]
 
 
+def steady_host_for_single_calls() -> Dict[str, object]:
+    """Host settings for the single-call (``time_once``) GPU timings, applied before the HIP context exists:
+    * ``hipSetDeviceFlags(hipDeviceScheduleSpin)``: ``torch.cuda.synchronize()`` spins instead of yielding the CPU,
+      as the HIP op's own completion wait already does (host-flag spin) - so both sides pay the same wake-up cost;
+    * the timing thread pinned to one CPU of its affinity set (no migration between the call and the sync).
+    Round 4/5 traces (scripts/trace_module2_miopen.py, profiles/r5/module2_miopen_trace.txt) show ONE MIOpen solver
+    (``naive_conv_ab_nonpacked_fwd_nchw``, ~5 us of device time) in every cell; the 32-108 us spread of torch's
+    single calls inside one cell is host-side (MIOpen's ~40 us per-call host path plus the synchronize wake-up).
+    Returns what was applied (recorded next to the CSV)."""
+    import ctypes
+    rec: Dict[str, object] = {"spin_sync": False, "pinned_cpu": None}
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        rec["spin_sync"] = hip.hipSetDeviceFlags(ctypes.c_uint(1)) == 0  # hipDeviceScheduleSpin
+    except OSError:
+        pass
+    cpus = sorted(os.sched_getaffinity(0))
+    if len(cpus) > 1:
+        os.sched_setaffinity(0, {cpus[0]})
+        rec["pinned_cpu"] = cpus[0]
+    return rec
+
+
 def run_part2(results_dir: str = "results", gpu: bool = True, cpu: bool = True, trials: int = TRIALS,
               nthreads: int | None = None, batch_sizes=BATCH_SIZES, kernel_sizes=KERNEL_SIZES,
               verbose: bool = True) -> Dict[str, List[Dict]]:
@@ -214,6 +237,10 @@ def run_part2(results_dir: str = "results", gpu: bool = True, cpu: bool = True, 
     out: Dict[str, List[Dict]] = {}
     nthreads = nthreads or usable_cpus()
     if gpu and torch.cuda.is_available():
+        prev_aff = os.sched_getaffinity(0)
+        host = steady_host_for_single_calls()
+        if verbose:
+            print(f"[HIP] single-call host settings: {host}", flush=True)
         # every cell gets an untimed pass of its own right before it is timed: its kernels, MIOpen's solver choice
         # for that shape, the host flag page and the allocator are cold on a cell's first calls (round 3: HIP 18.1 us
         # at B=64, K=3 against 9.0-11.8 us elsewhere; round 4, warming only the first cell: torch 77/84 us at B=64,
@@ -235,6 +262,7 @@ def run_part2(results_dir: str = "results", gpu: bool = True, cpu: bool = True, 
         safe_write_csv(rows, os.path.join(results_dir, "part2_hip_results.csv"), HIP_COLUMNS)
         safe_write_csv(raw, os.path.join(results_dir, "part2_hip_results_raw.csv"), PART2_RAW_COLUMNS)
         out["hip"] = rows
+        os.sched_setaffinity(0, prev_aff)  # the CPU comparison below sweeps thread counts
     if cpu:
         rng = np.random.default_rng(1337)
         torch.set_num_threads(nthreads)

@@ -277,7 +277,7 @@ struct TinySample {
     red = reinterpret_cast<float*>(smem + sm.red_off);
     tid = threadIdx.x;
     lane = tid & 63;
-    w = tid >> 6;
+    w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: w-derived bounds, taps and loops stay scalar
     h = lane >> 4;
     c = lane & 15;
   }
