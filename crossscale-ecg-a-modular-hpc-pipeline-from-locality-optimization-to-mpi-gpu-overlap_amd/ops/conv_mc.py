@@ -37,6 +37,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_set_big", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_set_mt", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_set_tap", [i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_set_tap64", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_set_dma_dil", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_ex", [vp] * 7 + [i32] * 10 + [vp, vp, vp, vp])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles", [_lib.C.c_long, i32])
@@ -67,6 +68,13 @@ def set_tap_shared(mode: int) -> int:
     """Tap-shared 256-row forward/data-grad kernel for stride-1 pad-1 3-tap convs (0: off, 1 (default): outputs with
     C_out % 128 == 0, 2: also 64-channel outputs); returns the previous mode.  Build step plans after setting it."""
     return _lib_k().ecg_conv1d_nlc_set_tap(int(mode))
+
+
+def set_tap64(on: bool) -> int:
+    """Persistent 64-channel tap kernel (weights resident in LDS, A' images streamed per 128-row tile, one partial
+    row per workgroup) for C_in == C_out == 64 stride-1 3-tap convs (True, default) or the one-tap kernels; returns
+    the previous setting.  Build step plans after setting it."""
+    return _lib_k().ecg_conv1d_nlc_set_tap64(1 if on else 0)
 
 
 def set_multi_tile(mode: int) -> int:

@@ -1094,6 +1094,166 @@ __global__ __launch_bounds__(512, 1) void conv1d_nlc_fwd_tap_kernel(FwdArgs a, i
   }
 }
 
+// ------------------------------------------------------------------ persistent tap-shared 64-channel kernel
+// The 64-channel stage (C_in = C_out = 64, stride 1, pad 1, 3 taps: every conv of ResNet layer1, forward AND
+// data-grad) is a thin GEMM - N = 64, K = 192 - over M = B*L = 128,000 rows at B=1024: 3.1 GFLOP against 33 MB of
+// activations in and out, so it is bound by moving rows, not by the MFMA.  The one-tap multi-tile kernel re-stages
+// the activation rows once per tap and the 64x64 weight tile every K step; here each workgroup
+//   * keeps the whole 3 x 64 x 64 weight image resident in LDS for the launch (DMA'd once),
+//   * walks M tiles gm, gm + GM, ... (persistent grid, two workgroups per CU), staging each tile's activation rows
+//     ONCE as a 136-row A' image (rows m0-1 .. m0+128, read by the three taps at row offsets 0/1/2, as the
+//     256-row tap-shared kernel does) in a two-slot ring: tile j+1's image lands while tile j's MFMAs and
+//     epilogue run,
+//   * stores each tile through its own LDS staging region (fwd_epi_tile_rowwise: bias / residual / masks / ReLU /
+//     BatchNorm partials, the same epilogue as every other kernel here) and accumulates the BatchNorm partials of
+//     all its tiles into ONE partial row (row gm of GM), finalized by the fused tail.
+// 4 waves as 2 (M) x 2 (N), wave tile 64 x 32.  LDS: weights 24 KB | A' slots 2 x 17 KB | epilogue 19.5 KB = 77.5 KB.
+constexpr int T64_BM = 128;
+constexpr int T64_AROWS = 136;                 // 17 DMA pieces of 8 rows (130 used)
+constexpr int T64_ASLOT = T64_AROWS * 128;     // 17,408 B
+constexpr int T64_WBYTES = 3 * 64 * 128;       // 24,576 B
+using T64Cfg = FwdCfg<T64_BM, 64, 2>;
+constexpr int T64_SMEM = T64_WBYTES + 2 * T64_ASLOT + T64Cfg::EP_BYTES;
+static_assert(2 * T64_SMEM <= 160 * 1024, "two workgroups per CU");
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void conv1d_nlc_tap64_kernel(FwdArgs a, int MT, int GM) {
+  constexpr int BM = T64_BM, BN = 64, NWR = 2, NW = 4;
+  constexpr int WM = T64Cfg::WM, WN = T64Cfg::WN, FM = T64Cfg::FM, FN = T64Cfg::FN;
+  static_assert(WM == 64 && WN == 32 && FM == 4 && FN == 2, "64 x 32 wave tiles");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* const Ws = smem;
+  unsigned char* const As = smem + T64_WBYTES;
+  unsigned char* const eps = As + 2 * T64_ASLOT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wv >> 1, wc = wv & 1;
+  const int gm = blockIdx.x;
+  const int L = a.Lout, M = a.B * L;
+  const int ntiles = gm < MT ? (MT - gm + GM - 1) / GM : 0;
+  const srd_t xr = make_rsrc(a.x, (long)M * 64 * 2);
+  const srd_t wrs = make_rsrc(a.w, 64L * 192 * 2);
+  const unsigned ldsW = lds_addr(Ws), ldsA = lds_addr(As);
+  // weight image [tap k][row n][64 ch], 16-B chunk cc of row n at cc ^ (n & 7): 24 pieces (k, 8-row block), 6 per
+  // wave; the XOR goes on the SOURCE chunk (the DMA writes lane-linear)
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int p = wv + NW * i, k = p >> 3, n = 8 * (p & 7) + (lane >> 3);
+    dma16_at(wrs, (unsigned)(n * 384 + k * 128 + (((lane & 7) ^ (n & 7)) << 4)), ldsW + p * 1024);
+  }
+  // A' image of the tile at m0: image row r <-> global row m0 - 1 + r; pieces p = wv + 4i (i < 4) and, by every
+  // wave with lanes 8wv .. 8wv+7 only, row 128 + wv (rows 128..131: 128 and 129 are used)
+  auto issue_a = [&](int m0, int slot) {
+    const unsigned base = ldsA + slot * T64_ASLOT;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int row = i < 4 ? 8 * (wv + NW * i) + (lane >> 3) : 128 + (lane >> 3);
+      const int g = m0 - 1 + row;
+      const unsigned off = (g >= 0 && g < M) ? (unsigned)(g * 128 + ((((lane & 7) ^ (row & 7))) << 4)) : 0x7ffffff0u;
+      if (i < 4)
+        dma16_at(xr, off, base + (wv + NW * i) * 1024);
+      else if ((lane >> 3) == wv)
+        dma16_at(xr, off, base + 16 * 1024);
+    }
+  };
+  EpiConst k;
+  k.load<EPI == 1>(a, EpiLane<BN, NWR>::n(0));
+  const int arow = (wr * WM + (lane & 15)) * 128, brow = (wc * WN + (lane & 15)) * 128;
+  if (ntiles > 0) issue_a(gm * BM, 0);
+  for (int j = 0; j < ntiles; ++j) {  // block-uniform
+    const int m0 = (gm + j * GM) * BM;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of A'(j) (and, at j = 0, W) landed
+    __syncthreads();                                  // ... every wave's; slot (j+1)&1 is no longer read
+    if (j + 1 < ntiles) issue_a((gm + (j + 1) * GM) * BM, (j + 1) & 1);
+    const unsigned char* Aj = As + (j & 1) * T64_ASLOT;
+    unsigned ok0 = 0u, ok2 = 0u;  // tap 0 reads the previous sample at t == 0, tap 2 the next at t == L-1
+#pragma unroll
+    for (int f = 0; f < FM; ++f) {
+      const int m = m0 + wr * WM + 16 * f + (lane & 15);
+      const int t = m - (m / L) * L;
+      ok0 |= (t != 0 ? 1u : 0u) << f;
+      ok2 |= (t != L - 1 ? 1u : 0u) << f;
+    }
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int f = 0; f < FM; ++f)
+#pragma unroll
+      for (int q = 0; q < FN; ++q) acc[f][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 3; ++tap) {
+      const unsigned char* Bs = Ws + tap * 8192;
+      const unsigned okm = tap == 0 ? ok0 : ok2;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int cc = 4 * ks + (lane >> 4);
+        const int asw = (cc ^ ((lane + tap) & 7)) << 4, bsw = (cc ^ (lane & 7)) << 4;
+        bf16x8 af[FM], bfr[FN];
+#pragma unroll
+        for (int f = 0; f < FM; ++f) {
+          af[f] = *reinterpret_cast<const bf16x8*>(Aj + arow + (16 * f + tap) * 128 + asw);
+          if (tap != 1 && !((okm >> f) & 1u)) af[f] = bf16x8{};
+        }
+#pragma unroll
+        for (int q = 0; q < FN; ++q) bfr[q] = *reinterpret_cast<const bf16x8*>(Bs + brow + 16 * q * 128 + bsw);
+#pragma unroll
+        for (int f = 0; f < FM; ++f)
+#pragma unroll
+          for (int q = 0; q < FN; ++q)
+            acc[f][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f], bfr[q], acc[f][q], 0, 0, 0);
+      }
+    }
+    // tile j's output through the epilogue's own LDS region (A'(j+1) keeps landing in its slot meanwhile)
+    fwd_epi_tile_rowwise<BM, BN, EPI, NWR>(a, acc, eps, k, m0, 0, L, M, 1, 0);
+  }
+  if (a.stats) {
+    fwd_epi_stats<BM, BN, EPI, NWR>(a, eps, k, 0, gm, GM);
+    if (a.tail) ecg::bn_tail<T64Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, GM, a.Cout, gm, 0, BN, smem);
+  }
+}
+
+// ECG_CONV_TAP64=0|1: the persistent 64-channel tap kernel (1, default) for C_in == C_out == 64 stride-1 3-tap
+// convs over whole samples; 0: the one-tap multi-tile kernel.  Read once.
+int g_conv_tap64 = -1;
+inline bool conv_tap64() {
+  if (g_conv_tap64 < 0) {
+    const char* e = getenv("ECG_CONV_TAP64");
+    g_conv_tap64 = e ? atoi(e) : 1;
+  }
+  return g_conv_tap64 != 0;
+}
+inline bool tap64_ok(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad, int in_dil) {
+  return conv_tap64() && Cin == 64 && Cout == 64 && Kw == 3 && stride == 1 && pad == 1 && in_dil == 1 && Lin == Lout &&
+         Lout >= 2 && (long)B * Lout * 64 * 2 < 0x7fff0000L;
+}
+inline int tap64_groups(int B, int Lout) {
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev))
+      cus = 256;
+  }
+  const int MT = (int)(((long)B * Lout + T64_BM - 1) / T64_BM);
+  return MT < 2 * cus ? MT : 2 * cus;
+}
+
+template <int EPI>
+int launch_tap64_t(const FwdArgs& a, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_tap64_kernel<EPI>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, T64_SMEM));
+    attr = true;
+  }
+  const int MT = (int)(((long)a.B * a.Lout + T64_BM - 1) / T64_BM), GM = tap64_groups(a.B, a.Lout);
+  hipLaunchKernelGGL((conv1d_nlc_tap64_kernel<EPI>), dim3((unsigned)GM), dim3(256), T64_SMEM, stream, a, MT, GM);
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
+}
+
+int launch_tap64(const FwdArgs& a, hipStream_t stream) {
+  return a.stat_mode == 1 ? launch_tap64_t<1>(a, stream) : launch_tap64_t<0>(a, stream);
+}
+
 // The tap-shared kernel applies to stride-1, pad-1, 3-tap convs over whole samples with BN | C_out (BN = 128 when
 // C_out % 128 == 0, else 64) and 32-bit addressable operands.
 inline bool tap_ok(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad, int in_dil) {
@@ -2101,6 +2261,7 @@ ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bia
   }
   a.tail = static_cast<const ecg::BnTail*>(tail);
   a.apply = static_cast<const ecg::BnApply*>(apply);
+  if (!apply && tap64_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return launch_tap64(a, stream);
   if (conv_tap(Cout) && tap_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return launch_fwd_tap(a, stream);
   int bm, bn;
   pick_fwd_tile((long)B * Lout, Cout, in_dil, &bm, &bn);
@@ -2121,6 +2282,14 @@ ECG_API int ecg_conv1d_nlc_tap_apply_ok(int B, int Lin, int Cin, int Lout, int C
   const bool ok = BN == 128 ? tap_grid_resident<128, 1>(grid) && tap_grid_resident<128, 0>(grid)
                             : tap_grid_resident<64, 1>(grid) && tap_grid_resident<64, 0>(grid);
   return ok ? 1 : 0;
+}
+
+// Persistent 64-channel tap kernel on (1) / off (0); returns the previous setting (tests, A/B).  Step plans size
+// their BatchNorm partial rows when built: set it first.
+ECG_API int ecg_conv1d_nlc_set_tap64(int on) {
+  const int prev = conv_tap64() ? 1 : 0;
+  g_conv_tap64 = on ? 1 : 0;
+  return prev;
 }
 
 // Strided data-grads on the LDS-DMA loop (1) or the register-staged loop (0); returns the previous setting (tests).
@@ -2166,6 +2335,7 @@ ECG_API int ecg_conv1d_nlc_fwd_stat_tiles(long M, int Cout) {
 ECG_API int ecg_conv1d_nlc_fwd_stat_tiles_ex(int B, int Lout, int Cout, int in_dil);
 ECG_API int ecg_conv1d_nlc_fwd_stat_rows(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad,
                                          int in_dil) {
+  if (tap64_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return tap64_groups(B, Lout);
   if (conv_tap(Cout) && tap_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return tap_mtiles(B, Lout);
   return ecg_conv1d_nlc_fwd_stat_tiles_ex(B, Lout, Cout, in_dil);
 }

@@ -175,6 +175,7 @@ def test_conv1d_nlc_stats_multi_tile(mode, B, L, C):
     x = torch.randn(B, L, C, device="cuda").bfloat16()
     w = (torch.randn(C, 3, C, device="cuda") * 0.05).bfloat16()
     prev = conv_mc.set_multi_tile(0)
+    prev64 = conv_mc.set_tap64(False)  # the 64-channel shapes go to the persistent tap kernel by default
     try:
         y0, _ = conv_mc.fwd_stats_raw(x, w, 1, 1, L)
         conv_mc.set_multi_tile(mode)
@@ -182,6 +183,7 @@ def test_conv1d_nlc_stats_multi_tile(mode, B, L, C):
         torch.cuda.synchronize()
     finally:
         conv_mc.set_multi_tile(prev)
+        conv_mc.set_tap64(prev64)
     assert torch.equal(y, y0)
     if mode == 1 and C == 64 or mode == 2:
         assert stats.shape[1] < (B * L + 127) // 128  # the multi-tile kernel ran (fewer partial rows than tiles)
@@ -208,6 +210,7 @@ def test_tap_shared_forward_matches_fp64(B, L, Cin, Cout):
     statistics of its own stored outputs."""
     from crossscale_ecg.ops import conv_mc
     prev = conv_mc.set_tap_shared(2)
+    prev64 = conv_mc.set_tap64(False)
     try:
         torch.manual_seed(11)
         x = torch.randn(B, L, Cin, device=DEV).bfloat16()
@@ -218,6 +221,7 @@ def test_tap_shared_forward_matches_fp64(B, L, Cin, Cout):
         assert stats.shape[1] == (B * L + 255) // 256  # one partial row per 256-row tile
     finally:
         conv_mc.set_tap_shared(prev)
+        conv_mc.set_tap64(prev64)
     ref = F.conv1d(x.double().transpose(1, 2), w.double().permute(0, 2, 1), None, stride=1, padding=1)
     got = y.double().transpose(1, 2)
     assert (got - ref).abs().max().item() <= 8e-3 * ref.abs().max().item()
@@ -226,3 +230,47 @@ def test_tap_shared_forward_matches_fp64(B, L, Cin, Cout):
     yf = ys.float().reshape(-1, Cout)
     assert torch.allclose(stats[0].sum(0), yf.sum(0), rtol=1e-4, atol=1e-2)
     assert torch.allclose(stats[1].sum(0), (yf * yf).sum(0), rtol=1e-4, atol=1e-2)
+
+
+TAP64_CASES = [  # C_in == C_out == 64 stride-1 3-tap convs on the persistent 64-channel kernel
+    (1024, 125, 1.0),  # the ResNet layer-1 shape: 1000 tiles over 512 workgroups
+    (3, 37, 1.0),  # ragged last tile (111 rows), one workgroup
+    (7, 2, 1.0),  # L = 2: every row is a sample boundary for an outer tap
+    (700, 125, 1.0),  # 684 tiles: some workgroups walk one tile, some two
+    (64, 125, 0.0),  # zero activations: exactly zero outputs and statistics
+]
+
+
+@pytest.mark.parametrize("B,L,scale", TAP64_CASES)
+def test_tap64_forward_matches_fp64(B, L, scale):
+    """The persistent 64-channel tap kernel (weights resident in LDS, each workgroup walking M tiles with the next
+    tile's A' image landing under the current tile's MFMAs and epilogue) against an fp64 conv of the same bf16
+    inputs; its per-workgroup BatchNorm partial rows against the statistics of its own stored outputs; the one-tap
+    kernels' outputs agree to bf16 rounding."""
+    from crossscale_ecg.ops import conv_mc
+    torch.manual_seed(5)
+    x = (torch.randn(B, L, 64, device=DEV) * scale).bfloat16()
+    w = (torch.randn(64, 3, 64, device=DEV) / 192 ** 0.5).bfloat16()
+    prev = conv_mc.set_tap64(True)
+    try:
+        y = conv_mc.fwd_raw(x, w, None, 1, 1, L)
+        ys, stats = conv_mc.fwd_stats_raw(x, w, 1, 1, L)
+        conv_mc.set_tap64(False)
+        y1 = conv_mc.fwd_raw(x, w, None, 1, 1, L)
+        torch.cuda.synchronize()
+    finally:
+        conv_mc.set_tap64(prev)
+    tiles = (B * L + 127) // 128
+    assert stats.shape[1] == min(tiles, 2 * torch.cuda.get_device_properties(0).multi_processor_count)
+    assert torch.equal(y, ys)
+    ref = F.conv1d(x.double().transpose(1, 2), w.double().permute(0, 2, 1), None, stride=1, padding=1)
+    got = y.double().transpose(1, 2)
+    if scale == 0.0:
+        assert not y.abs().any() and not stats.abs().any()
+        return
+    assert (got - ref).abs().max().item() <= 8e-3 * ref.abs().max().item()
+    assert _rel(got, ref) < 4e-3
+    assert _rel(y.double(), y1.double()) < 4e-3
+    yf = ys.double().reshape(-1, 64)
+    torch.testing.assert_close(stats[0].double().sum(0), yf.sum(0), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(stats[1].double().sum(0), (yf * yf).sum(0), rtol=1e-5, atol=1e-3)

@@ -127,9 +127,10 @@ def test_engine_multi_tile_forward_matches_one_tile(mode):
     towards the stem (the kernel-level equality is pinned by test_conv1d_nlc_stats_multi_tile)."""
     from crossscale_ecg.ops import conv_mc
     prev = conv_mc.set_multi_tile(0)
-    # the 128-channel stage convs go to the tap-shared kernel by default: off here, so mode 2 still covers their
-    # multi-tile path (advisor r4)
+    # the 128-channel stage convs go to the tap-shared kernel and the 64-channel ones to the persistent 64-channel
+    # kernel by default: both off here, so the multi-tile path stays covered (advisor r4)
     prev_tap = conv_mc.set_tap_shared(0)
+    prev64 = conv_mc.set_tap64(False)
     try:
         one = conv_mc.stat_rows(1024, 125, 64, 125, 64)
         m0, _, eng0, x, y = _setup(18, B=1024, use_graph=False, seed=5)
@@ -147,6 +148,7 @@ def test_engine_multi_tile_forward_matches_one_tile(mode):
     finally:
         conv_mc.set_multi_tile(prev)
         conv_mc.set_tap_shared(prev_tap)
+        conv_mc.set_tap64(prev64)
     assert abs(eng0.avg_loss() - eng1.avg_loss()) < 1e-3
     errs = {n: _rel(p1.grad, p0.grad) for (n, p0), (_, p1) in zip(m0.named_parameters(), m1.named_parameters())}
     assert errs["fc.weight"] < 1e-2 and errs["fc.bias"] < 1e-2, errs  # head: a few bf16 flips deep
