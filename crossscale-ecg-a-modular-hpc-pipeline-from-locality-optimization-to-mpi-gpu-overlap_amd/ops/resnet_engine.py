@@ -9,12 +9,15 @@ BASELINE.json config 5 (ResNet1D-34 stress, bf16, large batch).  Design (MI355X-
   transposes, no MIOpen), all shapes fixed at construction so every pointer is baked into the plan;
 * every conv is an MFMA implicit GEMM (conv1d_mc.hip) whose epilogue also emits the BatchNorm statistics;
   BN apply / backward passes are fused with ReLU and the residual;
-* fused apply (``fuse_apply``, default on for single-GPU plans): where a conv runs on the tap-shared kernel with
-  its whole grid resident, the BatchNorm that consumes its statistics is applied INSIDE the same launch once the
-  launch's own tail has finalized it (conv1d_mc.hip fwd_epi_apply_rowwise, bn_tail.h BnApply): the forward BN+ReLU
-  (+ residual) pass after conv1 / conv2 and the backward dz pass after each data-grad conv disappear from the
-  plan with their kernel boundaries.  Off when collectives may run concurrently with the step (DDP buckets,
-  tail FedAvg): a collective's kernel holding a CU could keep a grid-wide wait from completing;
+* fused apply (``fuse_apply`` = "fwd" (default for single-GPU plans) / "bwd" / "all" / "none"): where a conv runs on
+  the tap-shared kernel with its whole grid resident, the BatchNorm that consumes its statistics is applied INSIDE
+  the same launch once the launch's own tail has finalized it (conv1d_mc.hip fwd_epi_apply_rowwise, bn_tail.h
+  BnApply): the forward BN+ReLU (+ residual) pass after conv1 / conv2, and with "bwd" the dz pass after each
+  data-grad conv, disappear from the plan with their kernel boundaries.  The backward ones are off by default: the
+  side lane's weight-gradient workgroups hold CUs while a data-grad launch's workgroups wait for their last one
+  (ResNet1D-34 B=1024: 4.79 ms/step with every apply fused vs 3.44 without, profiles/r5/resnet_apply_ab.txt).  Off
+  when collectives may run concurrently with the step (DDP buckets, tail FedAvg): a collective's kernel holding a
+  CU could keep a grid-wide wait from completing;
 * backward is laid out in ``segments`` = gradient buckets of ~``bucket_mb`` (default 4 MB, closed at block
   boundaries; layer1 joins the stem's).  The gradients of a segment form one contiguous range of the flat grad
   buffer, so each range is all-reduced on a comm stream while the next segment runs (``run_segments``: the DDP
@@ -99,7 +102,7 @@ class ResNetStepEngine:
                  momentum: float = 0.9, weight_decay: float = 0.0, nesterov: bool = False, use_graph: bool = True,
                  grad_sync: Optional[Callable[[torch.Tensor], None]] = None,
                  source: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None,
-                 bucket_mb: Optional[float] = None, fuse_apply: Optional[bool] = None):
+                 bucket_mb: Optional[float] = None, fuse_apply=None):
         dev = next(model.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("ResNetStepEngine needs a GPU (HIP kernels)")
@@ -135,8 +138,13 @@ class ResNetStepEngine:
             bucket_mb = float(os.environ.get("ECG_RESNET_BUCKET_MB", "4"))
         self.bucket_bytes = int(float(bucket_mb) * (1 << 20))
         if fuse_apply is None:
-            fuse_apply = os.environ.get("ECG_RESNET_APPLY", "1") != "0" and grad_sync is None
-        self.fuse_apply = bool(fuse_apply)
+            fuse_apply = os.environ.get("ECG_RESNET_APPLY", "fwd") if grad_sync is None else "none"
+        modes = {"0": "none", "none": "none", "false": "none", "fwd": "fwd", "bwd": "bwd", "1": "all", "all": "all",
+                 "true": "all"}
+        fuse_apply = modes.get(str(fuse_apply).lower())
+        if fuse_apply is None:
+            raise ValueError("fuse_apply must be one of none / fwd / bwd / all")
+        self.fuse_apply = fuse_apply  # which BatchNorm applies run inside their conv's launch
         self.apply_status = torch.zeros(4, dtype=torch.int32, device=dev)  # sticky: 1 = a fused apply timed out
         self._build()
 
@@ -347,9 +355,10 @@ class ResNetStepEngine:
         apply_dev = self._t(96 * 64, dtype=torch.uint8)
         self.n_fused_applies = 0
 
-        def apply_ok(Lin, Cin, Lout, Cout, K, s, p, dil=1) -> bool:
-            return self.fuse_apply and use_tail and bool(
-                self.lib.ecg_conv1d_nlc_tap_apply_ok(B, Lin, Cin, Lout, Cout, K, s, p, dil))
+        def apply_ok(Lin, Cin, Lout, Cout, K, s, p, dil=1, bwd=False) -> bool:
+            if self.fuse_apply not in ("all", "bwd" if bwd else "fwd"):
+                return False
+            return use_tail and bool(self.lib.ecg_conv1d_nlc_tap_apply_ok(B, Lin, Cin, Lout, Cout, K, s, p, dil))
 
         def apply_blob(out, scale=None, out_d=None, scale_d=None, res=None) -> int:
             blob = struct.pack("<6q", P(out), P(scale), P(out_d), P(scale_d), P(res), self.apply_status.data_ptr())
@@ -500,7 +509,7 @@ class ResNetStepEngine:
             # dgrad conv2 (stride 1, pad 1) -> ReLU-masked grad wrt a1 + BN1 backward statistics (+ the BN1 backward
             # apply in the same launch: dz1 directly, the masked gradient itself is never stored)
             T1 = rows(Lo, Co, Lo, Co, 3, 1, 1)
-            fuse_b1 = apply_ok(Lo, Co, Lo, Co, 3, 1, 1)
+            fuse_b1 = apply_ok(Lo, Co, Lo, Co, 3, 1, 1, bwd=True)
             conv(dz2, Lo, Co, self._wb[id(blk.conv2)], None if fuse_b1 else ga1, Lo, Co, 3, 1, 1, st=stats,
                  bnb=(a["a1"], a["z1"], b1.mean, b1.rstd, 0, 0, 0), tail_ptr=tail(T1, Co, [fin_bwd_words(b1, R, 1)]),
                  mbn=(b1.scale, b1.shift), apply_ptr=apply_blob(dz1, scale=b1.scale) if fuse_b1 else 0)
@@ -521,7 +530,7 @@ class ResNetStepEngine:
                 fins = [fin_bwd_words(pb2, B * Li, 1)] + ([fin_bwd_words(pbd, B * Li, 2)] if pbd else [])
                 # the previous block's BN2 (+ downsample BN) backward apply inside this launch: its dz2 / dzd directly
                 # (din, the masked gradient, is still stored: the previous block adds it as its identity residual)
-                fuse_b2 = apply_ok(Lo, Co, Li, Ci, 3, 1, 1, s)
+                fuse_b2 = apply_ok(Lo, Co, Li, Ci, 3, 1, 1, s, bwd=True)
                 app = 0
                 if fuse_b2:
                     pdz2, _, pdzd = dz_bufs(bi - 1)
