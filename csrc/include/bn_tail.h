@@ -59,30 +59,6 @@ struct BnTail {
   BnFin fin[2];
 };
 
-__device__ __forceinline__ void bn_fin_channel(const BnFin& f, int c, double v1, double v2) {
-  const double n = f.n;
-  if (f.mode == 0) {
-    const double mu = v1 / n;
-    const double var = fmax(v2 / n - mu * mu, 0.0);
-    const float rs = (float)(1.0 / sqrt(var + f.eps));
-    const float sc = f.gamma[c] * rs;
-    f.mean[c] = (float)mu;
-    f.rstd[c] = rs;
-    f.scale[c] = sc;
-    f.shift[c] = f.beta[c] - (float)mu * sc;
-    if (f.run_mean) {
-      const float m = (float)f.momentum;
-      f.run_mean[c] = (1.f - m) * f.run_mean[c] + m * (float)mu;
-      f.run_var[c] = (1.f - m) * f.run_var[c] + m * (float)(var * n / fmax(n - 1.0, 1.0));
-    }
-  } else {
-    if (f.dbeta) f.dbeta[c] = (float)v1;
-    if (f.dgamma) f.dgamma[c] = (float)v2;
-    f.c1[c] = (float)(v1 / n);
-    f.c2[c] = (float)(v2 / n);
-  }
-}
-
 __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -94,6 +70,30 @@ __device__ __forceinline__ void st_sc1(float* p, float v) {
 }
 __device__ __forceinline__ void st_sc1(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void bn_fin_channel(const BnFin& f, int c, double v1, double v2) {
+  const double n = f.n;
+  if (f.mode == 0) {
+    const double mu = v1 / n;
+    const double var = fmax(v2 / n - mu * mu, 0.0);
+    const float rs = (float)(1.0 / sqrt(var + f.eps));
+    const float sc = f.gamma[c] * rs;
+    f.mean[c] = (float)mu;
+    f.rstd[c] = rs;
+    st_sc1(f.scale + c, sc);  // write-through: a fused apply reads them inside this launch (sc1 loads)
+    st_sc1(f.shift + c, f.beta[c] - (float)mu * sc);
+    if (f.run_mean) {
+      const float m = (float)f.momentum;
+      f.run_mean[c] = (1.f - m) * f.run_mean[c] + m * (float)mu;
+      f.run_var[c] = (1.f - m) * f.run_var[c] + m * (float)(var * n / fmax(n - 1.0, 1.0));
+    }
+  } else {
+    if (f.dbeta) f.dbeta[c] = (float)v1;
+    if (f.dgamma) f.dgamma[c] = (float)v2;
+    st_sc1(f.c1 + c, (float)(v1 / n));
+    st_sc1(f.c2 + c, (float)(v2 / n));
+  }
 }
 
 // Called by EVERY thread of a statistics-producing workgroup after it stored its partial row (sc1) for M tile
@@ -162,11 +162,14 @@ __device__ __forceinline__ void bn_tail(const BnTail* __restrict__ tp, const flo
     }
   }
   for (int i = tid; i <= NG; i += NTHR) __hip_atomic_store(&cnt[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // publish the finalized coefficients to the launch's waiting workgroups (fused apply): every wave's stores of
-  // them completed, the workgroup's barrier, then ONE agent-scope release store of the ready flag
+  // publish the finalized coefficients to the launch's waiting workgroups (fused apply; guide G16, the sc1 form of
+  // the hand-off: no release / acquire fences): the coefficients were stored write-through by every wave and
+  // drained, the workgroup's barrier, then ONE relaxed agent-scope (sc1) store of the ready flag.  (A release store
+  // here and acquire loads in the waiters' poll - an L2 write-back and an L2 invalidate per poll round from ~250
+  // spinning workgroups - cost ~26 us per launch, profiles/r5/resnet_apply_ab.txt.)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) __hip_atomic_store(&cnt[NG + 1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) __hip_atomic_store(&cnt[NG + 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   (void)nblk;
 }
 
@@ -184,7 +187,8 @@ constexpr unsigned long long kApplySpinTicks = 200000000ull;  // 2 s of s_memrea
 
 // Called by EVERY thread after bn_tail (same MT / n0).  Returns when the column block's coefficients are published
 // (or the bounded wait gave up: status set, the tile's applied output is then garbage and the host raises).  Ends
-// with a workgroup barrier: the LDS bn_tail used is free again.
+// with a workgroup barrier: the LDS bn_tail used is free again.  One lane polls with relaxed agent-scope (sc1)
+// loads; the coefficients are then read only with sc1 loads (EpiApply::load).
 __device__ __forceinline__ void bn_wait_final(const BnTail* __restrict__ tp, int MT, int n0, int* status) {
   const int gs = (int)tp->gs;
   const int NG = (MT + gs - 1) / gs;
@@ -192,7 +196,7 @@ __device__ __forceinline__ void bn_wait_final(const BnTail* __restrict__ tp, int
   if (threadIdx.x == 0) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     for (int spins = 0;; ++spins) {
-      if (__hip_atomic_load(&cnt[NG + 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+      if (__hip_atomic_load(&cnt[NG + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
       __builtin_amdgcn_s_sleep(2);
       if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kApplySpinTicks) {
         __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
