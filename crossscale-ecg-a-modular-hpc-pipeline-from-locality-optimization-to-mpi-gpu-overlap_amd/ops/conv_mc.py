@@ -39,7 +39,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_set_tap", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_set_tap64", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_set_dma_dil", [i32])
-    _lib._sig(lib, "ecg_conv1d_nlc_fwd_ex", [vp] * 7 + [i32] * 10 + [vp, vp, vp, vp])
+    _lib._sig(lib, "ecg_conv1d_nlc_fwd_ex", [vp] * 7 + [i32] * 10 + [vp, vp, vp])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles", [_lib.C.c_long, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_rows", [i32] * 9)
     lib._conv_mc_bound = True
@@ -104,7 +104,7 @@ def fwd_stats_raw(x: torch.Tensor, w_t: torch.Tensor, stride: int, pad: int, L_o
     y = torch.empty((B, L_out, Cout), dtype=torch.bfloat16, device=x.device)
     stats = torch.empty((2, rows, Cout), dtype=torch.float32, device=x.device)
     st = _lib_k().ecg_conv1d_nlc_fwd_ex(x.data_ptr(), w_t.data_ptr(), None, y.data_ptr(), stats.data_ptr(), None,
-                                        None, B, Lin, Cin, L_out, Cout, K, stride, pad, 1, 0, None, None, None,
+                                        None, B, Lin, Cin, L_out, Cout, K, stride, pad, 1, 0, None, None,
                                         _lib.stream_ptr(x.device))
     _lib.check(st, "ecg_conv1d_nlc_fwd_ex")
     return y, stats

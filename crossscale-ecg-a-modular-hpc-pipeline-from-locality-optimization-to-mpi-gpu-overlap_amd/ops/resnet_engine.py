@@ -9,15 +9,6 @@ BASELINE.json config 5 (ResNet1D-34 stress, bf16, large batch).  Design (MI355X-
   transposes, no MIOpen), all shapes fixed at construction so every pointer is baked into the plan;
 * every conv is an MFMA implicit GEMM (conv1d_mc.hip) whose epilogue also emits the BatchNorm statistics;
   BN apply / backward passes are fused with ReLU and the residual;
-* fused apply (``fuse_apply`` = "fwd" (default for single-GPU plans) / "bwd" / "all" / "none"): where a conv runs on
-  the tap-shared kernel with its whole grid resident, the BatchNorm that consumes its statistics is applied INSIDE
-  the same launch once the launch's own tail has finalized it (conv1d_mc.hip fwd_epi_apply_rowwise, bn_tail.h
-  BnApply): the forward BN+ReLU (+ residual) pass after conv1 / conv2, and with "bwd" the dz pass after each
-  data-grad conv, disappear from the plan with their kernel boundaries.  The backward ones are off by default: the
-  side lane's weight-gradient workgroups hold CUs while a data-grad launch's workgroups wait for their last one
-  (ResNet1D-34 B=1024: 4.79 ms/step with every apply fused vs 3.44 without, profiles/r5/resnet_apply_ab.txt).  Off
-  when collectives may run concurrently with the step (DDP buckets, tail FedAvg): a collective's kernel holding a
-  CU could keep a grid-wide wait from completing;
 * backward is laid out in ``segments`` = gradient buckets of ~``bucket_mb`` (default 4 MB, closed at block
   boundaries; layer1 joins the stem's).  The gradients of a segment form one contiguous range of the flat grad
   buffer, so each range is all-reduced on a comm stream while the next segment runs (``run_segments``: the DDP
@@ -67,7 +58,6 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_splits", [i32] * 8)
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles_ex", [i32, i32, i32, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_rows", [i32] * 9)
-    _lib._sig(lib, "ecg_conv1d_nlc_tap_apply_ok", [i32] * 9)
     lib._plan_bound = True
     if lib.ecg_plan_op_words() != OP_WORDS or lib.ecg_plan_wentry_bytes() != 40:
         raise _lib.NativeError("resnet plan ABI mismatch (rebuild csrc)")
@@ -102,7 +92,7 @@ class ResNetStepEngine:
                  momentum: float = 0.9, weight_decay: float = 0.0, nesterov: bool = False, use_graph: bool = True,
                  grad_sync: Optional[Callable[[torch.Tensor], None]] = None,
                  source: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None,
-                 bucket_mb: Optional[float] = None, fuse_apply=None):
+                 bucket_mb: Optional[float] = None):
         dev = next(model.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("ResNetStepEngine needs a GPU (HIP kernels)")
@@ -137,15 +127,6 @@ class ResNetStepEngine:
         if bucket_mb is None:
             bucket_mb = float(os.environ.get("ECG_RESNET_BUCKET_MB", "4"))
         self.bucket_bytes = int(float(bucket_mb) * (1 << 20))
-        if fuse_apply is None:
-            fuse_apply = os.environ.get("ECG_RESNET_APPLY", "fwd") if grad_sync is None else "none"
-        modes = {"0": "none", "none": "none", "false": "none", "fwd": "fwd", "bwd": "bwd", "1": "all", "all": "all",
-                 "true": "all"}
-        fuse_apply = modes.get(str(fuse_apply).lower())
-        if fuse_apply is None:
-            raise ValueError("fuse_apply must be one of none / fwd / bwd / all")
-        self.fuse_apply = fuse_apply  # which BatchNorm applies run inside their conv's launch
-        self.apply_status = torch.zeros(4, dtype=torch.int32, device=dev)  # sticky: 1 = a fused apply timed out
         self._build()
 
     # ------------------------------------------------------------------------------------------ allocation
@@ -331,9 +312,7 @@ class ResNetStepEngine:
             # profiles/r3/resnet_epi_tail_ab.txt.)
             gs = max(8, -(-T // 32))
             NG = (T + gs - 1) // gs
-            # per 64-column block: NG level-1 counters, the level-2 counter, the fused-apply ready flag and
-            # departure count (bn_tail.h kTailCounterPad)
-            cnt = torch.zeros((Cout // 64) * (NG + 3), dtype=torch.int32, device=dev)
+            cnt = torch.zeros((Cout // 64) * (NG + 1), dtype=torch.int32, device=dev)
             self._keep.append(cnt)
             gpart = self._t((Cout // 64) * NG * 3 * 64, dtype=torch.float64)
             blob = struct.pack("<qqqq", cnt.data_ptr(), gpart.data_ptr(), gs, len(fins)) + b"".join(fins)
@@ -350,34 +329,15 @@ class ResNetStepEngine:
         # profiles/r2/resnet_multi_tile/bn_apply_rpt_ab.txt; BN1 + ReLU folded into conv2's register-staged
         # operand load measured slower than the LDS-DMA loop + BN_ACT pass: 3.85 vs 3.755,
         # profiles/r2/resnet_multi_tile/bn_fold_ab.txt - both removed in round 4)
-        # fused BatchNorm apply (bn_tail.h BnApply, 48 B each, packed like the tails)
-        apply_blobs: List[bytes] = []
-        apply_dev = self._t(96 * 64, dtype=torch.uint8)
-        self.n_fused_applies = 0
-
-        def apply_ok(Lin, Cin, Lout, Cout, K, s, p, dil=1, bwd=False) -> bool:
-            if self.fuse_apply not in ("all", "bwd" if bwd else "fwd"):
-                return False
-            return use_tail and bool(self.lib.ecg_conv1d_nlc_tap_apply_ok(B, Lin, Cin, Lout, Cout, K, s, p, dil))
-
-        def apply_blob(out, scale=None, out_d=None, scale_d=None, res=None) -> int:
-            blob = struct.pack("<6q", P(out), P(scale), P(out_d), P(scale_d), P(res), self.apply_status.data_ptr())
-            apply_blobs.append(blob + b"\0" * (64 - len(blob)))
-            if len(apply_blobs) > 96:
-                raise RuntimeError("too many fused BatchNorm applies")
-            self.n_fused_applies += 1
-            return apply_dev.data_ptr() + 64 * (len(apply_blobs) - 1)
-
         def conv(x, Lin, Cin, w_ptr, y, Lout, Cout, K, s, p, dil=1, st=None, add=None, add_mask=None, bnb=None,
-                 tail_ptr=0, lane=0, mbn=None, apply_ptr=0):
+                 tail_ptr=0, lane=0, mbn=None):
             # bnb = (mask, z, mean, rstd, zd, mean_d, rstd_d): BN-backward statistics fused into the epilogue;
-            # mbn = (scale, shift): the mask is relu(z * scale + shift) > 0 (mask operand not read);
-            # apply_ptr: a fused BatchNorm apply (apply_blob) - y may then be None
+            # mbn = (scale, shift): the mask is relu(z * scale + shift) > 0 (mask operand not read)
             extra = [P(t) if isinstance(t, torch.Tensor) else int(t or 0) for t in (bnb or ())]
             extra += [0] * (7 - len(extra))
             m_words = [P(mbn[0]), P(mbn[1])] if mbn is not None else [0, 0]
             op("CONV_FWD", P(x), w_ptr, 0, P(y), P(st), P(add), P(add_mask), B, Lin, Cin, Lout, Cout, K, s, p, dil, 0,
-               *extra, tail_ptr, *m_words, apply_ptr, lane=lane)
+               *extra, tail_ptr, *m_words, lane=lane)
 
         def wgrad(dy, x, Lin, Cin, Lout, Cout, K, s, p, weight):
             S = wsplits(B * Lout, Cout, K, Cin, s, Lin, Lout)
@@ -409,20 +369,14 @@ class ResNetStepEngine:
             if bd is not None and ds_side:
                 conv(xin, Li, Ci, self._wf[id(blk.downsample[0])], a["zd"], Lo, Co, 1, s, 0, st=stats_d,
                      tail_ptr=tail(Td, Co, [fin_fwd_words(bd, B * Lo)]), lane=1)
-            fuse1 = apply_ok(Li, Ci, Lo, Co, 3, s, 1)  # BN1 + ReLU applied inside conv1's launch
             conv(xin, Li, Ci, self._wf[id(blk.conv1)], a["z1"], Lo, Co, 3, s, 1, st=stats,
-                 tail_ptr=tail(T, Co, [fin_fwd_words(b1, B * Lo)]),
-                 apply_ptr=apply_blob(a["a1"]) if fuse1 else 0)
+                 tail_ptr=tail(T, Co, [fin_fwd_words(b1, B * Lo)]))
             if not use_tail:
                 fin_fwd(b1, T, B * Lo)
-            if not fuse1:
-                op("BN_ACT", 0, P(a["z1"]), P(b1.scale), P(b1.shift), 0, 0, 0, P(a["a1"]), B * Lo, Co)
+            op("BN_ACT", 0, P(a["z1"]), P(b1.scale), P(b1.shift), 0, 0, 0, P(a["a1"]), B * Lo, Co)
             T2 = rows(Lo, Co, Lo, Co, 3, 1, 1)
-            # BN2 + identity residual + ReLU inside conv2's launch (the downsample branch's BN_ACT joins the lanes)
-            fuse2 = bd is None and apply_ok(Lo, Co, Lo, Co, 3, 1, 1)
             conv(a["a1"], Lo, Co, self._wf[id(blk.conv2)], a["z2"], Lo, Co, 3, 1, 1, st=stats,
-                 tail_ptr=tail(T2, Co, [fin_fwd_words(b2, B * Lo)]),
-                 apply_ptr=apply_blob(a["out"], res=xin) if fuse2 else 0)
+                 tail_ptr=tail(T2, Co, [fin_fwd_words(b2, B * Lo)]))
             if not use_tail:
                 fin_fwd(b2, T2, B * Lo)
             if bd is not None:
@@ -433,7 +387,7 @@ class ResNetStepEngine:
                     fin_fwd(bd, Td, B * Lo)
                 op("BN_ACT", 2, P(a["z2"]), P(b2.scale), P(b2.shift), P(a["zd"]), P(bd.scale), P(bd.shift),
                    P(a["out"]), B * Lo, Co, lane=2)
-            elif not fuse2:
+            else:
                 op("BN_ACT", 1, P(a["z2"]), P(b2.scale), P(b2.shift), P(xin), 0, 0, P(a["out"]), B * Lo, Co)
             a["in"] = xin
             xin = a["out"]
@@ -467,26 +421,12 @@ class ResNetStepEngine:
         nxt = gB
         seg_hi = self.space.param_numel
         bn2_src = None  # (partials base, T) of the current block's BN2 statistics
-        shared_dz = (dz2, dz1, dzd)
-        dz_of: Dict[int, Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = {}
-
-        def dz_bufs(i):
-            """BN-backward outputs (dz2, dz1, dzd) of block i: one set per block with the side lane (the side-stream
-            wgrads read them), else the stream-ordered shared set."""
-            if i not in dz_of:
-                if side and i < len(blocks) - 1:
-                    dz_of[i] = (self._t(maxel), self._t(maxel),
-                                self._t(maxel) if bns[i][2] is not None else shared_dz[2])
-                else:
-                    dz_of[i] = shared_dz
-            return dz_of[i]
-
-        bn2_fused = set()  # blocks whose BN2 (+ downsample BN) backward apply ran inside the next block's dgrad
         for bi in range(len(blocks) - 1, -1, -1):
             (Li, Ci, Lo, Co, s), blk, a, (b1, b2, bd) = shapes[bi], blocks[bi], acts[bi], bns[bi]
             R = B * Lo
             blk_begin = len(ops)
-            dz2, dz1, dzd = dz_bufs(bi)
+            if side and bi < len(blocks) - 1:  # per-block BN-backward outputs (read by the side-stream wgrads)
+                dz2, dz1, dzd = self._t(maxel), self._t(maxel), (self._t(maxel) if bd is not None else dzd)
             dzm, din = gcur, nxt  # dzm: ReLU-masked grad wrt this block's output
             if bn2_src is None:  # last block: gradient from the head
                 ch = chunk_for(Co)
@@ -501,23 +441,19 @@ class ResNetStepEngine:
                 fin_bwd(b2, T2, R, 1, base)
                 if bd is not None:
                     fin_bwd(bd, T2, R, 2, base)
-            if bi not in bn2_fused:
-                op("BN_BWD_APPLY", 1 if bd is not None else 0, P(dzm), 0, P(a["z2"]), P(b2.mean), P(b2.rstd),
-                   P(b2.scale), P(b2.c1), P(b2.c2), P(dz2), P(a.get("zd")), P(bd.mean) if bd else 0,
-                   P(bd.rstd) if bd else 0, P(bd.scale) if bd else 0, P(bd.c2) if bd else 0, P(dzd), R, Co)
+            op("BN_BWD_APPLY", 1 if bd is not None else 0, P(dzm), 0, P(a["z2"]), P(b2.mean), P(b2.rstd),
+               P(b2.scale), P(b2.c1), P(b2.c2), P(dz2), P(a.get("zd")), P(bd.mean) if bd else 0,
+               P(bd.rstd) if bd else 0, P(bd.scale) if bd else 0, P(bd.c2) if bd else 0, P(dzd), R, Co)
             wgrad(dz2, a["a1"], Lo, Co, Lo, Co, 3, 1, 1, blk.conv2.weight)
-            # dgrad conv2 (stride 1, pad 1) -> ReLU-masked grad wrt a1 + BN1 backward statistics (+ the BN1 backward
-            # apply in the same launch: dz1 directly, the masked gradient itself is never stored)
+            # dgrad conv2 (stride 1, pad 1) -> ReLU-masked grad wrt a1 + BN1 backward statistics
             T1 = rows(Lo, Co, Lo, Co, 3, 1, 1)
-            fuse_b1 = apply_ok(Lo, Co, Lo, Co, 3, 1, 1, bwd=True)
-            conv(dz2, Lo, Co, self._wb[id(blk.conv2)], None if fuse_b1 else ga1, Lo, Co, 3, 1, 1, st=stats,
+            conv(dz2, Lo, Co, self._wb[id(blk.conv2)], ga1, Lo, Co, 3, 1, 1, st=stats,
                  bnb=(a["a1"], a["z1"], b1.mean, b1.rstd, 0, 0, 0), tail_ptr=tail(T1, Co, [fin_bwd_words(b1, R, 1)]),
-                 mbn=(b1.scale, b1.shift), apply_ptr=apply_blob(dz1, scale=b1.scale) if fuse_b1 else 0)
+                 mbn=(b1.scale, b1.shift))
             if not use_tail:
                 fin_bwd(b1, T1, R, 1, stats.data_ptr())
-            if not fuse_b1:
-                op("BN_BWD_APPLY", 0, P(ga1), 0, P(a["z1"]), P(b1.mean), P(b1.rstd), P(b1.scale), P(b1.c1),
-                   P(b1.c2), P(dz1), 0, 0, 0, 0, 0, 0, R, Co)
+            op("BN_BWD_APPLY", 0, P(ga1), 0, P(a["z1"]), P(b1.mean), P(b1.rstd), P(b1.scale), P(b1.c1),
+               P(b1.c2), P(dz1), 0, 0, 0, 0, 0, 0, R, Co)
             wgrad(dz1, a["in"], Li, Ci, Lo, Co, 3, s, 1, blk.conv1.weight)
             add = dzm
             if bd is not None:
@@ -528,19 +464,9 @@ class ResNetStepEngine:
                 pa, (_, pb2, pbd) = acts[bi - 1], bns[bi - 1]
                 Tn = rows(Lo, Co, Li, Ci, 3, 1, 1, s)  # phase-decomposed when s > 1
                 fins = [fin_bwd_words(pb2, B * Li, 1)] + ([fin_bwd_words(pbd, B * Li, 2)] if pbd else [])
-                # the previous block's BN2 (+ downsample BN) backward apply inside this launch: its dz2 / dzd directly
-                # (din, the masked gradient, is still stored: the previous block adds it as its identity residual)
-                fuse_b2 = apply_ok(Lo, Co, Li, Ci, 3, 1, 1, s, bwd=True)
-                app = 0
-                if fuse_b2:
-                    pdz2, _, pdzd = dz_bufs(bi - 1)
-                    app = apply_blob(pdz2, scale=pb2.scale, out_d=pdzd if pbd else None,
-                                     scale_d=pbd.scale if pbd else None)
-                    bn2_fused.add(bi - 1)
                 conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=add, st=stats_b,
                      bnb=(pa["out"], pa["z2"], pb2.mean, pb2.rstd, pa.get("zd") if pbd else 0,
-                          pbd.mean if pbd else 0, pbd.rstd if pbd else 0), tail_ptr=tail(Tn, Ci, fins),
-                     apply_ptr=app)
+                          pbd.mean if pbd else 0, pbd.rstd if pbd else 0), tail_ptr=tail(Tn, Ci, fins))
                 bn2_src = (stats_b.data_ptr(), Tn, use_tail)
             else:  # into the stem: plain gradient wrt the pooled activations
                 conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=add)
@@ -577,9 +503,6 @@ class ResNetStepEngine:
         if tail_blobs:
             blob = torch.frombuffer(bytearray(b"".join(tail_blobs)), dtype=torch.uint8)
             tails_dev[:blob.numel()].copy_(blob)
-        if apply_blobs:
-            blob = torch.frombuffer(bytearray(b"".join(apply_blobs)), dtype=torch.uint8)
-            apply_dev[:blob.numel()].copy_(blob)
         self.n_bn_tails = len(tail_blobs)
         self.ops = torch.tensor(ops, dtype=torch.int64)
         self.n_ops = len(ops)
@@ -707,15 +630,7 @@ class ResNetStepEngine:
         st = self.lib.ecg_plan_run(ops.data_ptr(), 1, ctypes.byref(bad), sp)
         _lib.check(st, "ecg_plan_run(sgd_range)")
 
-    def check_status(self) -> None:
-        """Raise if a fused BatchNorm apply gave up waiting for its coefficients (workgroups not co-resident: the
-        outputs of that step are wrong).  Synchronises."""
-        if int(self.apply_status[0].item()):
-            raise _lib.NativeError("fused BatchNorm apply timed out waiting for its coefficients (grid not "
-                                   "co-resident); rebuild the engine with fuse_apply=False")
-
     def avg_loss(self) -> float:
-        self.check_status()
         return float(self.loss_acc.item()) / max(1, self._loss_steps)
 
     def reset_loss(self) -> None:

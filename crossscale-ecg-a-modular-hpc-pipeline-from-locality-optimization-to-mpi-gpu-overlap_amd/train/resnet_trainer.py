@@ -42,12 +42,9 @@ class ResNetEngineTrainer:
         self.sampler = DeviceIndexSampler(x.shape[0], batch_size, self.device, seed=seed)
         self._works: List = []
         ddp = sync == "ddp" and ctx is not None and ctx.distributed
-        # fused BatchNorm applies wait grid-wide inside their launch: not while collectives may run beside the
-        # step (DDP buckets, tail FedAvg - every multi-rank plan), whose kernels could hold a CU the wait needs
-        fuse = None if ctx is None or not ctx.distributed else "none"
         self.engine = ResNetStepEngine(model, batch_size, x.shape[1], lr=lr, momentum=momentum,
                                        weight_decay=weight_decay, use_graph=use_graph,
-                                       source=(self.x, self.y32, self.table), bucket_mb=bucket_mb, fuse_apply=fuse)
+                                       source=(self.x, self.y32, self.table), bucket_mb=bucket_mb)
         self.ddp = ddp
         self._comm = torch.cuda.Stream(device=self.device, priority=-1) if ctx is not None and ctx.distributed \
             else None

@@ -16,14 +16,6 @@
 // into ``gpart``; level 2: the last group reducer of the column block sums the group rows in group order and
 // finalizes.  The summation order never depends on arrival order: bitwise reproducible.  The final reducer
 // zeroes the block's counters for the next launch.
-//
-// Fused apply (``BnApply``, conv1d_mc.hip's tap-shared kernel): when every workgroup of the launch is resident at
-// once, the workgroups do not end after their tile's statistics - they wait for their column block's final reducer
-// to PUBLISH the finalized coefficients (ready flag, release -> acquire), then apply the BatchNorm to the tile still
-// held in their accumulators (forward: scale / shift + residual + ReLU; backward: dz = scale (g - c1 - xhat c2)),
-// replacing the separate element-wise BN pass and its kernel boundary.  A departure count lets the last workgroup
-// re-arm the flag for the next launch.  Per 64-column block the counter row holds [NG + 3] words: NG level-1
-// arrival counters, the level-2 counter, the ready flag, the departure count.
 #pragma once
 
 #include <stdint.h>
@@ -49,15 +41,37 @@ struct BnFin {
   float* c2;  // sum dz*xhat / n
 };
 
-constexpr int kTailCounterPad = 3;  // words per column block past the NG level-1 counters (level 2, flag, departures)
-
 struct BnTail {
-  unsigned* counters;  // [Cout/64][NG + kTailCounterPad] (column block nt uses row nt), zero between launches
+  unsigned* counters;  // [Cout/64][NG + 1] (column block nt uses row nt), zero between launches
   double* gpart;       // [Cout/64][NG][3][64] level-1 group partials (row stride in doubles: NG * 3 * 64)
   int64_t gs;          // M tiles per level-1 group
   int64_t nfin;        // 1 or 2 BatchNorms finalized from the same statistics (data-grad conv + downsample)
   BnFin fin[2];
 };
+
+__device__ __forceinline__ void bn_fin_channel(const BnFin& f, int c, double v1, double v2) {
+  const double n = f.n;
+  if (f.mode == 0) {
+    const double mu = v1 / n;
+    const double var = fmax(v2 / n - mu * mu, 0.0);
+    const float rs = (float)(1.0 / sqrt(var + f.eps));
+    const float sc = f.gamma[c] * rs;
+    f.mean[c] = (float)mu;
+    f.rstd[c] = rs;
+    f.scale[c] = sc;
+    f.shift[c] = f.beta[c] - (float)mu * sc;
+    if (f.run_mean) {
+      const float m = (float)f.momentum;
+      f.run_mean[c] = (1.f - m) * f.run_mean[c] + m * (float)mu;
+      f.run_var[c] = (1.f - m) * f.run_var[c] + m * (float)(var * n / fmax(n - 1.0, 1.0));
+    }
+  } else {
+    if (f.dbeta) f.dbeta[c] = (float)v1;
+    if (f.dgamma) f.dgamma[c] = (float)v2;
+    f.c1[c] = (float)(v1 / n);
+    f.c2[c] = (float)(v2 / n);
+  }
+}
 
 __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -70,30 +84,6 @@ __device__ __forceinline__ void st_sc1(float* p, float v) {
 }
 __device__ __forceinline__ void st_sc1(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void bn_fin_channel(const BnFin& f, int c, double v1, double v2) {
-  const double n = f.n;
-  if (f.mode == 0) {
-    const double mu = v1 / n;
-    const double var = fmax(v2 / n - mu * mu, 0.0);
-    const float rs = (float)(1.0 / sqrt(var + f.eps));
-    const float sc = f.gamma[c] * rs;
-    f.mean[c] = (float)mu;
-    f.rstd[c] = rs;
-    st_sc1(f.scale + c, sc);  // write-through: a fused apply reads them inside this launch (sc1 loads)
-    st_sc1(f.shift + c, f.beta[c] - (float)mu * sc);
-    if (f.run_mean) {
-      const float m = (float)f.momentum;
-      f.run_mean[c] = (1.f - m) * f.run_mean[c] + m * (float)mu;
-      f.run_var[c] = (1.f - m) * f.run_var[c] + m * (float)(var * n / fmax(n - 1.0, 1.0));
-    }
-  } else {
-    if (f.dbeta) f.dbeta[c] = (float)v1;
-    if (f.dgamma) f.dgamma[c] = (float)v2;
-    st_sc1(f.c1 + c, (float)(v1 / n));
-    st_sc1(f.c2 + c, (float)(v2 / n));
-  }
 }
 
 // Called by EVERY thread of a statistics-producing workgroup after it stored its partial row (sc1) for M tile
@@ -111,7 +101,7 @@ __device__ __forceinline__ void bn_tail(const BnTail* __restrict__ tp, const flo
   const int nb0 = n0 / 64, nblk = BN / 64;  // 64-column blocks of this workgroup
   // counters / group partials are kept per 64-column block so the host need not know the tile width: the
   // workgroup's blocks arrive together (one ticket on the first block's counter stands for all of them).
-  unsigned* cnt = tp->counters + (long)nb0 * (NG + kTailCounterPad);
+  unsigned* cnt = tp->counters + (long)nb0 * (NG + 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 partial stores have completed
   __syncthreads();
   if (tid == 0)
@@ -162,63 +152,7 @@ __device__ __forceinline__ void bn_tail(const BnTail* __restrict__ tp, const flo
     }
   }
   for (int i = tid; i <= NG; i += NTHR) __hip_atomic_store(&cnt[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // publish the finalized coefficients to the launch's waiting workgroups (fused apply; guide G16, the sc1 form of
-  // the hand-off: no release / acquire fences): the coefficients were stored write-through by every wave and
-  // drained, the workgroup's barrier, then ONE relaxed agent-scope (sc1) store of the ready flag.  (A release store
-  // here and acquire loads in the waiters' poll - an L2 write-back and an L2 invalidate per poll round from ~250
-  // spinning workgroups - cost ~26 us per launch, profiles/r5/resnet_apply_ab.txt.)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) __hip_atomic_store(&cnt[NG + 1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   (void)nblk;
-}
-
-// ---- fused apply: the coefficient hand-off to every workgroup of the column block
-struct BnApply {
-  __bf16* out;           // the applied tensor: forward activation / backward dz
-  const float* scale;    // backward: the BatchNorm's gamma * rstd (from the forward)
-  __bf16* out_d;         // backward, downsample branch sharing the gradient: dz_d (or null)
-  const float* scale_d;  // its gamma * rstd
-  const __bf16* res;     // forward: residual added before the ReLU (or null)
-  int* status;           // sticky error word: 1 = a wait for the coefficients timed out
-};
-
-constexpr unsigned long long kApplySpinTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
-
-// Called by EVERY thread after bn_tail (same MT / n0).  Returns when the column block's coefficients are published
-// (or the bounded wait gave up: status set, the tile's applied output is then garbage and the host raises).  Ends
-// with a workgroup barrier: the LDS bn_tail used is free again.  One lane polls with relaxed agent-scope (sc1)
-// loads; the coefficients are then read only with sc1 loads (EpiApply::load).
-__device__ __forceinline__ void bn_wait_final(const BnTail* __restrict__ tp, int MT, int n0, int* status) {
-  const int gs = (int)tp->gs;
-  const int NG = (MT + gs - 1) / gs;
-  unsigned* cnt = tp->counters + (long)(n0 / 64) * (NG + kTailCounterPad);
-  if (threadIdx.x == 0) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (int spins = 0;; ++spins) {
-      if (__hip_atomic_load(&cnt[NG + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
-      __builtin_amdgcn_s_sleep(2);
-      if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > kApplySpinTicks) {
-        __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-}
-
-// After the workgroup read the published coefficients: count it out; the last of the MT workgroups of the column
-// block re-arms the flag and the count for the next launch (stream order: that launch starts after this one ended).
-__device__ __forceinline__ void bn_depart(const BnTail* __restrict__ tp, int MT, int n0) {
-  if (threadIdx.x != 0) return;
-  const int gs = (int)tp->gs;
-  const int NG = (MT + gs - 1) / gs;
-  unsigned* cnt = tp->counters + (long)(n0 / 64) * (NG + kTailCounterPad);
-  if (__hip_atomic_fetch_add(&cnt[NG + 2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(MT - 1)) {
-    __hip_atomic_store(&cnt[NG + 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&cnt[NG + 2], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 }  // namespace ecg

@@ -57,10 +57,6 @@ struct FwdArgs {
   const float* mscale;
   const float* mshift;
   const ecg::BnTail* tail;  // BatchNorm finalize fused into this launch's tail (bn_tail.h), or null
-  // BatchNorm applied in this launch after its finalize (tap-shared kernel only, every workgroup resident):
-  // forward out = relu(y * scale + shift [+ res]); backward dz = scale * (v - c1 - xhat * c2) [and dz_d]; null = off.
-  // ``y`` may then be null (the pre-BatchNorm tensor is not stored).
-  const ecg::BnApply* apply;
 };
 
 // A tile: 64 rows (b,t) x 64 kk (one tap k, channels c0..c0+63); element e (0..511) = row e>>3, 8 bf16 part e&7
@@ -215,7 +211,7 @@ __device__ __forceinline__ void fwd_epi_tile_rowwise(const FwdArgs& a, f32x4 (&a
           outv[e] = (__bf16)v[e];
           v[e] = (float)outv[e];
         }
-        if (a.y) *reinterpret_cast<bf16x8*>(a.y + o) = outv;  // (null: fused apply, the tensor is not needed)
+        *reinterpret_cast<bf16x8*>(a.y + o) = outv;
         if constexpr (bwd) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
@@ -233,136 +229,6 @@ __device__ __forceinline__ void fwd_epi_tile_rowwise(const FwdArgs& a, f32x4 (&a
             k.s1[e] += v[e];
             k.s2[e] += v[e] * v[e];
           }
-        }
-      }
-    }
-  }
-}
-
-// Per-lane channel constants of the fused BatchNorm apply, loaded after the column block's coefficients were
-// published (bn_wait_final): write-through (sc1) loads, so no line an earlier launch left in this CU's L1 is used.
-struct EpiApply {
-  float sc[8], sh[8], c1[8], c2[8], scd[8], c2d[8];
-  template <bool BWD>
-  __device__ __forceinline__ void load(const FwdArgs& a, int n) {
-    const ecg::BnFin& f0 = a.tail->fin[0];
-    const bool ds = BWD && a.apply->out_d != nullptr;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if constexpr (BWD) {
-        sc[e] = a.apply->scale[n + e];
-        c1[e] = ecg::ld_sc1(f0.c1 + n + e);
-        c2[e] = ecg::ld_sc1(f0.c2 + n + e);
-        scd[e] = ds ? a.apply->scale_d[n + e] : 0.f;
-        c2d[e] = ds ? ecg::ld_sc1(a.tail->fin[1].c2 + n + e) : 0.f;
-        sh[e] = 0.f;
-      } else {
-        sc[e] = ecg::ld_sc1(f0.scale + n + e);
-        sh[e] = ecg::ld_sc1(f0.shift + n + e);
-        c1[e] = c2[e] = scd[e] = c2d[e] = 0.f;
-      }
-    }
-  }
-};
-
-// Pass 2 of a fused-apply launch: the tile's accumulators (still in registers) go through the same row-wise
-// staging and the same value expression as pass 1 (bitwise the value pass 1 stored / summed), then through the
-// BatchNorm with the published coefficients - the expression of the separate passes it replaces (resnet_nlc.hip
-// bn_act_kernel / bn_bwd_apply_kernel), so the output is the same tensor those passes wrote.
-template <int BM, int BN, int EPI, int NWR = 2>
-__device__ __forceinline__ void fwd_epi_apply_rowwise(const FwdArgs& a, f32x4 (&acc)[BM / NWR / 16][BN / 32],
-                                                      unsigned char* smem, const EpiConst& k, const EpiApply& q,
-                                                      int m0, int n0, int Lrow, int M) {
-  using Cfg = FwdCfg<BM, BN, NWR>;
-  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wr = wv >> 1;
-  constexpr int EP_LD = Cfg::EP_LD, HR = WM / 2;
-  float* ep = reinterpret_cast<float*>(smem) + wv * HR * EP_LD;
-  constexpr int CG = WN / 8, RSTEP = 64 / CG, ITEMS = HR / RSTEP;
-  const int cg = lane % CG, rs = lane / CG;
-  const int n = EpiLane<BN, NWR>::n(n0);
-  constexpr bool bwd = EPI == 1;
-  const bool ds = bwd && a.apply->out_d != nullptr;
-  __bf16* const out = a.apply->out;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if (h) __syncthreads();  // previous half fully read
-#pragma unroll
-    for (int i = 0; i < FM / 2; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq)
-          ep[(i * 16 + 4 * (lane >> 4) + qq) * EP_LD + j * 16 + (lane & 15)] = acc[h * (FM / 2) + i][j][qq];
-    __syncthreads();
-#pragma unroll 2
-    for (int it = 0; it < ITEMS; ++it) {
-      const int rl = rs + it * RSTEP;
-      const int r = h * HR + rl;
-      const int m = m0 + wr * WM + r;
-      if (m < M) {
-        const int bb = m / Lrow, tt = m - bb * Lrow;
-        const long o = ((long)bb * a.Lout + tt) * a.Cout + n;
-        const float4 v0 = *reinterpret_cast<const float4*>(ep + rl * EP_LD + cg * 8);
-        const float4 v1 = *reinterpret_cast<const float4*>(ep + rl * EP_LD + cg * 8 + 4);
-        float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += k.bv[e];
-        if (a.add) {
-          const bf16x8 ad = *reinterpret_cast<const bf16x8*>(a.add + o);
-          if (a.add_mask) {
-            const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.add_mask + o);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += (float)mk[e] > 0.f ? (float)ad[e] : 0.f;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += (float)ad[e];
-          }
-        }
-        bf16x8 zz;
-        if constexpr (bwd) zz = *reinterpret_cast<const bf16x8*>(a.sz + o);
-        if (bwd && a.mscale != nullptr) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const __bf16 act = (__bf16)fmaxf(fmaf((float)zz[e], k.msc[e], k.msh[e]), 0.f);
-            v[e] = (float)act > 0.f ? v[e] : 0.f;
-          }
-        } else if (bwd && a.smask != nullptr) {
-          const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.smask + o);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = (float)mk[e] > 0.f ? v[e] : 0.f;
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          if (a.relu) v[e] = fmaxf(v[e], 0.f);
-          v[e] = (float)(__bf16)v[e];  // the value pass 1 stored and summed
-        }
-        bf16x8 outv;
-        if constexpr (bwd) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            outv[e] = (__bf16)(q.sc[e] * (v[e] - q.c1[e] - ((float)zz[e] - k.mu[e]) * k.rsd[e] * q.c2[e]));
-          *reinterpret_cast<bf16x8*>(out + o) = outv;
-          if (ds) {
-            const bf16x8 zd = *reinterpret_cast<const bf16x8*>(a.szd + o);
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              outv[e] = (__bf16)(q.scd[e] * (v[e] - q.c1[e] - ((float)zd[e] - k.mud[e]) * k.rsdd[e] * q.c2d[e]));
-            *reinterpret_cast<bf16x8*>(a.apply->out_d + o) = outv;
-          }
-        } else {
-          float y[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) y[e] = fmaf(v[e], q.sc[e], q.sh[e]);
-          if (a.apply->res) {
-            const bf16x8 rr = *reinterpret_cast<const bf16x8*>(a.apply->res + o);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) y[e] += (float)rr[e];
-          }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) outv[e] = (__bf16)fmaxf(y[e], 0.f);
-          *reinterpret_cast<bf16x8*>(out + o) = outv;
         }
       }
     }
@@ -1085,13 +951,6 @@ __global__ __launch_bounds__(512, 1) void conv1d_nlc_fwd_tap_kernel(FwdArgs a, i
   if (a.stats) fwd_epi_stats<BM, BN, EPI, NWR>(a, smem, k, n0, mt, MT);  // block-uniform
   if (a.tail && a.stats)
     ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, MT, a.Cout, mt, n0, BN, smem);
-  if (a.apply) {  // block-uniform: every workgroup of the launch is resident (host-checked, ecg_conv1d_nlc_tap_apply_ok)
-    ecg::bn_wait_final(a.tail, MT, n0, a.apply->status);
-    EpiApply q;
-    q.load<EPI == 1>(a, EpiLane<BN, NWR>::n(n0));
-    ecg::bn_depart(a.tail, MT, n0);
-    fwd_epi_apply_rowwise<BM, BN, EPI, NWR>(a, acc, smem, k, q, m0, n0, L, M);
-  }
 }
 
 // ------------------------------------------------------------------ persistent tap-shared 64-channel kernel
@@ -1283,29 +1142,6 @@ int launch_fwd_tap(const FwdArgs& a, hipStream_t stream) {
   const bool b = a.stat_mode == 1;
   if (a.Cout % 128 == 0) return b ? launch_fwd_tap_t<128, 1>(a, stream) : launch_fwd_tap_t<128, 0>(a, stream);
   return b ? launch_fwd_tap_t<64, 1>(a, stream) : launch_fwd_tap_t<64, 0>(a, stream);
-}
-
-// Fused-apply residency: the grid (one workgroup per (M tile, column block)) must fit the device at one workgroup
-// per CU, since every workgroup waits for its column block's last one.  Queried once per kernel instance.
-template <int BN, int EPI>
-bool tap_grid_resident(int grid) {
-  static int cus = -1, per_cu = -1;
-  if (cus < 0) {
-    int dev = 0;
-    constexpr int SMEM = TapCfg<BN>::SMEM;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipFuncSetAttribute((const void*)conv1d_nlc_fwd_tap_kernel<BN, EPI>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, SMEM) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)conv1d_nlc_fwd_tap_kernel<BN, EPI>, 512,
-                                                     SMEM) != hipSuccess) {
-      cus = 0;
-      per_cu = 0;
-    }
-  }
-  // (the occupancy answer can be one block per CU too high - MI355X guide, correctness boundaries - so only
-  // grids of at most ONE workgroup per CU qualify, whatever it says beyond 1)
-  return per_cu >= 1 && grid <= cus;
 }
 
 // ECG_CONV_TAP=0|1|2: the tap-shared 256-row kernel for eligible convs with C_out % 128 == 0 (1, default), also
@@ -2227,19 +2063,11 @@ inline bool wgrad_big(int Cout, int Cin) { return conv_big() >= 2 && Cout % 256 
 // BatchNorm whose backward statistics the data-grad epilogue produces ([2 or 3][M tiles][Cout] into ``stats``);
 // mscale / mshift (both or neither) re-derive the ReLU mask from sz instead of reading smask.
 // ``tail`` (optional, with ``stats``): a BatchNorm finalize fused into this launch (bn_tail.h).
-// ``apply`` (optional, with ``tail``; device ecg::BnApply): the BatchNorm applied in the same launch once finalized
-// (only where ecg_conv1d_nlc_tap_apply_ok holds: the tap-shared kernel with every workgroup resident); ``y`` may be
-// null then.
-ECG_API int ecg_conv1d_nlc_tap_apply_ok(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad,
-                                        int in_dil);
 ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bias, void* y, float* stats,
                                   const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
                                   int Kw, int stride, int pad, int in_dil, int relu, const void* const* bnb,
-                                  const void* tail, const void* apply, hipStream_t stream) {
-  if (!x || !w || (!y && !apply) || B <= 0 || Lin <= 0 || Lout <= 0 || Kw <= 0 || stride <= 0 || in_dil <= 0 ||
-      pad < 0)
-    return ecg::kBadArg;
-  if (apply && (!tail || !ecg_conv1d_nlc_tap_apply_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)))
+                                  const void* tail, hipStream_t stream) {
+  if (!x || !w || !y || B <= 0 || Lin <= 0 || Lout <= 0 || Kw <= 0 || stride <= 0 || in_dil <= 0 || pad < 0)
     return ecg::kBadArg;
   if (Cin % BK != 0 || Cout % 64 != 0 || (add_mask && !add)) return ecg::kBadArg;
   if (bnb && (!stats || !bnb[1] || !bnb[2] || !bnb[3] || (bnb[4] && (!bnb[5] || !bnb[6])) || (!bnb[7] != !bnb[8])))
@@ -2260,8 +2088,7 @@ ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bia
     a.srstd_d = static_cast<const float*>(bnb[6]);
   }
   a.tail = static_cast<const ecg::BnTail*>(tail);
-  a.apply = static_cast<const ecg::BnApply*>(apply);
-  if (!apply && tap64_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return launch_tap64(a, stream);
+  if (tap64_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return launch_tap64(a, stream);
   if (conv_tap(Cout) && tap_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return launch_fwd_tap(a, stream);
   int bm, bn;
   pick_fwd_tile((long)B * Lout, Cout, in_dil, &bm, &bn);
@@ -2270,18 +2097,6 @@ ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bia
   if (bm == 128 && bn == 128) return launch_fwd<128, 128>(a, stream);
   if (bm == 128) return launch_fwd<128, 64>(a, stream);
   return launch_fwd<64, 64>(a, stream);
-}
-
-// 1 when this conv takes the tap-shared kernel and its whole grid is resident at once (one workgroup per CU), so
-// a launch may carry a fused BatchNorm apply (``apply`` of ecg_conv1d_nlc_fwd_ex); 0 otherwise.
-ECG_API int ecg_conv1d_nlc_tap_apply_ok(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad,
-                                        int in_dil) {
-  if (B <= 0 || !conv_tap(Cout) || !tap_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return 0;
-  const int BN = Cout % 128 == 0 ? 128 : 64;
-  const int grid = tap_mtiles(B, Lout) * (Cout / BN);
-  const bool ok = BN == 128 ? tap_grid_resident<128, 1>(grid) && tap_grid_resident<128, 0>(grid)
-                            : tap_grid_resident<64, 1>(grid) && tap_grid_resident<64, 0>(grid);
-  return ok ? 1 : 0;
 }
 
 // Persistent 64-channel tap kernel on (1) / off (0); returns the previous setting (tests, A/B).  Step plans size
@@ -2353,7 +2168,7 @@ ECG_API int ecg_conv1d_nlc_fwd(const void* x, const void* w, const float* bias, 
                                int Lout, int Cout, int Kw, int stride, int pad, int in_dil, int relu,
                                hipStream_t stream) {
   return ecg_conv1d_nlc_fwd_ex(x, w, bias, y, nullptr, nullptr, nullptr, B, Lin, Cin, Lout, Cout, Kw, stride, pad,
-                               in_dil, relu, nullptr, nullptr, nullptr, stream);
+                               in_dil, relu, nullptr, nullptr, stream);
 }
 
 // LDS-DMA weight-gradient loops: 32-bit buffer offsets from the split's first row / sample (cps row chunks of 64).
