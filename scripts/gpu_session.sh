@@ -70,7 +70,7 @@ for s in "$@"; do
       step module1 1000 python bench_locality.py --batch-sizes 64 128 256 512 --reps 5 --results-dir "$OUT/modules" ;;
     module1f)  # A0-A5 with the fused HIP training step: the data path without the eager step's launches
       [ -d data/shards ] || step shard_prep 300 python shard_prep.py --dataset synthetic
-      step module1f 1000 python bench_locality.py --compute fused --batch-sizes 64 128 256 512 --reps 5 \
+      step module1f 1000 python bench_locality.py --compute fused --batch-sizes 64 128 256 512 --reps 9 --reps-large 15 \
         --results-dir "$OUT/modules" ;;
     module2)
       step module2 900 python benchmark_part_2.py --results-dir "$OUT/modules" ;;
