@@ -119,6 +119,8 @@ for s in "$@"; do
       step pmc_tap2 120 timeout -s KILL 100 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
         SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD --kernel-trace --output-format csv \
         -d "$OUT/pmc_tap2" -o p -- python3 scripts/r4_conv_probe.py 5 1024 ;;
+    coldprobe)  # conv time with operands in HBM (a buffer ring larger than the Infinity Cache) vs cache-resident
+      step coldprobe 300 python scripts/conv_cold_probe.py 24 ;;
     probe64)  # isolated conv timings with the persistent 64-channel tap kernel on / off
       for m in 1 0; do ECG_CONV_TAP64=$m step probe64_$m 300 python scripts/r4_conv_probe.py 30 1024; done ;;
     tapab)
