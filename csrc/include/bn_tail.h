@@ -45,7 +45,10 @@ struct BnTail {
   unsigned* counters;  // [Cout/64][NG + 1] (column block nt uses row nt), zero between launches
   double* gpart;       // [Cout/64][NG][3][64] level-1 group partials (row stride in doubles: NG * 3 * 64)
   int64_t gs;          // M tiles per level-1 group
-  int64_t nfin;        // 1 or 2 BatchNorms finalized from the same statistics (data-grad conv + downsample)
+  int64_t nfin;        // 1 or 2 BatchNorms finalized from the same statistics (data-grad conv + downsample); bits
+                       // 8+: diagnostic early exit (scripts/conv_cold_probe.py): 1 after the level-1 ticket, 2 after
+                       // the level-2 ticket (counters reset, nothing finalized), 3 after the level-2 loads - never
+                       // set by the engine
   BnFin fin[2];
 };
 
@@ -96,6 +99,7 @@ __device__ __forceinline__ void bn_tail(const BnTail* __restrict__ tp, const flo
   int* flag = reinterpret_cast<int*>(lds);
   double* sums = reinterpret_cast<double*>(lds + 16);
   const int gs = (int)tp->gs;
+  const int stop = (int)(tp->nfin >> 8);
   const int NG = (MT + gs - 1) / gs;
   const int g = mt / gs, members = min(gs, MT - g * gs);
   const int nb0 = n0 / 64, nblk = BN / 64;  // 64-column blocks of this workgroup
@@ -108,6 +112,10 @@ __device__ __forceinline__ void bn_tail(const BnTail* __restrict__ tp, const flo
     flag[0] = __hip_atomic_fetch_add(&cnt[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(members - 1);
   __syncthreads();
   if (!flag[0]) return;
+  if (stop == 1) {
+    if (tid == 0) __hip_atomic_store(&cnt[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   // ---- level 1: the group's rows, in row order, per (stat, column).  Every load of a batch (up to 32 rows) is
   // issued before the first add: one round trip per batch, not one per row.
   const long gstride = (long)NG * 3 * 64;  // doubles per 64-column block
@@ -130,6 +138,10 @@ __device__ __forceinline__ void bn_tail(const BnTail* __restrict__ tp, const flo
     flag[1] = __hip_atomic_fetch_add(&cnt[NG], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(NG - 1);
   __syncthreads();
   if (!flag[1]) return;
+  if (stop == 2 || stop == 3) {
+    for (int i = tid; i <= NG; i += NTHR) __hip_atomic_store(&cnt[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (stop == 2) return;
+  }
   // ---- level 2: the group partials in group order (batches of 32 in flight), then the per-channel finalize
   for (int p = tid; p < NS * BN; p += NTHR) {
     const int st = p / BN, c = p - st * BN;
@@ -145,8 +157,9 @@ __device__ __forceinline__ void bn_tail(const BnTail* __restrict__ tp, const flo
     sums[p] = s;
   }
   __syncthreads();
+  if (stop == 3) return;
   for (int c = tid; c < BN; c += NTHR) {
-    for (int f = 0; f < (int)tp->nfin; ++f) {
+    for (int f = 0; f < (int)(tp->nfin & 0xff); ++f) {
       const BnFin& fin = tp->fin[f];
       bn_fin_channel(fin, n0 + c, sums[c], sums[(int)fin.statB * BN + c]);
     }

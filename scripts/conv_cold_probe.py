@@ -48,11 +48,11 @@ def graph_time(fns, reps):
     return a.elapsed_time(b) / (3 * reps) * 1e3
 
 
-def make_tail(dev, T, C, n):
+def make_tail(dev, T, C, n, stop=0, gs=None):
     """A device BnTail blob (csrc/include/bn_tail.h) with one forward finalize, packed as the ResNet engine packs it:
     the launch then also runs the fused BatchNorm finalize (the in-step configuration of every statistics conv)."""
     import struct
-    gs = max(8, -(-T // 32))
+    gs = gs or max(8, -(-T // 32))
     NG = (T + gs - 1) // gs
     keep = [torch.zeros((C // 64) * (NG + 1), dtype=torch.int32, device=dev),
             torch.zeros((C // 64) * NG * 3 * 64, dtype=torch.float64, device=dev),
@@ -61,7 +61,7 @@ def make_tail(dev, T, C, n):
     P = lambda t: t.data_ptr()  # noqa: E731
     fin = struct.pack("<qqddd12q", 0, 1, float(n), 1e-5, 0.1, P(gam), P(bet), P(mean), P(rstd), P(scale), P(shift),
                       P(rm), P(rv), 0, 0, 0, 0)
-    blob = struct.pack("<qqqq", P(cnt), P(gpart), gs, 1) + fin
+    blob = struct.pack("<qqqq", P(cnt), P(gpart), gs, 1 | (stop << 8)) + fin
     blob += b"\0" * (304 - len(blob))
     dt = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
     keep.append(dt)
@@ -95,18 +95,22 @@ def main():
             fns = [mk(i) for i in range(nbuf)]
             warm = graph_time(fns[:1], reps)
             cold = graph_time(fns, max(reps, nbuf))
-            tail_ptr, keep = make_tail(dev, rows, Co, B * L)
+            tails = {}
+            # full tail; diagnostic exits after the level-1 / level-2 tickets (bn_tail.h); one level-1 group
+            for key, kw in (("warm_tail_us", {}), ("tail_stop1_us", {"stop": 1}), ("tail_stop2_us", {"stop": 2}),
+                            ("tail_stop3_us", {"stop": 3}),
+                            ("tail_1group_us", {"gs": rows})):
+                tail_ptr, keep = make_tail(dev, rows, Co, B * L, **kw)
 
-            def ft():
-                lib.ecg_conv1d_nlc_fwd_ex(xs[0].data_ptr(), w.data_ptr(), None, ys[0].data_ptr(), st.data_ptr(),
-                                          None, None, B, L, Ci, L, Co, 3, 1, 1, 1, 0, None, tail_ptr,
-                                          torch.cuda.current_stream().cuda_stream)
-            warm_tail = graph_time([ft], reps)
+                def ft():
+                    lib.ecg_conv1d_nlc_fwd_ex(xs[0].data_ptr(), w.data_ptr(), None, ys[0].data_ptr(), st.data_ptr(),
+                                              None, None, B, L, Ci, L, Co, 3, 1, 1, 1, 0, None, tail_ptr,
+                                              torch.cuda.current_stream().cuda_stream)
+                tails[key] = round(graph_time([ft], reps), 2)
+                del keep
             print(json.dumps({"shape": name, "kernel": label, "B": B, "io_mb": round(mb, 1), "ring": nbuf,
-                              "warm_us": round(warm, 2), "warm_tail_us": round(warm_tail, 2),
-                              "cold_us": round(cold, 2),
+                              "stat_rows": rows, "warm_us": round(warm, 2), **tails, "cold_us": round(cold, 2),
                               "cold_tbs": round(mb * 2 ** 20 / (cold * 1e-6) / 1e12, 2)}), flush=True)
-            del keep
         conv_mc.set_tap64(True)
         del xs
 
