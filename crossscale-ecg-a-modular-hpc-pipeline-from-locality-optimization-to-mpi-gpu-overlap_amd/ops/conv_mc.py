@@ -42,6 +42,8 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_ex", [vp] * 7 + [i32] * 10 + [vp, vp, vp])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles", [_lib.C.c_long, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_rows", [i32] * 9)
+    _lib._sig(lib, "ecg_conv1d_nlc_fwd_pa", [vp] * 7 + [i32] * 10 + [vp, vp, vp, vp])
+    _lib._sig(lib, "ecg_conv1d_nlc_pa_ok", [i32] * 9)
     lib._conv_mc_bound = True
 
 
@@ -108,6 +110,33 @@ def fwd_stats_raw(x: torch.Tensor, w_t: torch.Tensor, stride: int, pad: int, L_o
                                         _lib.stream_ptr(x.device))
     _lib.check(st, "ecg_conv1d_nlc_fwd_ex")
     return y, stats
+
+
+def pre_act_ok(B: int, L: int, c_in: int, c_out: int) -> bool:
+    """Whether a stride-1 pad-1 3-tap conv over [B, L, c_in] -> c_out takes an input pre-activation (the 128-column
+    tap-shared kernel)."""
+    return bool(_lib_k().ecg_conv1d_nlc_pa_ok(int(B), int(L), int(c_in), int(L), int(c_out), 3, 1, 1, 1))
+
+
+def fwd_pre_act_raw(z: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, w_t: torch.Tensor):
+    """Stride-1 pad-1 3-tap conv of relu(z * scale + shift) (per input channel: a BatchNorm + ReLU folded into the
+    tap-shared kernel's staged operand image).  Returns (y, a) with a the activated operand the kernel stores for the
+    weight gradient.  z [B, L, C_in] bf16, scale / shift [C_in] fp32, w_t [C_out, 3, C_in] bf16."""
+    B, L, Cin = z.shape
+    Cout = w_t.shape[0]
+    if not (z.dtype == w_t.dtype == torch.bfloat16 and z.is_contiguous() and w_t.is_contiguous()
+            and scale.dtype == shift.dtype == torch.float32 and scale.numel() == shift.numel() == Cin):
+        raise ValueError("fwd_pre_act_raw: contiguous bf16 z / w_t and fp32 [C_in] scale / shift required")
+    if not pre_act_ok(B, L, Cin, Cout):
+        raise ValueError("fwd_pre_act_raw: shape not routed to the tap-shared kernel")
+    y = torch.empty((B, L, Cout), dtype=torch.bfloat16, device=z.device)
+    a = torch.empty_like(z)
+    sc, sh = scale.contiguous(), shift.contiguous()
+    pa = (_lib.C.c_void_p * 3)(sc.data_ptr(), sh.data_ptr(), a.data_ptr())
+    st = _lib_k().ecg_conv1d_nlc_fwd_pa(z.data_ptr(), w_t.data_ptr(), None, y.data_ptr(), None, None, None, B, L, Cin,
+                                        L, Cout, 3, 1, 1, 1, 0, None, None, pa, _lib.stream_ptr(z.device))
+    _lib.check(st, "ecg_conv1d_nlc_fwd_pa")
+    return y, a
 
 
 def fwd_raw(x: torch.Tensor, w_t: torch.Tensor, bias: Optional[torch.Tensor], stride: int, pad: int,

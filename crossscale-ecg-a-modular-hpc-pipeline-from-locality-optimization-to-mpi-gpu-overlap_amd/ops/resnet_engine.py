@@ -58,6 +58,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_wgrad_splits", [i32] * 8)
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles_ex", [i32, i32, i32, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_rows", [i32] * 9)
+    _lib._sig(lib, "ecg_conv1d_nlc_pa_ok", [i32] * 9)
     lib._plan_bound = True
     if lib.ecg_plan_op_words() != OP_WORDS or lib.ecg_plan_wentry_bytes() != 40:
         raise _lib.NativeError("resnet plan ABI mismatch (rebuild csrc)")
@@ -330,14 +331,26 @@ class ResNetStepEngine:
         # operand load measured slower than the LDS-DMA loop + BN_ACT pass: 3.85 vs 3.755,
         # profiles/r2/resnet_multi_tile/bn_fold_ab.txt - both removed in round 4)
         def conv(x, Lin, Cin, w_ptr, y, Lout, Cout, K, s, p, dil=1, st=None, add=None, add_mask=None, bnb=None,
-                 tail_ptr=0, lane=0, mbn=None):
+                 tail_ptr=0, lane=0, mbn=None, pa=None):
             # bnb = (mask, z, mean, rstd, zd, mean_d, rstd_d): BN-backward statistics fused into the epilogue;
-            # mbn = (scale, shift): the mask is relu(z * scale + shift) > 0 (mask operand not read)
+            # mbn = (scale, shift): the mask is relu(z * scale + shift) > 0 (mask operand not read);
+            # pa = (scale, shift, out): the operand is relu(x * scale + shift), also stored to out (pre-activation)
             extra = [P(t) if isinstance(t, torch.Tensor) else int(t or 0) for t in (bnb or ())]
             extra += [0] * (7 - len(extra))
             m_words = [P(mbn[0]), P(mbn[1])] if mbn is not None else [0, 0]
+            pa_words = [P(t) for t in pa] if pa is not None else []
             op("CONV_FWD", P(x), w_ptr, 0, P(y), P(st), P(add), P(add_mask), B, Lin, Cin, Lout, Cout, K, s, p, dil, 0,
-               *extra, tail_ptr, *m_words, lane=lane)
+               *extra, tail_ptr, *m_words, *pa_words, lane=lane)
+
+        # BatchNorm + ReLU of a block's first conv folded into the second conv's operand staging (ECG_RESNET_PREACT=1,
+        # default, where that conv is a 128-column tap-shared conv): the tap kernel applies relu(z1 * scale + shift)
+        # to its staged image of z1 and stores a1 for the weight gradient - no BN_ACT pass over the tensor.  Bitwise
+        # the BN_ACT pass (the same fmaf + max + bf16 rounding).
+        use_preact = os.environ.get("ECG_RESNET_PREACT", "1") != "0"
+        self.pre_act = use_preact
+
+        def pre_act_ok(L_, C_in, C_out):
+            return use_preact and bool(self.lib.ecg_conv1d_nlc_pa_ok(B, L_, C_in, L_, C_out, 3, 1, 1, 1))
 
         def wgrad(dy, x, Lin, Cin, Lout, Cout, K, s, p, weight):
             S = wsplits(B * Lout, Cout, K, Cin, s, Lin, Lout)
@@ -373,10 +386,12 @@ class ResNetStepEngine:
                  tail_ptr=tail(T, Co, [fin_fwd_words(b1, B * Lo)]))
             if not use_tail:
                 fin_fwd(b1, T, B * Lo)
-            op("BN_ACT", 0, P(a["z1"]), P(b1.scale), P(b1.shift), 0, 0, 0, P(a["a1"]), B * Lo, Co)
+            pre = pre_act_ok(Lo, Co, Co)
+            if not pre:
+                op("BN_ACT", 0, P(a["z1"]), P(b1.scale), P(b1.shift), 0, 0, 0, P(a["a1"]), B * Lo, Co)
             T2 = rows(Lo, Co, Lo, Co, 3, 1, 1)
-            conv(a["a1"], Lo, Co, self._wf[id(blk.conv2)], a["z2"], Lo, Co, 3, 1, 1, st=stats,
-                 tail_ptr=tail(T2, Co, [fin_fwd_words(b2, B * Lo)]))
+            conv(a["z1"] if pre else a["a1"], Lo, Co, self._wf[id(blk.conv2)], a["z2"], Lo, Co, 3, 1, 1, st=stats,
+                 tail_ptr=tail(T2, Co, [fin_fwd_words(b2, B * Lo)]), pa=(b1.scale, b1.shift, a["a1"]) if pre else None)
             if not use_tail:
                 fin_fwd(b2, T2, B * Lo)
             if bd is not None:

@@ -57,6 +57,13 @@ struct FwdArgs {
   const float* mscale;
   const float* mshift;
   const ecg::BnTail* tail;  // BatchNorm finalize fused into this launch's tail (bn_tail.h), or null
+  // Input pre-activation (pa_scale != null; the 128-column tap-shared kernel only): the GEMM operand is
+  // bf16(relu(fmaf(x, pa_scale, pa_shift))) per input channel - the BatchNorm + ReLU of the conv that produced x,
+  // bitwise the BN_ACT pass - applied to the staged A' image; nt == 0 workgroups store the activated rows of their
+  // tile to pa_out (the weight gradient's operand).
+  const float* pa_scale;
+  const float* pa_shift;
+  __bf16* pa_out;
 };
 
 // A tile: 64 rows (b,t) x 64 kk (one tap k, channels c0..c0+63); element e (0..511) = row e>>3, 8 bf16 part e&7
@@ -561,6 +568,14 @@ __device__ __forceinline__ void dma16_at(srd_t r, unsigned voff, unsigned lds) {
 __device__ __forceinline__ void dma16(srd_t r, unsigned voff, unsigned char* lds_piece) {
   dma16_at(r, voff, lds_addr(lds_piece));
 }
+// 16-byte vector store through a buffer resource (out-of-range offsets are dropped by the range check), from asm so
+// that it is always issued - one vmcnt entry per call, which the counted waits of the tap loop rely on.  The s_nop
+// is the wait state a VALU write of the store's data VGPRs needs after a >8-byte buffer store (hipcc does not pad
+// hazards of an asm statement, MI355X guide §5.7).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16_at(srd_t r, unsigned voff, u32x4 v) {
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 0" ::"v"(v), "v"(voff), "s"(r) : "memory");
+}
 
 // NWR = waves along M: 2 -> 4 waves (2x2), 4 -> 8 waves (4x2, 2 per SIMD at one workgroup per CU).  256-row
 // tiles need one workgroup per CU (2 x 64 KB of stages at 256x256).  Two LDS stages: one K step in flight while the
@@ -822,22 +837,33 @@ constexpr int TAP_AROWS = TAP_BM + 8;       // image rows m0-1 .. m0+262 (258 us
 constexpr int TAP_ASLOT = TAP_AROWS * 128;  // 33,792 B
 constexpr int TAP_NA = 5;                   // DMA instructions per wave per A' image (4 full pieces + 1 row)
 
-template <int BN>
+// Input pre-activation (FwdArgs::pa_*): each wave transforms its OWN DMA pieces of A'(c) in place right after the
+// counted wait that makes them visible and before the step's barrier - the DMA writes lane-linear, so a lane's piece
+// sits at a fixed LDS offset and always holds the same 8 channels of the chunk (source chunk (lane & 7) ^ (row & 7)
+// with row & 7 == (lane >> 3) & 7).  Image rows outside the tensor stay zero (the conv's padding); nt == 0
+// workgroups store their tile's rows (1 .. 256 of the image) for the weight gradient.  Per-channel scale / shift
+// in an LDS table [2][Cin].
+constexpr int PA_MAXC = 512;
+
+template <int BN, bool PA = false>
 struct TapCfg {
   static constexpr int BSLOT = BN * 128;
   static constexpr int BP = BN / 64;  // weight pieces per wave per step (8 waves x 8 rows)
-  static constexpr int STAGES = 2 * TAP_ASLOT + 3 * BSLOT;
+  static constexpr int TOFF = 2 * TAP_ASLOT + 3 * BSLOT;  // pre-activation table (PA)
+  static constexpr int STAGES = TOFF + (PA ? 2 * PA_MAXC * 4 : 0);
   static constexpr int SMEM = STAGES > FwdCfg<TAP_BM, BN, 4>::EP_BYTES ? STAGES : FwdCfg<TAP_BM, BN, 4>::EP_BYTES;
 };
 
-template <int BN, int EPI>
+template <int BN, int EPI, bool PA>
 // (launch bounds: one workgroup per CU is all the ~115 KB of LDS allows; the code object is identical to the one
 // built with a min-blocks hint of 2 - 103-161 VGPRs, no scratch - so the hint now states the real residency)
 __global__ __launch_bounds__(512, 1) void conv1d_nlc_fwd_tap_kernel(FwdArgs a, int MT, int NT) {
   constexpr int BM = TAP_BM, NWR = 4, NW = 8;
   using Cfg = FwdCfg<BM, BN, NWR>;
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
-  constexpr int BP = TapCfg<BN>::BP, BSLOT = TapCfg<BN>::BSLOT;
+  using TC = TapCfg<BN, PA>;
+  constexpr int BP = TC::BP, BSLOT = TC::BSLOT;
+  constexpr int ST = PA ? TAP_NA : 0;  // pre-activation stores per wave per chunk (issued at k = 0)
   static_assert(WM == 64 && FM == 4, "64-row wave tiles");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -880,6 +906,51 @@ __global__ __launch_bounds__(512, 1) void conv1d_nlc_fwd_tap_kernel(FwdArgs a, i
 #pragma unroll
     for (int i = 0; i < BP; ++i) dma16_at(wrs, boff[i] + (k * Cin + c * 64) * 2, base + (wv + NW * i) * 1024);
   };
+  // pre-activation: per-piece row validity, store offsets (image rows 1..256 = the tile's own rows, nt == 0 only;
+  // the rest land out of range and are dropped) and the [2][Cin] scale / shift table
+  srd_t pr{};
+  unsigned soff[TAP_NA];
+  unsigned pvalid = 0u;
+  if constexpr (PA) {
+    pr = make_rsrc(a.pa_out, a.pa_out ? (long)M * Cin * 2 : 0L);
+#pragma unroll
+    for (int i = 0; i < TAP_NA; ++i) {
+      const int row = i < 4 ? 8 * (wv + NW * i) + (lane >> 3) : 256 + (lane >> 3);
+      const int g = m0 - 1 + row;
+      const bool in = g >= 0 && g < M && (i < 4 || (lane >> 3) == wv);
+      pvalid |= (in ? 1u : 0u) << i;
+      soff[i] = (in && nt == 0 && row >= 1 && row <= 256 && a.pa_out) ? aoff[i] : 0x7ffffff0u;
+    }
+    float* tab = reinterpret_cast<float*>(smem + TC::TOFF);
+    for (int ch = tid; ch < Cin; ch += 512) {
+      tab[ch] = a.pa_scale[ch];
+      tab[Cin + ch] = a.pa_shift[ch];
+    }
+    __syncthreads();  // (no DMA in flight yet)
+  }
+  // the wave's own pieces of A'(c) (LDS slot) -> relu(x * scale + shift), stored to pa_out (ST stores, always issued)
+  auto pre_act = [&](int c, int slot) {
+    const float* tab = reinterpret_cast<const float*>(smem + TC::TOFF);
+    const int ch = c * 64 + 8 * ((lane & 7) ^ ((lane >> 3) & 7));
+    float sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sc[e] = tab[ch + e];
+      sh[e] = tab[Cin + ch + e];
+    }
+#pragma unroll
+    for (int i = 0; i < TAP_NA; ++i) {
+      unsigned char* xp = smem + slot * TAP_ASLOT + (i < 4 ? wv + NW * i : 32) * 1024 + lane * 16;
+      const u32x4 xv = *reinterpret_cast<const u32x4*>(xp);
+      const bf16x8 x = __builtin_bit_cast(bf16x8, xv);
+      bf16x8 y;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) y[e] = (__bf16)fmaxf(fmaf((float)x[e], sc[e], sh[e]), 0.f);
+      const u32x4 v = ((pvalid >> i) & 1u) ? __builtin_bit_cast(u32x4, y) : xv;
+      if (i < 4 || (lane >> 3) == wv) *reinterpret_cast<u32x4*>(xp) = v;  // (piece 32: 8 lanes of each wave)
+      st16_at(pr, soff[i] + c * 128, v);
+    }
+  };
   // this lane's fragment rows: i_f = wr*64 + 16f + (lane & 15); tap 0 is invalid at t == 0, tap 2 at t == L-1
   unsigned ok0 = 0u, ok2 = 0u;
 #pragma unroll
@@ -907,12 +978,15 @@ __global__ __launch_bounds__(512, 1) void conv1d_nlc_fwd_tap_kernel(FwdArgs a, i
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int s = 3 * c + k;
-      // wait for weight step s (and, at k == 0, A'(c), issued before it): the younger DMA of this wave is counted
+      // wait for weight step s (and, at k == 0, A'(c), issued before it): the younger vector-memory operations of
+      // this wave are counted - per chunk, in issue order: [ST pre-activation stores] B(3c+2) A'(c+1) at k = 0,
+      // B(3c+3) at k = 1, B(3c+4) at k = 2
       if (k == 0) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BP) : "memory");
+        if constexpr (PA) pre_act(c, c & 1);
       } else if (k == 1) {
-        if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BP + TAP_NA) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BP) : "memory");
+        if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ST + BP + TAP_NA) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ST + BP) : "memory");
       } else {
         if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BP + TAP_NA) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -975,7 +1049,7 @@ using T64Cfg = FwdCfg<T64_BM, 64, 2>;
 constexpr int T64_SMEM = T64_WBYTES + 2 * T64_ASLOT + T64Cfg::EP_BYTES;
 static_assert(2 * T64_SMEM <= 160 * 1024, "two workgroups per CU");
 
-template <int EPI>
+template <int EPI, bool PA = false>
 __global__ __launch_bounds__(256, 2) void conv1d_nlc_tap64_kernel(FwdArgs a, int MT, int GM) {
   constexpr int BM = T64_BM, BN = 64, NWR = 2, NW = 4;
   constexpr int WM = T64Cfg::WM, WN = T64Cfg::WN, FM = T64Cfg::FM, FN = T64Cfg::FN;
@@ -1018,10 +1092,38 @@ __global__ __launch_bounds__(256, 2) void conv1d_nlc_tap64_kernel(FwdArgs a, int
   EpiConst k;
   k.load<EPI == 1>(a, EpiLane<BN, NWR>::n(0));
   const int arow = (wr * WM + (lane & 15)) * 128, brow = (wc * WN + (lane & 15)) * 128;
+  // input pre-activation (FwdArgs::pa_*): a lane's DMA pieces always hold the same 8 channels (the single 64-channel
+  // chunk, source chunk (lane & 7) ^ (row & 7) with row & 7 == (lane >> 3) & 7): their scale / shift in registers
+  float psc[8], psh[8];
+  if constexpr (PA) {
+    const int ch = 8 * ((lane & 7) ^ ((lane >> 3) & 7));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      psc[e] = a.pa_scale[ch + e];
+      psh[e] = a.pa_shift[ch + e];
+    }
+  }
   if (ntiles > 0) issue_a(gm * BM, 0);
   for (int j = 0; j < ntiles; ++j) {  // block-uniform
     const int m0 = (gm + j * GM) * BM;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of A'(j) (and, at j = 0, W) landed
+    if constexpr (PA) {  // this wave's own pieces -> relu(x * scale + shift); image rows 1..128 (the tile) stored
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const int row = i < 4 ? 8 * (wv + NW * i) + (lane >> 3) : 128 + (lane >> 3);
+        const int g = m0 - 1 + row;
+        if ((i < 4 || (lane >> 3) == wv) && g >= 0 && g < M) {
+          bf16x8* xp = reinterpret_cast<bf16x8*>(As + (j & 1) * T64_ASLOT + (i < 4 ? wv + NW * i : 16) * 1024 + lane * 16);
+          const bf16x8 x = *xp;
+          bf16x8 y;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) y[e] = (__bf16)fmaxf(fmaf((float)x[e], psc[e], psh[e]), 0.f);
+          *xp = y;
+          if (a.pa_out && row >= 1 && row <= BM)
+            *reinterpret_cast<bf16x8*>(a.pa_out + (long)g * 64 + 8 * ((lane & 7) ^ (row & 7))) = y;
+        }
+      }
+    }
     __syncthreads();                                  // ... every wave's; slot (j+1)&1 is no longer read
     if (j + 1 < ntiles) issue_a((gm + (j + 1) * GM) * BM, (j + 1) & 1);
     const unsigned char* Aj = As + (j & 1) * T64_ASLOT;
@@ -1095,21 +1197,22 @@ inline int tap64_groups(int B, int Lout) {
   return MT < 2 * cus ? MT : 2 * cus;
 }
 
-template <int EPI>
+template <int EPI, bool PA = false>
 int launch_tap64_t(const FwdArgs& a, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
-    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_tap64_kernel<EPI>,
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_tap64_kernel<EPI, PA>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, T64_SMEM));
     attr = true;
   }
   const int MT = (int)(((long)a.B * a.Lout + T64_BM - 1) / T64_BM), GM = tap64_groups(a.B, a.Lout);
-  hipLaunchKernelGGL((conv1d_nlc_tap64_kernel<EPI>), dim3((unsigned)GM), dim3(256), T64_SMEM, stream, a, MT, GM);
+  hipLaunchKernelGGL((conv1d_nlc_tap64_kernel<EPI, PA>), dim3((unsigned)GM), dim3(256), T64_SMEM, stream, a, MT, GM);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
 
 int launch_tap64(const FwdArgs& a, hipStream_t stream) {
+  if (a.pa_scale) return a.stat_mode == 1 ? launch_tap64_t<1, true>(a, stream) : launch_tap64_t<0, true>(a, stream);
   return a.stat_mode == 1 ? launch_tap64_t<1>(a, stream) : launch_tap64_t<0>(a, stream);
 }
 
@@ -1121,25 +1224,29 @@ inline bool tap_ok(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stri
 }
 inline int tap_mtiles(int B, int Lout) { return (int)(((long)B * Lout + TAP_BM - 1) / TAP_BM); }
 
-template <int BN, int EPI>
+template <int BN, int EPI, bool PA = false>
 int launch_fwd_tap_t(const FwdArgs& a, hipStream_t stream) {
-  constexpr int SMEM = TapCfg<BN>::SMEM;
+  constexpr int SMEM = TapCfg<BN, PA>::SMEM;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static bool attr = false;
   if (!attr) {
-    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_tap_kernel<BN, EPI>,
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_fwd_tap_kernel<BN, EPI, PA>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
     attr = true;
   }
   const int MT = tap_mtiles(a.B, a.Lout), NT = a.Cout / BN;
-  hipLaunchKernelGGL((conv1d_nlc_fwd_tap_kernel<BN, EPI>), dim3((unsigned)(MT * NT)), dim3(512), SMEM, stream, a, MT,
-                     NT);
+  hipLaunchKernelGGL((conv1d_nlc_fwd_tap_kernel<BN, EPI, PA>), dim3((unsigned)(MT * NT)), dim3(512), SMEM, stream, a,
+                     MT, NT);
   ECG_HIP_CHECK(hipGetLastError());
   return ecg::kOk;
 }
 
 int launch_fwd_tap(const FwdArgs& a, hipStream_t stream) {
   const bool b = a.stat_mode == 1;
+  if (a.pa_scale) {  // input pre-activation: 128-column tiles (ecg_conv1d_nlc_pa_ok)
+    if (a.Cout % 128 || a.Cin > PA_MAXC) return ecg::kBadArg;
+    return b ? launch_fwd_tap_t<128, 1, true>(a, stream) : launch_fwd_tap_t<128, 0, true>(a, stream);
+  }
   if (a.Cout % 128 == 0) return b ? launch_fwd_tap_t<128, 1>(a, stream) : launch_fwd_tap_t<128, 0>(a, stream);
   return b ? launch_fwd_tap_t<64, 1>(a, stream) : launch_fwd_tap_t<64, 0>(a, stream);
 }
@@ -2063,11 +2170,39 @@ inline bool wgrad_big(int Cout, int Cin) { return conv_big() >= 2 && Cout % 256 
 // BatchNorm whose backward statistics the data-grad epilogue produces ([2 or 3][M tiles][Cout] into ``stats``);
 // mscale / mshift (both or neither) re-derive the ReLU mask from sz instead of reading smask.
 // ``tail`` (optional, with ``stats``): a BatchNorm finalize fused into this launch (bn_tail.h).
+// Whether ecg_conv1d_nlc_fwd_pa accepts an input pre-activation for this conv (it routes to the persistent
+// 64-channel tap kernel or to the 128-column tap-shared kernel).
+ECG_API int ecg_conv1d_nlc_pa_ok(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad,
+                                 int in_dil) {
+  if (tap64_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return 1;
+  return conv_tap(Cout) && Cout % 128 == 0 && Cin <= PA_MAXC && tap_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)
+             ? 1
+             : 0;
+}
+
+ECG_API int ecg_conv1d_nlc_fwd_pa(const void* x, const void* w, const float* bias, void* y, float* stats,
+                                  const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
+                                  int Kw, int stride, int pad, int in_dil, int relu, const void* const* bnb,
+                                  const void* tail, const void* const* pa, hipStream_t stream);
+
 ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bias, void* y, float* stats,
                                   const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
                                   int Kw, int stride, int pad, int in_dil, int relu, const void* const* bnb,
                                   const void* tail, hipStream_t stream) {
+  return ecg_conv1d_nlc_fwd_pa(x, w, bias, y, stats, add, add_mask, B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil,
+                               relu, bnb, tail, nullptr, stream);
+}
+
+// ecg_conv1d_nlc_fwd_ex with an input pre-activation ``pa`` = {scale, shift, out} (FwdArgs::pa_*; null = none):
+// the conv's operand is bf16(relu(x * scale + shift)) per input channel, and the activated rows are also stored to
+// ``out`` (null: not stored).  Only where ecg_conv1d_nlc_pa_ok holds.
+ECG_API int ecg_conv1d_nlc_fwd_pa(const void* x, const void* w, const float* bias, void* y, float* stats,
+                                  const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
+                                  int Kw, int stride, int pad, int in_dil, int relu, const void* const* bnb,
+                                  const void* tail, const void* const* pa, hipStream_t stream) {
   if (!x || !w || !y || B <= 0 || Lin <= 0 || Lout <= 0 || Kw <= 0 || stride <= 0 || in_dil <= 0 || pad < 0)
+    return ecg::kBadArg;
+  if (pa && (!pa[0] || !pa[1] || !ecg_conv1d_nlc_pa_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)))
     return ecg::kBadArg;
   if (Cin % BK != 0 || Cout % 64 != 0 || (add_mask && !add)) return ecg::kBadArg;
   if (bnb && (!stats || !bnb[1] || !bnb[2] || !bnb[3] || (bnb[4] && (!bnb[5] || !bnb[6])) || (!bnb[7] != !bnb[8])))
@@ -2088,6 +2223,13 @@ ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bia
     a.srstd_d = static_cast<const float*>(bnb[6]);
   }
   a.tail = static_cast<const ecg::BnTail*>(tail);
+  if (pa) {
+    a.pa_scale = static_cast<const float*>(pa[0]);
+    a.pa_shift = static_cast<const float*>(pa[1]);
+    a.pa_out = static_cast<__bf16*>(const_cast<void*>(pa[2]));
+    return tap64_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil) ? launch_tap64(a, stream)
+                                                                      : launch_fwd_tap(a, stream);
+  }
   if (tap64_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return launch_tap64(a, stream);
   if (conv_tap(Cout) && tap_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return launch_fwd_tap(a, stream);
   int bm, bn;

@@ -36,6 +36,11 @@ extern "C" int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* 
                                      const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout,
                                      int Cout, int Kw, int stride, int pad, int in_dil, int relu,
                                      const void* const* bnb, const void* tail, hipStream_t stream);
+extern "C" int ecg_conv1d_nlc_fwd_pa(const void* x, const void* w, const float* bias, void* y, float* stats,
+                                     const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout,
+                                     int Cout, int Kw, int stride, int pad, int in_dil, int relu,
+                                     const void* const* bnb, const void* tail, const void* const* pa,
+                                     hipStream_t stream);
 extern "C" int ecg_conv1d_nlc_wgrad(const void* dy, const void* x, float* part, int splits, int B, int Lin, int Cin,
                                     int Lout, int Cout, int Kw, int stride, int pad, hipStream_t stream);
 extern "C" int ecg_sgd_flat(float* params, const float* grads, float* mom, long n, float lr, float momentum,
@@ -988,13 +993,15 @@ int run_op(const int64_t* o, hipStream_t st) {
   switch (kind) {
     case OP_CONV_FWD: {  // words 18..24: BN-backward statistics operands (stat_mode 1 when o[19] != 0);
                          // word 25: fused BatchNorm finalize (ecg::BnTail in device memory) or 0;
-                         // words 26, 27: scale / shift that re-derive the ReLU mask from sz (or 0: load smask)
+                         // words 26, 27: scale / shift that re-derive the ReLU mask from sz (or 0: load smask);
+                         // words 28..30: input pre-activation {scale, shift, out} (ecg_conv1d_nlc_fwd_pa) or 0
       const void* bnb[9] = {P<void>(o[18]), P<void>(o[19]), P<void>(o[20]), P<void>(o[21]), P<void>(o[22]),
                             P<void>(o[23]), P<void>(o[24]), P<void>(o[26]), P<void>(o[27])};
-      return ecg_conv1d_nlc_fwd_ex(P<void>(o[1]), P<void>(o[2]), P<float>(o[3]), P<void>(o[4]), P<float>(o[5]),
+      const void* pa[3] = {P<void>(o[28]), P<void>(o[29]), P<void>(o[30])};
+      return ecg_conv1d_nlc_fwd_pa(P<void>(o[1]), P<void>(o[2]), P<float>(o[3]), P<void>(o[4]), P<float>(o[5]),
                                    P<void>(o[6]), P<void>(o[7]), (int)o[8], (int)o[9], (int)o[10], (int)o[11],
                                    (int)o[12], (int)o[13], (int)o[14], (int)o[15], (int)o[16], (int)o[17],
-                                   o[19] ? bnb : nullptr, P<void>(o[25]), st);
+                                   o[19] ? bnb : nullptr, P<void>(o[25]), o[28] ? pa : nullptr, st);
     }
     case OP_CONV_WGRAD:
       return ecg_conv1d_nlc_wgrad(P<void>(o[1]), P<void>(o[2]), P<float>(o[3]), (int)o[4], (int)o[5], (int)o[6],

@@ -274,3 +274,37 @@ def test_tap64_forward_matches_fp64(B, L, scale):
     yf = ys.double().reshape(-1, 64)
     torch.testing.assert_close(stats[0].double().sum(0), yf.sum(0), rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(stats[1].double().sum(0), (yf * yf).sum(0), rtol=1e-5, atol=1e-3)
+
+
+PREACT_CASES = [  # stride-1 3-tap convs of the ResNet stages: the persistent 64-channel kernel, the 128-column tap kernel
+    (1024, 125, 64, 64),  # layer 1 at B=1024: 1000 tiles over 512 persistent workgroups (one or two each)
+    (3, 37, 64, 64),  # one ragged 64-channel tile
+    (64, 63, 128, 128),  # layer 2, ragged last tile
+    (40, 32, 256, 256),  # layer 3: 4 chunks, 2 column blocks (only nt == 0 stores the activated rows)
+    (33, 16, 512, 512),  # layer 4: 8 chunks, 4 column blocks
+    (3, 5, 128, 256),  # one tile, most image rows outside the tensor
+]
+
+
+@pytest.mark.parametrize("B,L,Cin,Cout", PREACT_CASES)
+def test_tap_pre_activation_matches_fp64(B, L, Cin, Cout):
+    """Input pre-activation (BatchNorm scale / shift + ReLU applied to the tap-shared kernel's staged A' image): the
+    activated operand it stores equals relu(z * scale + shift) to bf16 rounding, the conv equals an fp64 conv of that
+    stored operand, and the plain tap kernel on the stored operand gives bitwise the same output."""
+    from crossscale_ecg.ops import conv_mc
+    torch.manual_seed(9)
+    z = torch.randn(B, L, Cin, device=DEV).bfloat16()
+    w = (torch.randn(Cout, 3, Cin, device=DEV) / (3 * Cin) ** 0.5).bfloat16()
+    sc = torch.rand(Cin, device=DEV) + 0.5
+    sh = torch.randn(Cin, device=DEV) * 0.5
+    assert conv_mc.pre_act_ok(B, L, Cin, Cout)
+    y, act = conv_mc.fwd_pre_act_raw(z, sc, sh, w)
+    torch.cuda.synchronize()
+    want = torch.relu(z.double() * sc.double() + sh.double())
+    assert (act.double() - want).abs().max().item() <= 8e-3 * want.abs().max().item()
+    assert _rel(act.double(), want) < 4e-3
+    ref = F.conv1d(act.double().transpose(1, 2), w.double().permute(0, 2, 1), None, stride=1, padding=1)
+    got = y.double().transpose(1, 2)
+    assert (got - ref).abs().max().item() <= 8e-3 * ref.abs().max().item()
+    assert _rel(got, ref) < 4e-3
+    assert torch.equal(conv_mc.fwd_raw(act, w, None, 1, 1, L), y)

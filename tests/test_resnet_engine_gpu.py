@@ -402,3 +402,24 @@ def test_engine_gradient_buckets(bucket_mb):
         assert segs[0][1] < layer4_end  # the first bucket closes before layer4's backward ends
         assert all(4 * (h - lo) >= bucket_mb * (1 << 20) for (_, _, lo, h) in segs[:-1])
     eng.close()
+
+
+def test_pre_activation_bitwise_equals_bn_act_pass(monkeypatch):
+    """BatchNorm + ReLU of each block's first conv folded into the second conv's staged operand (ECG_RESNET_PREACT=1,
+    every block's second conv) == the separate BN_ACT pass (0), bit for bit (same fmaf + max + bf16
+    rounding; the persistent 64-channel kernel of layer 1 and the 128-column tap kernel of layers 2-4): two SGD steps
+    of ResNet1D-34, with one plan op fewer per block."""
+    outs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("ECG_RESNET_PREACT", mode)
+        m, ref, eng, x, y = _setup(34, B=64, seed=5)
+        assert eng.pre_act == (mode == "1")
+        eng.step()
+        eng.step()
+        torch.cuda.synchronize()
+        outs.append((eng.flat.clone(), eng.mom.clone(), [b.clone() for b in m.buffers()], eng.n_ops))
+        del eng, m, ref
+    (f0, m0, b0, n0), (f1, m1, b1, n1) = outs
+    assert torch.equal(f0, f1) and torch.equal(m0, m1)
+    assert all(torch.equal(a, b) for a, b in zip(b0, b1))
+    assert n1 == n0 - 16  # one BN_ACT per block
