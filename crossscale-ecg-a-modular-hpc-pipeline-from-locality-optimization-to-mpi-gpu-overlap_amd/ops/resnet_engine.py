@@ -179,7 +179,8 @@ class ResNetStepEngine:
         self.h0 = self._t(B, Lp, 64)
         acts = []
         for (Li, Ci, Lo, Co, s), blk in zip(shapes, blocks):
-            a = dict(z1=self._t(B, Lo, Co), a1=self._t(B, Lo, Co), z2=self._t(B, Lo, Co), out=self._t(B, Lo, Co))
+            a = dict(z1=self._t(B, Lo, Co), a1=self._t(B, Lo, Co), z2=self._t(B, Lo, Co), out=self._t(B, Lo, Co),
+                     mb=self._t(B * Lo * Co // 8, dtype=torch.uint8))  # out's ReLU mask, one bit per element
             if blk.downsample is not None:
                 a["zd"] = self._t(B, Lo, Co)
             acts.append(a)
@@ -331,16 +332,17 @@ class ResNetStepEngine:
         # operand load measured slower than the LDS-DMA loop + BN_ACT pass: 3.85 vs 3.755,
         # profiles/r2/resnet_multi_tile/bn_fold_ab.txt - both removed in round 4)
         def conv(x, Lin, Cin, w_ptr, y, Lout, Cout, K, s, p, dil=1, st=None, add=None, add_mask=None, bnb=None,
-                 tail_ptr=0, lane=0, mbn=None, pa=None):
+                 tail_ptr=0, lane=0, mbn=None, pa=None, mask_bits=False):
             # bnb = (mask, z, mean, rstd, zd, mean_d, rstd_d): BN-backward statistics fused into the epilogue;
             # mbn = (scale, shift): the mask is relu(z * scale + shift) > 0 (mask operand not read);
-            # pa = (scale, shift, out): the operand is relu(x * scale + shift), also stored to out (pre-activation)
+            # pa = (scale, shift, out): the operand is relu(x * scale + shift), also stored to out (pre-activation);
+            # mask_bits: bnb's mask is the bit mask a BN_ACT pass wrote (flag bit 1 of the relu word)
             extra = [P(t) if isinstance(t, torch.Tensor) else int(t or 0) for t in (bnb or ())]
             extra += [0] * (7 - len(extra))
             m_words = [P(mbn[0]), P(mbn[1])] if mbn is not None else [0, 0]
             pa_words = [P(t) for t in pa] if pa is not None else []
-            op("CONV_FWD", P(x), w_ptr, 0, P(y), P(st), P(add), P(add_mask), B, Lin, Cin, Lout, Cout, K, s, p, dil, 0,
-               *extra, tail_ptr, *m_words, *pa_words, lane=lane)
+            op("CONV_FWD", P(x), w_ptr, 0, P(y), P(st), P(add), P(add_mask), B, Lin, Cin, Lout, Cout, K, s, p, dil,
+               2 if mask_bits else 0, *extra, tail_ptr, *m_words, *pa_words, lane=lane)
 
         # BatchNorm + ReLU of a block's first conv folded into the second conv's operand staging (ECG_RESNET_PREACT=1,
         # default, where that conv is a 128-column tap-shared conv): the tap kernel applies relu(z1 * scale + shift)
@@ -401,9 +403,9 @@ class ResNetStepEngine:
                 if not use_tail:
                     fin_fwd(bd, Td, B * Lo)
                 op("BN_ACT", 2, P(a["z2"]), P(b2.scale), P(b2.shift), P(a["zd"]), P(bd.scale), P(bd.shift),
-                   P(a["out"]), B * Lo, Co, lane=2)
+                   P(a["out"]), B * Lo, Co, P(a["mb"]), lane=2)
             else:
-                op("BN_ACT", 1, P(a["z2"]), P(b2.scale), P(b2.shift), P(xin), 0, 0, P(a["out"]), B * Lo, Co)
+                op("BN_ACT", 1, P(a["z2"]), P(b2.scale), P(b2.shift), P(xin), 0, 0, P(a["out"]), B * Lo, Co, P(a["mb"]))
             a["in"] = xin
             xin = a["out"]
 
@@ -480,8 +482,9 @@ class ResNetStepEngine:
                 Tn = rows(Lo, Co, Li, Ci, 3, 1, 1, s)  # phase-decomposed when s > 1
                 fins = [fin_bwd_words(pb2, B * Li, 1)] + ([fin_bwd_words(pbd, B * Li, 2)] if pbd else [])
                 conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=add, st=stats_b,
-                     bnb=(pa["out"], pa["z2"], pb2.mean, pb2.rstd, pa.get("zd") if pbd else 0,
-                          pbd.mean if pbd else 0, pbd.rstd if pbd else 0), tail_ptr=tail(Tn, Ci, fins))
+                     bnb=(pa["mb"], pa["z2"], pb2.mean, pb2.rstd, pa.get("zd") if pbd else 0,
+                          pbd.mean if pbd else 0, pbd.rstd if pbd else 0), tail_ptr=tail(Tn, Ci, fins),
+                     mask_bits=True)
                 bn2_src = (stats_b.data_ptr(), Tn, use_tail)
             else:  # into the stem: plain gradient wrt the pooled activations
                 conv(dz1, Lo, Co, self._wb[id(blk.conv1)], din, Li, Ci, 3, 1, 1, dil=s, add=add)

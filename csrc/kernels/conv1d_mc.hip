@@ -57,6 +57,9 @@ struct FwdArgs {
   const float* mscale;
   const float* mshift;
   const ecg::BnTail* tail;  // BatchNorm finalize fused into this launch's tail (bn_tail.h), or null
+  // ReLU mask as bits (stat_mode 1, instead of smask): byte i of smask_bits holds (smask[8i + e] > 0) in bit e, one
+  // byte per 8-channel vector - what the block-output BN_ACT pass writes beside its output (1/16 of the bytes)
+  const uint8_t* smask_bits;
   // Input pre-activation (pa_scale != null; the 128-column tap-shared kernel only): the GEMM operand is
   // bf16(relu(fmaf(x, pa_scale, pa_shift))) per input channel - the BatchNorm + ReLU of the conv that produced x,
   // bitwise the BN_ACT pass - applied to the staged A' image; nt == 0 workgroups store the activated rows of their
@@ -206,6 +209,10 @@ __device__ __forceinline__ void fwd_epi_tile_rowwise(const FwdArgs& a, f32x4 (&a
             const __bf16 act = (__bf16)fmaxf(fmaf((float)zz[e], k.msc[e], k.msh[e]), 0.f);
             v[e] = (float)act > 0.f ? v[e] : 0.f;
           }
+        } else if (bwd && a.smask_bits != nullptr) {
+          const unsigned mb = a.smask_bits[o >> 3];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = (mb >> e) & 1u ? v[e] : 0.f;
         } else if (bwd && a.smask != nullptr) {
           const bf16x8 mk = *reinterpret_cast<const bf16x8*>(a.smask + o);
 #pragma unroll
@@ -257,7 +264,8 @@ __device__ __forceinline__ void fwd_epi_tile_pref(const FwdArgs& a, f32x4 (&acc)
   const int n = EpiLane<BN, NWR>::n(n0);
   constexpr bool bwd = EPI == 1;  // compile-time: the forward epilogue carries none of the backward code
   const bool ds = bwd && a.szd != nullptr;
-  const bool mk_smask = bwd && a.mscale == nullptr && a.smask != nullptr;
+  const bool mk_bits = bwd && a.mscale == nullptr && a.smask_bits != nullptr;
+  const bool mk_smask = bwd && a.mscale == nullptr && !mk_bits && a.smask != nullptr;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     // The half's global operands (z, z_d, residual gradient and its mask) for all ITEMS rows are issued before the
@@ -266,6 +274,7 @@ __device__ __forceinline__ void fwd_epi_tile_pref(const FwdArgs& a, f32x4 (&acc)
     long po[ITEMS];
     bool pv[ITEMS];
     bf16x8 pz[ITEMS], pzd[ITEMS], pad[ITEMS], pmk[ITEMS];
+    unsigned pmb[ITEMS];
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
       const int r = h * HR + rs + it * RSTEP;
@@ -279,6 +288,7 @@ __device__ __forceinline__ void fwd_epi_tile_pref(const FwdArgs& a, f32x4 (&acc)
       if (a.add) pad[it] = *reinterpret_cast<const bf16x8*>(a.add + po[it]);
       if (a.add && a.add_mask) pmk[it] = *reinterpret_cast<const bf16x8*>(a.add_mask + po[it]);
       else if (mk_smask) pmk[it] = *reinterpret_cast<const bf16x8*>(a.smask + po[it]);
+      if (mk_bits) pmb[it] = a.smask_bits[po[it] >> 3];
     }
     if (h) __syncthreads();  // previous half fully read
 #pragma unroll
@@ -318,6 +328,9 @@ __device__ __forceinline__ void fwd_epi_tile_pref(const FwdArgs& a, f32x4 (&acc)
             const __bf16 act = (__bf16)fmaxf(fmaf((float)zz[e], k.msc[e], k.msh[e]), 0.f);
             v[e] = (float)act > 0.f ? v[e] : 0.f;
           }
+        } else if (mk_bits) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = (pmb[it] >> e) & 1u ? v[e] : 0.f;
         } else if (mk_smask) {
           const bf16x8 mk = a.add && a.add_mask ? *reinterpret_cast<const bf16x8*>(a.smask + o) : pmk[it];
 #pragma unroll
@@ -2166,6 +2179,7 @@ inline bool wgrad_big(int Cout, int Cin) { return conv_big() >= 2 && Cout % 256 
 // in_dil > 1 reads x as zero-inserted with that dilation (used for the data-gradient of strided convs).
 // Extended form used by the ResNet step plan: ``stats`` receives [2][ceil(B*Lout/64)][Cout] BN partials;
 // ``add`` (optionally masked by ``add_mask`` > 0) is added to the output before rounding.
+// ``relu``: bit 0 = ReLU on the output; bit 1 = bnb[0] is the mask as bits (FwdArgs::smask_bits).
 // ``bnb`` (optional, stat_mode 1): {smask, sz, smean, srstd, szd, smean_d, srstd_d, mscale, mshift} of the
 // BatchNorm whose backward statistics the data-grad epilogue produces ([2 or 3][M tiles][Cout] into ``stats``);
 // mscale / mshift (both or neither) re-derive the ReLU mask from sz instead of reading smask.
@@ -2210,11 +2224,14 @@ ECG_API int ecg_conv1d_nlc_fwd_pa(const void* x, const void* w, const float* bia
   if (tail && !stats) return ecg::kBadArg;
   FwdArgs a{static_cast<const __bf16*>(x), static_cast<const __bf16*>(w), bias, static_cast<__bf16*>(y), stats,
             static_cast<const __bf16*>(add), static_cast<const __bf16*>(add_mask),
-            B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil, relu, bnb ? 1 : 0};
+            B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil, relu & 1, bnb ? 1 : 0};
   if (bnb) {
     a.mscale = static_cast<const float*>(bnb[7]);
     a.mshift = static_cast<const float*>(bnb[8]);
-    a.smask = static_cast<const __bf16*>(bnb[0]);
+    if (relu & 2)  // the mask operand is a bit mask (FwdArgs::smask_bits)
+      a.smask_bits = static_cast<const uint8_t*>(bnb[0]);
+    else
+      a.smask = static_cast<const __bf16*>(bnb[0]);
     a.sz = static_cast<const __bf16*>(bnb[1]);
     a.smean = static_cast<const float*>(bnb[2]);
     a.srstd = static_cast<const float*>(bnb[3]);

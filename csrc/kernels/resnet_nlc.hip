@@ -421,13 +421,15 @@ __global__ __launch_bounds__(1024) void bn_fin1_kernel(FinArgs a) {
   }
 }
 
-// MODE 0: out = relu(z*scale + shift); 1: out = relu(z*scale + shift + res); 2: + (zd*scale_d + shift_d)
+// MODE 0: out = relu(z*scale + shift); 1: out = relu(z*scale + shift + res); 2: + (zd*scale_d + shift_d).
+// mbits (optional): the ReLU mask of out as one byte per 8-channel vector (bit e: out[e] > 0) - the backward's
+// data-grad epilogue reads it instead of out (FwdArgs::smask_bits: 1/16 of the bytes).
 template <int MODE>
 __global__ __launch_bounds__(TPB) void bn_act_kernel(const __bf16* __restrict__ z, const float* __restrict__ scale,
                                                      const float* __restrict__ shift, const __bf16* __restrict__ res,
                                                      const float* __restrict__ scale_d,
                                                      const float* __restrict__ shift_d, __bf16* __restrict__ out,
-                                                     long R, int C) {
+                                                     long R, int C, uint8_t* __restrict__ mbits) {
   const int cg = C / 8;
   const long nv = R * cg;
   int cur = -1;  // the thread's channel group, fixed under bn_pass_grid: coefficients loaded once
@@ -460,6 +462,12 @@ __global__ __launch_bounds__(TPB) void bn_act_kernel(const __bf16* __restrict__ 
 #pragma unroll
     for (int i = 0; i < 8; ++i) y[i] = fmaxf(y[i], 0.f);
     st8(out + o, y);
+    if (mbits) {
+      unsigned mb = 0u;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mb |= ((float)(__bf16)y[i] > 0.f ? 1u : 0u) << i;  // the stored value's sign
+      mbits[v] = (uint8_t)mb;
+    }
   }
 }
 
@@ -1057,14 +1065,15 @@ int run_op(const int64_t* o, hipStream_t st) {
       const dim3 g(bn_pass_grid(R, C));
       if (mode == 0)
         hipLaunchKernelGGL(bn_act_kernel<0>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]), P<const float>(o[3]),
-                           P<const float>(o[4]), nullptr, nullptr, nullptr, P<__bf16>(o[8]), R, C);
+                           P<const float>(o[4]), nullptr, nullptr, nullptr, P<__bf16>(o[8]), R, C, P<uint8_t>(o[11]));
       else if (mode == 1)
         hipLaunchKernelGGL(bn_act_kernel<1>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]), P<const float>(o[3]),
-                           P<const float>(o[4]), P<const __bf16>(o[5]), nullptr, nullptr, P<__bf16>(o[8]), R, C);
+                           P<const float>(o[4]), P<const __bf16>(o[5]), nullptr, nullptr, P<__bf16>(o[8]), R, C,
+                           P<uint8_t>(o[11]));
       else
         hipLaunchKernelGGL(bn_act_kernel<2>, g, dim3(TPB), 0, st, P<const __bf16>(o[2]), P<const float>(o[3]),
                            P<const float>(o[4]), P<const __bf16>(o[5]), P<const float>(o[6]), P<const float>(o[7]),
-                           P<__bf16>(o[8]), R, C);
+                           P<__bf16>(o[8]), R, C, P<uint8_t>(o[11]));
       break;
     }
     case OP_BN_BWD_REDUCE: {

@@ -301,7 +301,7 @@ def test_engine_teacher_forced_numerics(depth):
         bn = {"bn1": pbn(blk.bn1), "bn2": pbn(blk.bn2)}
         if ds:
             bn["ds"] = pbn(blk.downsample[1])
-        t = {k: _ncl(v) for k, v in a.items()}
+        t = {k: _ncl(v) for k, v in a.items() if v.dim() == 3}  # (mb: the bit mask)
         fw = block_forward_reference(t["in"], t["z1"], t["a1"], t["z2"], t.get("zd"), W(blk.conv1.weight),
                                      W(blk.conv2.weight), W(blk.downsample[0].weight) if ds else None, bn, s, eps)
         for k, want in fw.items():
@@ -325,7 +325,7 @@ def test_engine_teacher_forced_numerics(depth):
         blk, a, shp = eng._blocks[bi], eng._acts[bi], eng._shapes[bi]
         Li, Ci, Lo, Co, _ = shp
         G = _flat(gin.clone(), B, Lo, Co)
-        t = {k: _ncl(v) for k, v in a.items()}
+        t = {k: _ncl(v) for k, v in a.items() if v.dim() == 3}  # (mb: the bit mask)
         if bi == len(eng._blocks) - 1:  # the head's gradient is masked by the block's output ReLU in place
             G = G * (t["out"] > 0)
         eng._run(b0, b1)
