@@ -1034,7 +1034,7 @@ __global__ __launch_bounds__(512, 1) void conv1d_nlc_fwd_tap_kernel(FwdArgs a, i
   __syncthreads();  // the epilogue reuses the stage buffers
   EpiConst k;
   k.load<EPI == 1>(a, EpiLane<BN, NWR>::n(n0));
-  fwd_epi_tile<BM, BN, EPI, NWR, false>(a, acc, smem, k, m0, n0, L, M, 1, 0);
+  fwd_epi_tile<BM, BN, EPI, NWR, EPI == 1>(a, acc, smem, k, m0, n0, L, M, 1, 0);
   if (a.stats) fwd_epi_stats<BM, BN, EPI, NWR>(a, smem, k, n0, mt, MT);  // block-uniform
   if (a.tail && a.stats)
     ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, MT, a.Cout, mt, n0, BN, smem);
