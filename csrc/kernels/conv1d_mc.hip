@@ -1225,7 +1225,7 @@ int launch_tap64_t(const FwdArgs& a, hipStream_t stream) {
 }
 
 int launch_tap64(const FwdArgs& a, hipStream_t stream) {
-  if (a.pa_scale) return a.stat_mode == 1 ? launch_tap64_t<1, true>(a, stream) : launch_tap64_t<0, true>(a, stream);
+  if (a.pa_scale) return a.stat_mode == 1 ? ecg::kBadArg : launch_tap64_t<0, true>(a, stream);  // (forward convs)
   return a.stat_mode == 1 ? launch_tap64_t<1>(a, stream) : launch_tap64_t<0>(a, stream);
 }
 
@@ -1256,9 +1256,9 @@ int launch_fwd_tap_t(const FwdArgs& a, hipStream_t stream) {
 
 int launch_fwd_tap(const FwdArgs& a, hipStream_t stream) {
   const bool b = a.stat_mode == 1;
-  if (a.pa_scale) {  // input pre-activation: 128-column tiles (ecg_conv1d_nlc_pa_ok)
-    if (a.Cout % 128 || a.Cin > PA_MAXC) return ecg::kBadArg;
-    return b ? launch_fwd_tap_t<128, 1, true>(a, stream) : launch_fwd_tap_t<128, 0, true>(a, stream);
+  if (a.pa_scale) {  // input pre-activation (forward convs): 128-column tiles (ecg_conv1d_nlc_pa_ok)
+    if (b || a.Cout % 128 || a.Cin > PA_MAXC) return ecg::kBadArg;
+    return launch_fwd_tap_t<128, 0, true>(a, stream);
   }
   if (a.Cout % 128 == 0) return b ? launch_fwd_tap_t<128, 1>(a, stream) : launch_fwd_tap_t<128, 0>(a, stream);
   return b ? launch_fwd_tap_t<64, 1>(a, stream) : launch_fwd_tap_t<64, 0>(a, stream);
@@ -2209,7 +2209,7 @@ ECG_API int ecg_conv1d_nlc_fwd_ex(const void* x, const void* w, const float* bia
 
 // ecg_conv1d_nlc_fwd_ex with an input pre-activation ``pa`` = {scale, shift, out} (FwdArgs::pa_*; null = none):
 // the conv's operand is bf16(relu(x * scale + shift)) per input channel, and the activated rows are also stored to
-// ``out`` (null: not stored).  Only where ecg_conv1d_nlc_pa_ok holds.
+// ``out`` (null: not stored).  Forward convs (no ``bnb``) where ecg_conv1d_nlc_pa_ok holds.
 ECG_API int ecg_conv1d_nlc_fwd_pa(const void* x, const void* w, const float* bias, void* y, float* stats,
                                   const void* add, const void* add_mask, int B, int Lin, int Cin, int Lout, int Cout,
                                   int Kw, int stride, int pad, int in_dil, int relu, const void* const* bnb,
