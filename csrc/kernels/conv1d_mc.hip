@@ -60,7 +60,7 @@ struct FwdArgs {
   // ReLU mask as bits (stat_mode 1, instead of smask): byte i of smask_bits holds (smask[8i + e] > 0) in bit e, one
   // byte per 8-channel vector - what the block-output BN_ACT pass writes beside its output (1/16 of the bytes)
   const uint8_t* smask_bits;
-  // Input pre-activation (pa_scale != null; the 128-column tap-shared kernel only): the GEMM operand is
+  // Input pre-activation (pa_scale != null; forward convs on the tap-shared kernels only): the GEMM operand is
   // bf16(relu(fmaf(x, pa_scale, pa_shift))) per input channel - the BatchNorm + ReLU of the conv that produced x,
   // bitwise the BN_ACT pass - applied to the staged A' image; nt == 0 workgroups store the activated rows of their
   // tile to pa_out (the weight gradient's operand).
@@ -868,8 +868,8 @@ struct TapCfg {
 };
 
 template <int BN, int EPI, bool PA>
-// (launch bounds: one workgroup per CU is all the ~115 KB of LDS allows; the code object is identical to the one
-// built with a min-blocks hint of 2 - 103-161 VGPRs, no scratch - so the hint now states the real residency)
+// (launch bounds: one workgroup per CU is all the ~115 KB of LDS allows; 103-228 VGPRs per variant (two waves per
+// SIMD allow 256), no scratch)
 __global__ __launch_bounds__(512, 1) void conv1d_nlc_fwd_tap_kernel(FwdArgs a, int MT, int NT) {
   constexpr int BM = TAP_BM, NWR = 4, NW = 8;
   using Cfg = FwdCfg<BM, BN, NWR>;
