@@ -39,6 +39,7 @@ def _bind(lib):
     _lib._sig(lib, "ecg_conv1d_nlc_set_tap", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_set_tap64", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_set_dma_dil", [i32])
+    _lib._sig(lib, "ecg_conv1d_nlc_set_tap_s2", [i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_ex", [vp] * 7 + [i32] * 10 + [vp, vp, vp])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_tiles", [_lib.C.c_long, i32])
     _lib._sig(lib, "ecg_conv1d_nlc_fwd_stat_rows", [i32] * 9)
@@ -70,6 +71,13 @@ def set_tap_shared(mode: int) -> int:
     """Tap-shared 256-row forward/data-grad kernel for stride-1 pad-1 3-tap convs (0: off, 1 (default): outputs with
     C_out % 128 == 0, 2: also 64-channel outputs); returns the previous mode.  Build step plans after setting it."""
     return _lib_k().ecg_conv1d_nlc_set_tap(int(mode))
+
+
+def set_tap_s2(on: bool) -> int:
+    """Tap-shared strided data-grad kernel (the data-grads of stride-2 pad-1 3-tap convs: one staged dz image per
+    chunk read by both output phases) (True, default) or the phase-decomposed one-tap kernels; returns the previous
+    setting.  Build step plans after setting it."""
+    return _lib_k().ecg_conv1d_nlc_set_tap_s2(1 if on else 0)
 
 
 def set_tap64(on: bool) -> int:

@@ -158,6 +158,8 @@ __device__ __forceinline__ void fwd_epi_tile_rowwise(const FwdArgs& a, f32x4 (&a
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1;
+  // ph < 0: the strided tap data-grad's layout - wave row wr holds phase wr >> 1, rows (wr & 1) * WM of the phase
+  const int wph = ph < 0 ? wr >> 1 : ph, wrow = ph < 0 ? (wr & 1) * WM : wr * WM;
   constexpr int EP_LD = Cfg::EP_LD, HR = WM / 2;
   float* ep = reinterpret_cast<float*>(smem) + wv * HR * EP_LD;
   constexpr int CG = WN / 8, RSTEP = 64 / CG, ITEMS = HR / RSTEP;
@@ -180,9 +182,9 @@ __device__ __forceinline__ void fwd_epi_tile_rowwise(const FwdArgs& a, f32x4 (&a
     for (int it = 0; it < ITEMS; ++it) {
       const int rl = rs + it * RSTEP;
       const int r = h * HR + rl;
-      const int m = m0 + wr * WM + r;
+      const int m = m0 + wrow + r;
       const int bb = m / Lrow, tt = m - bb * Lrow;
-      const int uu = P > 1 ? tt * P + ph : tt;
+      const int uu = P > 1 ? tt * P + wph : tt;
       if (m < M && uu < a.Lout) {
         const long o = ((long)bb * a.Lout + uu) * a.Cout + n;
         const float4 v0 = *reinterpret_cast<const float4*>(ep + rl * EP_LD + cg * 8);
@@ -257,6 +259,7 @@ __device__ __forceinline__ void fwd_epi_tile_pref(const FwdArgs& a, f32x4 (&acc)
   constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1;
+  const int wph = ph < 0 ? wr >> 1 : ph, wrow = ph < 0 ? (wr & 1) * WM : wr * WM;  // (ph < 0: see the rowwise form)
   constexpr int EP_LD = Cfg::EP_LD, HR = WM / 2;
   float* ep = reinterpret_cast<float*>(smem) + wv * HR * EP_LD;
   constexpr int CG = WN / 8, RSTEP = 64 / CG, ITEMS = HR / RSTEP;
@@ -278,9 +281,9 @@ __device__ __forceinline__ void fwd_epi_tile_pref(const FwdArgs& a, f32x4 (&acc)
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
       const int r = h * HR + rs + it * RSTEP;
-      const int m = m0 + wr * WM + r;
+      const int m = m0 + wrow + r;
       const int bb = m / Lrow, tt = m - bb * Lrow;
-      const int uu = P > 1 ? tt * P + ph : tt;
+      const int uu = P > 1 ? tt * P + wph : tt;
       pv[it] = m < M && uu < a.Lout;
       po[it] = pv[it] ? ((long)bb * a.Lout + uu) * a.Cout + n : 0;
       if constexpr (bwd) pz[it] = *reinterpret_cast<const bf16x8*>(a.sz + po[it]);
@@ -1040,6 +1043,149 @@ __global__ __launch_bounds__(512, 1) void conv1d_nlc_fwd_tap_kernel(FwdArgs a, i
     ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, MT, a.Cout, mt, n0, BN, smem);
 }
 
+// ------------------------------------------------------------------ tap-shared strided data-grad
+// The data-grad of a stride-2, pad-1, 3-tap conv (the first conv of a ResNet stage): dx[u] = sum_k W'[k] dz_dil[u + k
+// - 1] over the zero-inserted dz.  Output u = 2i + ph: phase 0 takes tap 1 at dz row i, phase 1 takes tap 0 at row i
+// and tap 2 at row i + 1 (inside the sample).  So both phases of the output rows 2i, 2i+1 for i in a 128-row range
+// read the SAME dz rows [i0, i0 + 129): the workgroup stages that A' image once per 64-channel chunk and its three
+// taps read it at row offsets 0 / 0 / 1 - the tap-shared kernel's structure, at half its MACs per tile (the
+// phase-decomposed one-tap kernel restages the rows for every tap and phase).  256 output rows per tile (128 i-rows
+// x 2 phases), 8 waves as 4 x 2: wave row wr computes phase wr >> 1, i-rows (wr & 1) * 64 .. + 64, so phase-0 waves
+// run the MFMAs of tap 1 and phase-1 waves those of taps 0 and 2 (wave-uniform).  The epilogue maps the rows back
+// to u = 2i + ph (fwd_epi_tile with ph < 0).  LDS: two A' slots [136 rows][128 B], three weight slots [BN][128 B].
+constexpr int S2_IR = 128;                 // i-rows per tile
+constexpr int S2_AROWS = S2_IR + 8;        // image rows i0 .. i0 + 135 (129 used): 17 DMA pieces of 8 rows
+constexpr int S2_ASLOT = S2_AROWS * 128;   // 17,408 B
+constexpr int S2_NA = 3;                   // DMA instructions per wave per A' image (2 full pieces + 1 row)
+
+template <int BN>
+struct TapS2Cfg {
+  static constexpr int BSLOT = BN * 128;
+  static constexpr int BP = BN / 64;
+  static constexpr int STAGES = 2 * S2_ASLOT + 3 * BSLOT;
+  static constexpr int SMEM = STAGES > FwdCfg<TAP_BM, BN, 4>::EP_BYTES ? STAGES : FwdCfg<TAP_BM, BN, 4>::EP_BYTES;
+};
+
+template <int BN, int EPI>
+__global__ __launch_bounds__(512, 1) void conv1d_nlc_dgrad_s2_tap_kernel(FwdArgs a, int MT, int NT) {
+  constexpr int NWR = 4, NW = 8;
+  using Cfg = FwdCfg<TAP_BM, BN, NWR>;
+  constexpr int WM = Cfg::WM, WN = Cfg::WN, FM = Cfg::FM, FN = Cfg::FN;
+  constexpr int BP = TapS2Cfg<BN>::BP, BSLOT = TapS2Cfg<BN>::BSLOT;
+  static_assert(WM == 64 && FM == 4, "64-row wave tiles");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wv >> 1, wc = wv & 1, ph = wr >> 1, irow0 = (wr & 1) * WM;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int mt = wgid / NT, nt = wgid % NT;
+  const int Lz = a.Lin, Mi = a.B * Lz;  // dz rows per sample / in total (the i-rows)
+  const int i0 = mt * S2_IR, n0 = nt * BN;
+  const int Cin = a.Cin, CB = Cin / 64, K3 = 3 * Cin;
+  const srd_t xr = make_rsrc(a.x, (long)Mi * Cin * 2);
+  const srd_t wrs = make_rsrc(a.w, (long)a.Cout * K3 * 2);
+  const unsigned lds0 = lds_addr(smem);
+  const unsigned ldsA = lds0, ldsB = lds0 + 2 * S2_ASLOT;
+  // A' DMA: pieces p = wv + 8i (i < 2) cover image rows 8p .. 8p+7; piece 16 (rows 128..135) by every wave with lanes
+  // 8wv .. 8wv+7 only (row 128 + wv).  Image row r <-> dz row i0 + r; rows past the tensor land as zeros.
+  unsigned aoff[S2_NA];
+#pragma unroll
+  for (int i = 0; i < S2_NA; ++i) {
+    const int row = i < 2 ? 8 * (wv + NW * i) + (lane >> 3) : S2_IR + (lane >> 3);
+    const int g = i0 + row;
+    const int src = (lane & 7) ^ (row & 7);
+    aoff[i] = g < Mi ? (unsigned)(g * Cin * 2 + src * 16) : 0x7ffffff0u;
+  }
+  unsigned boff[BP];
+#pragma unroll
+  for (int i = 0; i < BP; ++i) {
+    const int n = 8 * (wv + NW * i) + (lane >> 3);
+    boff[i] = (unsigned)((n0 + n) * K3 * 2 + (((lane & 7) ^ (n & 7)) * 16));
+  }
+  auto issue_a = [&](int c, int slot) {
+    const unsigned base = ldsA + slot * S2_ASLOT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) dma16_at(xr, aoff[i] + c * 128, base + (wv + NW * i) * 1024);
+    if ((lane >> 3) == wv) dma16_at(xr, aoff[2] + c * 128, base + 16 * 1024);
+  };
+  auto issue_b = [&](int c, int k, int slot) {
+    const unsigned base = ldsB + slot * BSLOT;
+#pragma unroll
+    for (int i = 0; i < BP; ++i) dma16_at(wrs, boff[i] + (k * Cin + c * 64) * 2, base + (wv + NW * i) * 1024);
+  };
+  // phase 1, tap 2 reads dz row i + 1: invalid at the sample's last row
+  unsigned ok2 = 0u;
+#pragma unroll
+  for (int f = 0; f < FM; ++f) {
+    const int m = i0 + irow0 + 16 * f + (lane & 15);
+    const int t = m - (m / Lz) * Lz;
+    ok2 |= (t != Lz - 1 ? 1u : 0u) << f;
+  }
+  const int arow = (irow0 + (lane & 15)) * 128, brow = (wc * WN + (lane & 15)) * 128;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = 3 * CB;
+  issue_a(0, 0);
+  issue_b(0, 0, 0);
+  issue_b(0, 1, 1);
+  for (int c = 0; c < CB; ++c) {
+    const bool more = c + 1 < CB;  // block-uniform
+    const unsigned char* As = smem + (c & 1) * S2_ASLOT;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int s = 3 * c + k;
+      // the tap-shared kernel's counted waits (S2_NA A' instructions per chunk)
+      if (k == 0) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BP) : "memory");
+      } else if (k == 1) {
+        if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BP + S2_NA) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BP) : "memory");
+      } else {
+        if (more) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(BP + S2_NA) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (s + 2 < nk) issue_b((s + 2) / 3, (k + 2) % 3, (k + 2) % 3);
+      if (k == 0 && more) issue_a(c + 1, (c + 1) & 1);
+      if ((ph == 0) != (k == 1)) continue;  // wave-uniform: phase 0 takes tap 1, phase 1 taps 0 and 2
+      const int off = k == 2 ? 1 : 0;
+      const unsigned char* Bs = smem + 2 * S2_ASLOT + k * BSLOT;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int cc = 4 * ks + (lane >> 4);
+        const int asw = (cc ^ ((lane + off) & 7)) << 4, bsw = (cc ^ (lane & 7)) << 4;
+        bf16x8 af[FM], bfr[FN];
+#pragma unroll
+        for (int f = 0; f < FM; ++f) {
+          af[f] = *reinterpret_cast<const bf16x8*>(As + arow + (16 * f + off) * 128 + asw);
+          if (k == 2 && !((ok2 >> f) & 1u)) af[f] = bf16x8{};
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + brow + 16 * j * 128 + bsw);
+#pragma unroll
+        for (int f = 0; f < FM; ++f)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[f][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[f], bfr[j], acc[f][j], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // the epilogue reuses the stage buffers
+  EpiConst kc;
+  kc.load<EPI == 1>(a, EpiLane<BN, NWR>::n(n0));
+  fwd_epi_tile<TAP_BM, BN, EPI, NWR, EPI == 1>(a, acc, smem, kc, i0, n0, Lz, Mi, 2, -1);
+  if (a.stats) fwd_epi_stats<TAP_BM, BN, EPI, NWR>(a, smem, kc, n0, mt, MT);  // block-uniform
+  if (a.tail && a.stats)
+    ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, MT, a.Cout, mt, n0, BN, smem);
+}
+
 // ------------------------------------------------------------------ persistent tap-shared 64-channel kernel
 // The 64-channel stage (C_in = C_out = 64, stride 1, pad 1, 3 taps: every conv of ResNet layer1, forward AND
 // data-grad) is a thin GEMM - N = 64, K = 192 - over M = B*L = 128,000 rows at B=1024: 3.1 GFLOP against 33 MB of
@@ -1262,6 +1408,48 @@ int launch_fwd_tap(const FwdArgs& a, hipStream_t stream) {
   }
   if (a.Cout % 128 == 0) return b ? launch_fwd_tap_t<128, 1>(a, stream) : launch_fwd_tap_t<128, 0>(a, stream);
   return b ? launch_fwd_tap_t<64, 1>(a, stream) : launch_fwd_tap_t<64, 0>(a, stream);
+}
+
+// ECG_CONV_TAP_S2=1|0: the tap-shared strided data-grad kernel (1, default) for the data-grads of stride-2 pad-1
+// 3-tap convs, or the phase-decomposed one-tap kernels (0).  Read once.
+int g_conv_tap_s2 = -1;
+inline bool conv_tap_s2() {
+  if (g_conv_tap_s2 < 0) {
+    const char* e = getenv("ECG_CONV_TAP_S2");
+    g_conv_tap_s2 = e ? atoi(e) : 1;
+  }
+  return g_conv_tap_s2 != 0;
+}
+// The call shape of such a data-grad: dz [B][Lin][Cin] read with input dilation 2, 3 flipped taps, pad 1, output
+// length 2*Lin - 1 or 2*Lin (the forward's input length), 32-bit addressable operands.
+inline bool tap_s2_ok(int B, int Lin, int Cin, int Lout, int Cout, int Kw, int stride, int pad, int in_dil) {
+  return conv_tap_s2() && Kw == 3 && stride == 1 && pad == 1 && in_dil == 2 && (Lout + 1) / 2 == Lin && Lin >= 2 &&
+         Cin % 64 == 0 && Cout % 64 == 0 && (long)B * Lin * Cin * 2 < 0x7fff0000L &&
+         (long)Cout * 3 * Cin * 2 < 0x7fff0000L && (long)B * Lout * Cout < 0x7fffffffL;
+}
+inline int tap_s2_mtiles(int B, int Lin) { return (int)(((long)B * Lin + S2_IR - 1) / S2_IR); }
+
+template <int BN, int EPI>
+int launch_dgrad_s2_t(const FwdArgs& a, hipStream_t stream) {
+  constexpr int SMEM = TapS2Cfg<BN>::SMEM;
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    ECG_HIP_CHECK(hipFuncSetAttribute((const void*)conv1d_nlc_dgrad_s2_tap_kernel<BN, EPI>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, SMEM));
+    attr = true;
+  }
+  const int MT = tap_s2_mtiles(a.B, a.Lin), NT = a.Cout / BN;
+  hipLaunchKernelGGL((conv1d_nlc_dgrad_s2_tap_kernel<BN, EPI>), dim3((unsigned)(MT * NT)), dim3(512), SMEM, stream, a,
+                     MT, NT);
+  ECG_HIP_CHECK(hipGetLastError());
+  return ecg::kOk;
+}
+
+int launch_dgrad_s2(const FwdArgs& a, hipStream_t stream) {
+  const bool b = a.stat_mode == 1;
+  if (a.Cout % 128 == 0) return b ? launch_dgrad_s2_t<128, 1>(a, stream) : launch_dgrad_s2_t<128, 0>(a, stream);
+  return b ? launch_dgrad_s2_t<64, 1>(a, stream) : launch_dgrad_s2_t<64, 0>(a, stream);
 }
 
 // ECG_CONV_TAP=0|1|2: the tap-shared 256-row kernel for eligible convs with C_out % 128 == 0 (1, default), also
@@ -2249,6 +2437,7 @@ ECG_API int ecg_conv1d_nlc_fwd_pa(const void* x, const void* w, const float* bia
   }
   if (tap64_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return launch_tap64(a, stream);
   if (conv_tap(Cout) && tap_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return launch_fwd_tap(a, stream);
+  if (tap_s2_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return launch_dgrad_s2(a, stream);
   int bm, bn;
   pick_fwd_tile((long)B * Lout, Cout, in_dil, &bm, &bn);
   if (bm == 256 && bn == 256) return launch_fwd<256, 256>(a, stream);
@@ -2263,6 +2452,14 @@ ECG_API int ecg_conv1d_nlc_fwd_pa(const void* x, const void* w, const float* bia
 ECG_API int ecg_conv1d_nlc_set_tap64(int on) {
   const int prev = conv_tap64() ? 1 : 0;
   g_conv_tap64 = on ? 1 : 0;
+  return prev;
+}
+
+// Tap-shared strided data-grad kernel on (1) / off (0); returns the previous setting (tests, A/B).  Step plans size
+// their BatchNorm partial rows when built: set it first.
+ECG_API int ecg_conv1d_nlc_set_tap_s2(int on) {
+  const int prev = conv_tap_s2() ? 1 : 0;
+  g_conv_tap_s2 = on ? 1 : 0;
   return prev;
 }
 
@@ -2311,6 +2508,7 @@ ECG_API int ecg_conv1d_nlc_fwd_stat_rows(int B, int Lin, int Cin, int Lout, int 
                                          int in_dil) {
   if (tap64_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return tap64_groups(B, Lout);
   if (conv_tap(Cout) && tap_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return tap_mtiles(B, Lout);
+  if (tap_s2_ok(B, Lin, Cin, Lout, Cout, Kw, stride, pad, in_dil)) return tap_s2_mtiles(B, Lin);
   return ecg_conv1d_nlc_fwd_stat_tiles_ex(B, Lout, Cout, in_dil);
 }
 

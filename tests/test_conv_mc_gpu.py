@@ -61,11 +61,12 @@ STRIDED = [c for c in CASES if c[5] > 1]
 def test_strided_dgrad_dma_equals_register_loop(B, L, Cin, Cout, K, s, p):
     """The phase-decomposed strided data-grad on the LDS-DMA loop (default) and on the register-staged loop compute
     the same MFMA sums in the same order: bitwise-equal input gradients (and both match fp32, test above)."""
-    from crossscale_ecg.ops.conv_mc import conv1d_nlc, set_dma_dilated
+    from crossscale_ecg.ops.conv_mc import conv1d_nlc, set_dma_dilated, set_tap_s2
     torch.manual_seed(1)
     x0 = torch.randn(B, L, Cin, device=DEV).bfloat16()
     w = torch.randn(Cout, Cin, K, device=DEV) / (Cin * K) ** 0.5
     grads = []
+    prev_s2 = set_tap_s2(False)  # the phase-decomposed one-tap kernels (the tap-shared form: test below)
     for on in (True, False):
         prev = set_dma_dilated(on)
         try:
@@ -77,7 +78,43 @@ def test_strided_dgrad_dma_equals_register_loop(B, L, Cin, Cout, K, s, p):
             grads.append(x.grad.clone())
         finally:
             set_dma_dilated(prev)
+    set_tap_s2(prev_s2)
     assert torch.equal(grads[0], grads[1])
+
+
+S2_CASES = [c for c in STRIDED if c[4] == 3 and c[5] == 2 and c[6] == 1] + [
+    (1024, 125, 64, 128, 3, 2, 1),  # ResNet layer-2 first conv at B=1024 (dgrad: 64 output channels, odd L)
+    (1024, 32, 256, 512, 3, 2, 1),  # layer-4 first conv (dgrad: 256 output channels, 4 chunks)
+]
+
+
+@pytest.mark.parametrize("B,L,Cin,Cout,K,s,p", S2_CASES)
+def test_strided_dgrad_tap_shared(B, L, Cin, Cout, K, s, p):
+    """The tap-shared strided data-grad (one staged dz image per 128 i-rows read by both output phases: tap 1 for
+    even outputs, taps 0 / 2 for odd ones) against an fp64 transposed conv of the same bf16 operands, its BatchNorm
+    partial rows are one per 128 i-rows, and it agrees with the phase-decomposed one-tap kernels to bf16 rounding."""
+    from crossscale_ecg.ops import conv_mc
+    torch.manual_seed(3)
+    Lo = conv_mc.out_len(L, K, s, p)
+    dy = torch.randn(B, Lo, Cout, device=DEV).bfloat16()
+    wd = (torch.randn(Cin, K, Cout, device=DEV) / (Cout * K) ** 0.5).bfloat16()  # flipped [Cin][K][Cout] layout
+    assert conv_mc.stat_rows(B, Lo, Cout, L, Cin, K, 1, K - 1 - p, s) == (B * Lo + 127) // 128
+    dx = conv_mc.fwd_raw(dy, wd, None, 1, K - 1 - p, L, in_dil=s)
+    prev = conv_mc.set_tap_s2(False)
+    try:
+        dx1 = conv_mc.fwd_raw(dy, wd, None, 1, K - 1 - p, L, in_dil=s)
+    finally:
+        conv_mc.set_tap_s2(prev)
+    torch.cuda.synchronize()
+    # reference: dx = conv_transpose(dy, W) with W [Cout][Cin][K] = the un-flipped forward weight
+    w_fwd = wd.double().flip(1).permute(2, 0, 1)  # [Cout][Cin][K]
+    ref = F.conv_transpose1d(dy.double().transpose(1, 2), w_fwd, None, stride=s, padding=p,
+                             output_padding=L - ((Lo - 1) * s - 2 * p + K))
+    got = dx.double().transpose(1, 2)
+    assert got.shape == ref.shape
+    assert (got - ref).abs().max().item() <= 8e-3 * ref.abs().max().item()
+    assert _rel(got, ref) < 4e-3
+    assert _rel(dx.double(), dx1.double()) < 4e-3
 
 
 BIG_CASES = [  # shapes that select the 256-row DMA tiles once the big-tile family is enabled
