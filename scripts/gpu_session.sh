@@ -85,6 +85,14 @@ for s in "$@"; do
       step fedavg 600 python part3_fedavg_overlap_mpi_gpu.py --data-root data/shards --rounds 5 --local-steps 50 \
         --config both --results-csv "$OUT/modules/fedavg_results_w1.csv"
       step plots 300 python plot_results.py --results-dir "$OUT/modules" ;;
+    dist2)  # two ranks sharing the one GPU over gloo (RCCL needs one GPU per rank): the N>1 bench path on real
+            # kernels - self-launch, per-rank placement, timing bracket, cross-rank weight self-check
+      for ov in none tail; do
+        step dist2_tiny_$ov 300 env ECG_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 100 --warmup 10 \
+          --overlap $ov --no-extras
+      done
+      step dist2_resnet 300 env ECG_DIST_BACKEND=gloo python bench.py --gpus 2 --model resnet1d18 --steps 10 \
+        --warmup 3 --batch-size 256 --no-extras ;;
     libab)  # LIBS="a b c": interleaved ResNet runs against _ablib/<a>, _ablib/<b>, ...
       for r in 1 2 3; do for v in ${LIBS}; do
         ECG_LIB_DIR=$PWD/_ablib/$v step resnet_lib${v}_$r 300 python bench.py --model resnet1d34 --steps 20 --warmup 5 --no-extras
