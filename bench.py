@@ -128,127 +128,52 @@ def round_plan(steps: int, local_steps: int):
     return [local_steps] * full + ([rem] if rem else [])
 
 
-class CommTimer:
-    """Times the timed region's FedAvg collectives (reference: comm timed apart from local work,
-    Module_3/TRUE_FL_M3/part3_fedavg_overlap_mpi_gpu.py:188-214).
-
-    GPU: hipEvents.  ``issue`` is recorded on the compute stream right before the collective is enqueued (RCCL's
-    stream is ordered after it); completion is recorded on a side stream that waits for RCCL (``done``); the
-    compute stream's own wait for ``done`` is bracketed by two compute-stream events.  So per collective
-    ``comm_ms`` = issue -> done (the collective's span) and ``exposed_ms`` = the compute stream's stall on it.
-    CPU (gloo): host clocks around the same points.  Resolved once, after the timed region."""
-
-    def __init__(self, gpu: bool, device=None):
-        self.gpu = gpu
-        self.recs = []  # (issue, done, wait_before, wait_after)
-        self.side = None
-        if gpu:
-            import torch
-            self.side = torch.cuda.Stream(device=device)
-
-    def _mark(self, stream=None):
-        if self.gpu:
-            import torch
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record(stream) if stream is not None else ev.record()
-            return ev
-        return time.perf_counter()
-
-    def collective(self, fn, async_op: bool):
-        """Run ``fn(async_op)`` (the all-reduce call); returns a handle whose ``wait()`` makes the compute stream
-        (GPU) / the host (CPU) wait and records the stall."""
-        issue = self._mark()
-        work = fn(async_op)
-        rec = [issue, None, None, None]
-        self.recs.append(rec)
-        timer = self
-
-        class _Handle:
-            def wait(self_inner):
-                if rec[3] is not None:
-                    return
-                rec[2] = timer._mark()
-                if timer.gpu:
-                    import torch
-                    torch.cuda.current_stream().wait_event(rec[1])
-                elif work is not None:
-                    work.wait()
-                    rec[1] = timer._mark()
-                rec[3] = timer._mark()
-
-        if not async_op:  # blocking: the compute stream (GPU) / the host (CPU) stalls for the whole collective
-            rec[1] = rec[3] = self._mark()
-            rec[2] = issue
-        elif self.gpu and work is not None:
-            import torch
-            with torch.cuda.stream(self.side):
-                work.wait()  # the side stream waits for RCCL (whose stream is ordered after ``issue``)
-                rec[1] = self._mark(self.side)
-        return _Handle()
-
-    def summary(self):
-        """(comm_ms, exposed_ms) summed over the collectives (call after a device synchronize)."""
-        comm = exp = 0.0
-        for issue, done, w0, w1 in self.recs:
-            if done is None:
-                continue
-            if self.gpu:
-                comm += issue.elapsed_time(done)
-                exp += w0.elapsed_time(w1) if w1 is not None else 0.0
-            else:
-                comm += (done - issue) * 1e3
-                exp += (w1 - w0) * 1e3 if w1 is not None else 0.0
-        return comm, exp
-
-
 class FedAvgRunner:
     """Runs a round plan on a trainer: each round = local steps then the FedAvg all-reduce (AVG).
 
-    Per round, in enqueue order: launch the round's steps -> issue the all-reduce -> stage the NEXT round's
-    batches (weight-independent) -> [next round] wait for the all-reduce -> launch.  With ``tail`` the
-    collective is issued async, so RCCL's stream waits only for the round's steps and the staging kernels run
-    on the compute stream beside it; with ``none`` the host blocks on the collective before staging.
-    ``timer`` (a CommTimer, optional) measures each collective's span and the compute stream's stall on it."""
+    The collectives go through ``parallel.overlap.FedAvgComm`` / ``FedAvgRound`` - the framework's one comm-timing
+    path (the device's comm stream, RCCL ordered after it, hipEvents on both streams) - so the bench's ``comm_ms``
+    (each collective's own span) and ``comm_exposed_ms`` (the compute stream's stall on it) mean exactly what the
+    FedAvg driver's CSV columns mean.  Per round, in enqueue order: launch the round's steps -> issue the
+    all-reduce -> stage the NEXT round's batches (weight-independent) -> [next round] wait for the all-reduce ->
+    launch.  ``none`` waits right after issuing (before the staging); ``tail`` waits only after the staging was
+    enqueued, so the collective runs beside it.  ``collectives=False`` runs the same plan without any
+    communication (the compute-only reference of the wall-clock exposure)."""
 
-    def __init__(self, trainer, flat, ctx, overlap: str, allreduce=None, timer=None):
-        if allreduce is None:
-            from crossscale_ecg.parallel.fedavg import allreduce_mean_ as allreduce
+    def __init__(self, trainer, flat, ctx, overlap: str, allreduce=None, comm=None):
+        from crossscale_ecg.parallel.overlap import FedAvgComm, FedAvgRound
         self.trainer, self.flat, self.ctx = trainer, flat, ctx
-        self.allreduce = allreduce
         self.overlap = overlap if ctx.distributed else "none"
+        self.comm = comm or FedAvgComm(ctx, allreduce=allreduce)
+        self.fround = FedAvgRound(flat, self.comm, self.overlap)
         self.syncs = 0
-        self.timer = timer
-        self._pending = None
-
-    def _collective(self, async_op: bool):
-        if self.timer is not None and self.ctx.distributed:
-            return self.timer.collective(lambda a: self.allreduce(self.flat, self.ctx, async_op=a), async_op)
-        if async_op:
-            return self.allreduce(self.flat, self.ctx, async_op=True)
-        return self.allreduce(self.flat, self.ctx)
+        self.collectives = True
+        self.recs = []
 
     def run(self, plan, then=None):
         """``then``: size of the round that will follow ``plan`` (its batches are staged behind the last round)."""
+        from crossscale_ecg.parallel.overlap import CommRecord
         for i, n in enumerate(plan):
             next_n = plan[i + 1] if i + 1 < len(plan) else then
             self.trainer.prepare_round(n, reset_loss=False)  # no-op when the previous round staged it
-            if self._pending is not None:  # tail: the next batches were staged while the all-reduce ran
-                self._pending.wait()
-                self._pending = None
+            self.fround.begin_round()  # tail: the next batches were staged while the all-reduce ran
             self.trainer.launch_round(n)
-            if self.overlap == "tail":
-                self._pending = self._collective(True)
-            else:
-                self._collective(False)
-            self.syncs += 1
+            if self.collectives:
+                if self.ctx.distributed:
+                    rec = CommRecord()
+                    self.fround.end_round(rec)
+                    self.recs.append(rec)
+                self.syncs += 1
             if next_n is not None and hasattr(self.trainer, "stage"):
                 self.trainer.stage(next_n)
         self.drain()
 
     def drain(self):
-        if self._pending is not None:
-            self._pending.wait()
-            self._pending = None
+        self.fround.finalize()
+
+    def comm_summary(self):
+        """(comm_ms, exposed_ms) summed over the recorded rounds (call after a device synchronize)."""
+        return (sum(r.comm_ms() for r in self.recs), sum(r.exposed_ms() for r in self.recs))
 
 
 def weights_digest(flat):
@@ -346,7 +271,7 @@ def main(argv=None):
     import crossscale_ecg  # noqa: F401
     from crossscale_ecg.models.tiny_ecg import TinyECG, num_params
     from crossscale_ecg.parallel.env import (init_distributed, barrier, shutdown_distributed, rccl_init_log,
-                                             rccl_transports, peer_access)
+                                             rccl_transports, peer_access, rccl_log_env_restore, rccl_log_remove)
 
     # RCCL runs: its INIT log (channel -> transport) goes to a per-rank file read back after the run
     rccl_log = None
@@ -354,6 +279,8 @@ def main(argv=None):
             int(os.environ.get("WORLD_SIZE", "1")) > 1:
         rccl_log = rccl_init_log()
     ctx = init_distributed(prefer_gpu=a.device == "gpu")
+    if rccl_log is not None:  # the communicator exists (eager device_id init): children must not inherit the log
+        rccl_log_env_restore()
     if ctx.world_size != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={ctx.world_size}")
     dev = ctx.device
@@ -430,38 +357,51 @@ def main(argv=None):
     ev0 = ev1 = None
     if on_gpu:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # the timed collectives' span and the compute stream's stall on them (events; resolved after the region)
-    runner.timer = CommTimer(on_gpu, dev) if ctx.distributed else None
-    # no cyclic-GC pass inside the timed region (a collection there is host jitter, not work: one K=20 run measured
-    # 15.7 us/step wall at 11.4 us/step of GPU time); the full pass ran before the warm-up, the collector resumes
-    # right after the region
-    gc.disable()
-    try:
-        bracket()
-        if ev0 is not None:  # recorded on the idle stream just before the clock starts (its host cost stays outside)
-            ev0.record()
-        t0 = time.perf_counter()
-        runner.run(timed_plan)
-        if ev1 is not None:
-            ev1.record()
-        bracket()
-        elapsed = time.perf_counter() - t0
-    finally:
-        gc.enable()
+
+    def timed(plan, then=None):
+        """Wall seconds of ``plan`` between two brackets; no cyclic-GC pass inside (a collection there is host
+        jitter, not work: one K=20 run measured 15.7 us/step wall at 11.4 us/step of GPU time; the full pass ran
+        before the warm-up, the collector resumes right after the region)."""
+        gc.disable()
+        try:
+            bracket()
+            if ev0 is not None:  # recorded on the idle stream just before the clock starts (its host cost stays outside)
+                ev0.record()
+            t0 = time.perf_counter()
+            runner.run(plan, then=then)
+            if ev1 is not None:
+                ev1.record()
+            bracket()
+            return time.perf_counter() - t0
+        finally:
+            gc.enable()
+
+    # N>1: the same K steps once WITHOUT collectives first (untimed for the headline), so the wall-clock exposure of
+    # the communication is measured on every backend as elapsed(with comm) - elapsed(compute only); the final
+    # FedAvg of the timed region leaves every rank on identical weights again (checked below)
+    solo_s = float("nan")
+    if ctx.distributed:
+        runner.collectives = False
+        solo_s = timed(timed_plan, then=timed_plan[0])
+        runner.collectives = True
+    runner.recs.clear()
+    runner.syncs = 0
+    elapsed = timed(timed_plan)
     gpu_s = ev0.elapsed_time(ev1) / 1e3 if ev0 is not None else float("nan")
-    comm_ms, exposed_ms = runner.timer.summary() if runner.timer is not None else (0.0, 0.0)
+    comm_ms, exposed_ms = runner.comm_summary()
+    exposed_wall_ms = max(0.0, (elapsed - solo_s) * 1e3) if solo_s == solo_s else 0.0
     digest = weights_digest(flat)  # after the last FedAvg all-reduce every rank must hold these exact weights
     tbar_kind = tbar.kind
     tbar.close()
     world_seen, dist_backend = 1, "none"
-    per_rank = [[elapsed, gpu_s, comm_ms, exposed_ms]]
+    per_rank = [[elapsed, gpu_s, comm_ms, exposed_ms, exposed_wall_ms]]
     placements = [placement]
     digests = [digest]
     links = None
     if ctx.distributed:
         import torch.distributed as dist
         world_seen, dist_backend = dist.get_world_size(), dist.get_backend()
-        mine = torch.tensor([elapsed, gpu_s, comm_ms, exposed_ms], dtype=torch.float64,
+        mine = torch.tensor([elapsed, gpu_s, comm_ms, exposed_ms, exposed_wall_ms], dtype=torch.float64,
                             device=dev if dist_backend == "nccl" else "cpu")
         allv = [torch.zeros_like(mine) for _ in range(world_seen)]
         dist.all_gather(allv, mine)
@@ -474,6 +414,7 @@ def main(argv=None):
         digests = [[float(v) for v in t.tolist()] for t in digs]
         links = [None] * world_seen
         dist.all_gather_object(links, {"transports": rccl_transports(rccl_log), "peer_access": peer_access(dev)})
+        rccl_log_remove(rccl_log)
         elapsed = max(r[0] for r in per_rank)
         gpu_s = max(r[1] for r in per_rank)
     total = a.gpus * B * a.steps
@@ -532,12 +473,17 @@ def main(argv=None):
             "timing_barrier": tbar_kind,
             "timed_round_plan": timed_plan if len(timed_plan) <= 4 else f"{len(timed_plan)} rounds",
             "final_avg_loss": round(loss, 6) if loss == loss else None,
-            # per-rank diagnosis of the MAX: wall and GPU-event ms/step, the timed collectives' span (comm_ms) and
-            # the compute stream's stall on them (comm_exposed_ms), summed over the timed rounds, per rank
+            # per-rank diagnosis of the MAX: wall and GPU-event ms/step; the timed collectives' own span (comm_ms)
+            # and the compute side's measured stall on them (comm_exposed_ms: compute-stream events on RCCL, host
+            # time blocked in wait on host-staged gloo; parallel/overlap.py), summed over the timed rounds; and the
+            # wall-clock exposure (comm_exposed_wall_ms = elapsed - elapsed of the same K steps without
+            # collectives, any backend)
             "per_rank_ms_per_step": [round(r[0] * 1e3 / a.steps, 5) for r in per_rank],
             "per_rank_gpu_ms_per_step": [round(r[1] * 1e3 / a.steps, 5) if r[1] == r[1] else None for r in per_rank],
             "comm_ms": [round(r[2], 4) for r in per_rank],
             "comm_exposed_ms": [round(r[3], 4) for r in per_rank],
+            "comm_exposed_wall_ms": [round(r[4], 4) for r in per_rank],
+            "comm_timing": runner.comm.kind if ctx.distributed else "none",
             # rank -> NUMA node : CPU slice [split basis: kfd = planned over every GPU of the machine]
             "rank_cpus": [f"node{p.get('numa_node', -1)}:{p.get('cpus', '')}" + ("" if p.get("bound") else " (unbound)")
                           + (f" [{p['basis']}]" if p.get("basis") else "") for p in placements],

@@ -106,12 +106,33 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, pr
         kw = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = device
+            opts = nccl_pg_options()
+            if opts is not None:
+                kw["pg_options"] = opts
         dist.init_process_group(**kw)
         ctx.initialized_here = True
     elif world > 1 and dist.is_initialized():
         ctx.backend = dist.get_backend()
     _CTX = ctx
     return ctx
+
+
+def nccl_pg_options():
+    """RCCL process-group options: RCCL's internal stream from torch's HIGH-priority pool (``ECG_RCCL_HIGH_PRIORITY``,
+    default 1).  Measured on MI355X (profiles/r6/stream_queues.txt): with the default normal-priority pool stream,
+    RCCL's kernels landed on the SAME hardware queue as the compute (null) stream - HIP maps streams onto at most
+    GPU_MAX_HW_QUEUES=4 queues per priority - so a collective ran only after every compute kernel enqueued before it
+    (a 40 us all-reduce issued under a 1.7 ms compute kernel finished at 1.72 ms) and the comm stream behind it
+    stalled too.  The high-priority pool maps onto separate queues (the comm stream's class), so the collective runs
+    beside the compute kernels."""
+    if os.environ.get("ECG_RCCL_HIGH_PRIORITY", "1") == "0":
+        return None
+    try:
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        return opts
+    except (AttributeError, RuntimeError):  # a build without the NCCL process group
+        return None
 
 
 def get_context() -> DistContext:
@@ -144,10 +165,36 @@ def rccl_init_log(directory: Optional[str] = None) -> Optional[str]:
         return None
     directory = directory or os.environ.get("TMPDIR", "/tmp")
     path = os.path.join(directory, f"ecg_rccl_init.{os.getpid()}.log")
+    for k in _RCCL_LOG_VARS:
+        _RCCL_ENV_PREV[k] = os.environ.get(k)
     os.environ["NCCL_DEBUG"] = "INFO"
     os.environ["NCCL_DEBUG_SUBSYS"] = "INIT"
     os.environ["NCCL_DEBUG_FILE"] = path
     return path
+
+
+_RCCL_LOG_VARS = ("NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "NCCL_DEBUG_FILE")
+_RCCL_ENV_PREV: dict = {}
+
+
+def rccl_log_env_restore() -> None:
+    """Put the NCCL_DEBUG* variables back as they were before ``rccl_init_log`` (call once the communicator exists:
+    the eager ``device_id`` init creates it inside ``init_process_group``), so child processes do not inherit them."""
+    for k, v in _RCCL_ENV_PREV.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+    _RCCL_ENV_PREV.clear()
+
+
+def rccl_log_remove(path: Optional[str]) -> None:
+    """Delete the per-process INIT log once ``rccl_transports`` has read it."""
+    if path:
+        try:
+            os.remove(path)
+        except OSError:
+            pass
 
 
 def rccl_transports(path: Optional[str]) -> dict:

@@ -111,10 +111,27 @@ def allreduce_mean_(t: torch.Tensor, ctx: DistContext, async_op: bool = False):
 
 
 class _DivAfter:
+    """Async SUM + divide (gloo has no AVG).  The divide is chained onto the SUM's future, so it runs on the
+    backend's thread as soon as the sum lands - under whatever the caller enqueued after issuing - instead of
+    inside ``wait``; ``get_future()`` completes after the divide."""
+
     def __init__(self, work, t, n):
         self.work, self.t, self.n = work, t, n
+        self.fut = None
+        try:
+            self.fut = work.get_future().then(lambda _f: t.div_(n))
+        except Exception:  # a backend without futures: divide in wait()
+            self.fut = None
+
+    def get_future(self):
+        if self.fut is None:
+            raise RuntimeError("no future")
+        return self.fut
 
     def wait(self):
+        if self.fut is not None:
+            self.fut.wait()
+            return
         self.work.wait()
         self.t.div_(self.n)
 

@@ -8,7 +8,11 @@ its GPU, to a disjoint slice of the CPUs of that GPU's NUMA node:
 
     GPU PCI address (torch device properties) -> /sys/bus/pci/devices/<bdf>/numa_node
     -> /sys/devices/system/node/node<n>/cpulist  (intersected with the CPUs this process may use)
-    -> the GPUs on the same NUMA node split that list into contiguous, equal slices (in PCI-address order).
+    -> the node's PHYSICAL cores (logical CPUs grouped by ``cpu<n>/topology/thread_siblings_list``)
+    -> the GPUs on the same NUMA node split those cores into contiguous, equal slices (in PCI-address order);
+       each rank gets every allowed hyper-thread of its own cores, so no two ranks share a core (on the usual
+       EPYC numbering CPU n+128 is the SMT sibling of n: a split of the logical list ``0-63,128-191`` into four
+       would have put rank 2 on the siblings of rank 0's cores).
 
 The GPUs that share a node are taken from the KFD topology (``/sys/class/kfd/kfd/topology/nodes``: every GPU of
 the machine, whatever ``HIP_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES`` or ``srun --gpus-per-task=1`` let this
@@ -73,11 +77,27 @@ def node_cpus(node: int, sysfs: str = "/sys") -> List[int]:
     return parse_cpulist(v) if v else []
 
 
+def core_groups(cpus: Sequence[int], sysfs: str = "/sys") -> List[List[int]]:
+    """``cpus`` grouped by physical core (``thread_siblings_list``; a CPU without the file is its own core), each
+    group sorted, groups ordered by their lowest CPU.  Siblings outside ``cpus`` are dropped."""
+    want = set(cpus)
+    seen, groups = set(), []
+    for c in sorted(want):
+        if c in seen:
+            continue
+        sib = _read(os.path.join(sysfs, "devices", "system", "cpu", f"cpu{c}", "topology", "thread_siblings_list"))
+        g = sorted((set(parse_cpulist(sib)) & want) | {c}) if sib else [c]
+        seen.update(g)
+        groups.append(g)
+    return sorted(groups, key=lambda g: g[0])
+
+
 def plan_affinity(bdfs: Sequence[str], index: int, allowed: Iterable[int],
                   sysfs: str = "/sys") -> Tuple[int, List[int]]:
-    """CPUs for the rank driving GPU ``bdfs[index]``: its NUMA node's CPUs (within ``allowed``), split into equal
-    contiguous slices among the GPUs of ``bdfs`` on the same node, in list order.  Returns (node, cpus); cpus is
-    empty when nothing can be decided (unknown node, no allowed CPU on it)."""
+    """CPUs for the rank driving GPU ``bdfs[index]``: its NUMA node's CPUs (within ``allowed``) grouped into physical
+    cores, the cores split into equal contiguous slices among the GPUs of ``bdfs`` on the same node, in list order;
+    the rank gets both hyper-threads of each of its cores.  Returns (node, cpus); cpus is empty when nothing can be
+    decided (unknown node, no allowed CPU on it)."""
     allowed = set(allowed)
     nodes = [numa_node_of(b, sysfs) for b in bdfs]
     node = nodes[index]
@@ -88,9 +108,13 @@ def plan_affinity(bdfs: Sequence[str], index: int, allowed: Iterable[int],
         return node, []
     peers = [i for i, n in enumerate(nodes) if n == node]
     k, n_peers = peers.index(index), len(peers)
+    cores = core_groups(cpus, sysfs)
+    if len(cores) >= n_peers:  # whole cores per rank
+        per = len(cores) // n_peers
+        return node, sorted(c for g in cores[k * per:(k + 1) * per] for c in g)
     if len(cpus) < n_peers:  # fewer CPUs than ranks on this node: share the node's CPUs
         return node, cpus
-    per = len(cpus) // n_peers
+    per = len(cpus) // n_peers  # fewer cores than ranks: ranks must share cores, split the threads
     return node, cpus[k * per:(k + 1) * per]
 
 

@@ -1,34 +1,61 @@
-"""FedAvg communication with MEASURED overlap: a dedicated comm stream, hipEvents on both streams.
+"""FedAvg communication with MEASURED overlap: one comm stream per device, one timing definition per backend.
 
 Reference: the FedAvg round (TRUE_FL_M3/part3_fedavg_overlap_mpi_gpu.py:186-216) times its host-staged
 collectives with ``perf_counter`` around blocking calls (:188-190, :209-211), so ``comm_ms`` is always fully
-exposed.  Here every collective is issued from a high-priority comm stream that first waits on an event of
-the compute stream; RCCL's internal stream is ordered after the comm stream, and ``work.wait()`` issued under
-the comm stream makes the COMM stream (not the compute stream) wait for RCCL.  Four events per collective:
+exposed.  Here every collective is issued through ``FedAvgComm`` - the ONLY comm-timing path (bench.py, the
+FedAvg driver, the ResNet tail step and the tests all use it) - and two numbers are kept per collective:
 
-* ``issue``  (comm stream, after it waited for the weights to be final) and ``done`` (comm stream, after RCCL
-  finished): ``comm_ms = issue -> done`` is the collective's own duration;
-* ``before`` and ``after`` (compute stream) around the compute stream's wait on ``done``:
-  ``exposed_ms = before -> after`` is the time the compute stream actually stalled on communication.
+* ``comm_ms`` - the collective's OWN span: from the moment it could start (its input is final) to its
+  completion, on every backend;
+* ``comm_exposed_ms`` - the time the compute side actually stalled on it (whatever weight-independent work was
+  enqueued between issue and wait - the next round's batch staging for ``tail``, a whole local round for
+  ``delayed``, the remaining backward segments of the ResNet tail step - shows up as the difference).
 
-So ``comm_exposed_ms`` is measured, not copied from ``comm_ms``: whatever compute stream work was enqueued
-between issue and wait (next round's batch preparation for ``tail``, a whole local round for ``delayed``, the
-earlier backward segments of the ResNet tail step) shows up as the difference.
+How each backend realises those points (``FedAvgComm.kind``):
 
-On CPU (gloo) the same API uses host clocks: ``comm_ms`` = issue -> completion observed by ``wait`` and
-``exposed_ms`` = time blocked inside ``wait``.
+``stream`` (GPU tensors on RCCL): the collective is issued from the device's comm stream (``comm_stream``, high
+  priority) after that stream waited for the compute stream; RCCL's internal stream is ordered after it and
+  ``work.wait()`` under the comm stream makes the COMM stream (not the compute stream) wait for RCCL.  hipEvents:
+  ``issue``/``done`` on the comm stream (span), ``before``/``after`` around the compute stream's
+  ``wait_event(done)`` (stall).
+``host`` (CPU tensors, gloo): ``issue`` = host clock at the call (the input is final: CPU ops are synchronous),
+  ``done`` = the clock when the work's future completed (a done-callback run by the backend's thread - the
+  completion time, not the time the consumer looked; it can trail completion by up to one GIL switch interval when
+  the main thread is running Python), stall = host time blocked in ``wait``.
+``host_staged`` (GPU tensors over a host-staging backend, i.e. gloo rehearsing several ranks on one GPU): gloo
+  copies the tensor to the host after the compute stream's pending work, so ``issue`` first synchronises the
+  compute stream (that wait is compute, not communication), then as ``host``; the host blocks inside the issuing
+  call (the staging copy) and in ``wait`` while the GPU runs only what was enqueued before it, so the host stall
+  (both blocks, for every host kind) is the exposure.
+
+``comm_stream(device)`` is shared by every issuer on a device (FedAvgComm, the ResNet trainer's DDP buckets and
+tail SGD), so an N>1 rank runs on four streams: compute (torch's current stream), the engine's low-priority side
+lane, this comm stream, and RCCL's internal stream (profiles/r6/stream_queues.txt audits the queue mapping).
 """
 from __future__ import annotations
 
 import contextlib
 import time
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import Callable, Dict, List, Optional
 
 import torch
 
 from .env import DistContext
 from .fedavg import allreduce_mean_
+
+_COMM_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def comm_stream(device: torch.device) -> "torch.cuda.Stream":
+    """The device's communication stream (created once, high priority): every collective issuer on the device
+    uses it, so the stream count of a rank stays at compute + side lane + comm + RCCL's."""
+    idx = torch.device(device).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    s = _COMM_STREAMS.get(idx)
+    if s is None:
+        s = _COMM_STREAMS[idx] = torch.cuda.Stream(device=idx, priority=-1)
+    return s
 
 
 class Mark:
@@ -36,14 +63,14 @@ class Mark:
 
     __slots__ = ("ev", "t")
 
-    def __init__(self, stream: Optional[torch.cuda.Stream] = None, gpu: bool = False):
+    def __init__(self, stream: Optional[torch.cuda.Stream] = None, gpu: bool = False, t: Optional[float] = None):
         if gpu:
             self.ev = torch.cuda.Event(enable_timing=True)
             self.ev.record(stream or torch.cuda.current_stream())
             self.t = None
         else:
             self.ev = None
-            self.t = time.perf_counter()
+            self.t = time.perf_counter() if t is None else t
 
     def ms_to(self, other: "Mark") -> float:
         if self.ev is not None:
@@ -59,63 +86,101 @@ class Pending:
     issue: Optional[Mark] = None
     done: Optional[Mark] = None
     waited: bool = False
+    completed_at: Optional[list] = None  # host kinds: [perf_counter at the work's completion] (done-callback)
 
 
 @dataclass
 class CommRecord:
     """Timing of one round's communication (resolved after the events completed)."""
-    first_issue: Optional[Mark] = None
-    last_done: Optional[Mark] = None
-    stalls: List[tuple] = field(default_factory=list)  # (before, after) on the compute stream
+    spans: List[tuple] = field(default_factory=list)  # (issue, done) per collective
+    stalls: List[tuple] = field(default_factory=list)  # (before, after) on the compute stream / host
     blocking: List[tuple] = field(default_factory=list)  # synchronous collectives (broadcast): comm == exposed
 
+    @property
+    def first_issue(self) -> Optional[Mark]:
+        return self.spans[0][0] if self.spans else None
+
     def comm_ms(self) -> float:
+        """Blocking collectives plus the union span of the issued ones (first issue -> last completion)."""
         ms = sum(a.ms_to(b) for a, b in self.blocking)
-        if self.first_issue is not None and self.last_done is not None:
-            ms += self.first_issue.ms_to(self.last_done)
+        done = [d for _, d in self.spans if d is not None]
+        if self.spans and done:
+            first = self.spans[0][0]
+            ms += max(first.ms_to(d) for d in done)
         return ms
 
     def exposed_ms(self) -> float:
         return sum(a.ms_to(b) for a, b in self.blocking) + sum(a.ms_to(b) for a, b in self.stalls)
 
 
-class FedAvgComm:
-    """Flat-buffer FedAvg collectives on a dedicated comm stream with per-collective timing marks."""
+def _completion_box(work) -> Optional[list]:
+    """A list that receives ``perf_counter()`` when ``work`` completes (its future's done-callback), or None."""
+    get = getattr(work, "get_future", None)  # fedavg._DivAfter: completes after its chained divide
+    if get is None:
+        return None
+    try:
+        fut = get()
+    except Exception:  # backend without futures
+        return None
+    box: list = []
+    fut.add_done_callback(lambda _f: box.append(time.perf_counter()))
+    return box
 
-    def __init__(self, ctx: DistContext):
+
+class FedAvgComm:
+    """Flat-buffer FedAvg collectives with per-collective timing marks (module docstring: the three kinds).
+
+    ``allreduce(t, ctx, async_op=True)`` is the collective (default: ``fedavg.allreduce_mean_``, RCCL AVG /
+    gloo SUM + divide); tests inject recorders."""
+
+    def __init__(self, ctx: DistContext, allreduce: Optional[Callable] = None):
         self.ctx = ctx
-        self.gpu = ctx.device.type == "cuda"
+        self.allreduce = allreduce or allreduce_mean_
+        dev = getattr(ctx, "device", None)
+        self.gpu = dev is not None and dev.type == "cuda"
         self.stream = None
-        if self.gpu and ctx.distributed:
-            self.stream = torch.cuda.Stream(device=ctx.device, priority=-1)
+        if self.gpu and getattr(ctx, "backend", "none") == "nccl":
+            self.kind = "stream"
+        elif self.gpu:
+            self.kind = "host_staged"
+        else:
+            self.kind = "host"
+        if self.kind == "stream" and ctx.distributed:
+            self.stream = comm_stream(dev)
 
     def mark(self, stream=None) -> Mark:
+        """A point on ``stream`` (GPU: hipEvent, for callers timing their own device work) / the host clock."""
         return Mark(stream, self.gpu)
+
+    def _point(self, stream=None) -> Mark:
+        """A timing point of this backend's kind (device event for ``stream``, host clock otherwise)."""
+        return Mark(stream, self.kind == "stream")
 
     def issue(self, t: torch.Tensor, rec: CommRecord) -> Pending:
         """Start an all-reduce(AVG) of ``t`` once the compute stream's pending writes to it are done."""
         if not self.ctx.distributed:
-            m = self.mark()
-            if rec.first_issue is None:
-                rec.first_issue = m
-            rec.last_done = m
+            m = self._point()
             return Pending(None, m, m, True)
-        if self.gpu:
+        if self.kind == "stream":
             compute = torch.cuda.current_stream(self.ctx.device)
             self.stream.wait_stream(compute)
             with torch.cuda.stream(self.stream):
-                issue = self.mark(self.stream)
-                work = allreduce_mean_(t, self.ctx, async_op=True)
+                issue = self._point(self.stream)
+                work = self.allreduce(t, self.ctx, async_op=True)
                 if work is not None:
-                    work.wait()  # comm stream waits for RCCL (and runs gloo's divide, if any)
-                done = self.mark(self.stream)
+                    work.wait()  # comm stream waits for RCCL
+                done = self._point(self.stream)
             t.record_stream(self.stream)
             p = Pending(None, issue, done)
         else:
-            issue = self.mark()
-            p = Pending(allreduce_mean_(t, self.ctx, async_op=True), issue)
-        if rec.first_issue is None:
-            rec.first_issue = p.issue
+            if self.kind == "host_staged":
+                torch.cuda.current_stream(self.ctx.device).synchronize()  # t final: compute, not communication
+            issue = self._point()
+            work = self.allreduce(t, self.ctx, async_op=True)
+            # the call itself can block the host (gloo copies CUDA tensors to the host inside it): exposed time too
+            rec.stalls.append((issue, self._point()))
+            p = Pending(work, issue, None, completed_at=_completion_box(work))
+        rec.spans.append((p.issue, p.done))
         return p
 
     def wait(self, pendings: List[Pending], rec: CommRecord) -> None:
@@ -123,29 +188,37 @@ class FedAvgComm:
         todo = [p for p in pendings if not p.waited]
         if not todo:
             return
-        before = self.mark()
-        if self.gpu:
+        before = self._point()
+        if self.kind == "stream":
             compute = torch.cuda.current_stream(self.ctx.device)
             for p in todo:
                 compute.wait_event(p.done.ev)
                 p.waited = True
-            after = self.mark()
+            after = self._point()
         else:
             for p in todo:
                 if p.work is not None:
-                    p.work.wait()
+                    p.work.wait()  # host_staged: also orders the compute stream after gloo's copy back
                 p.waited = True
-            after = self.mark()
+            after = self._point()
             for p in todo:
-                p.done = after
+                box = p.completed_at
+                if box is not None and not box:  # the callback needs the GIL: give the backend thread a chance
+                    for _ in range(200):
+                        time.sleep(0)
+                        if box:
+                            break
+                p.done = Mark(t=min(box[0], after.t)) if box else after
+                for i, (iss, d) in enumerate(rec.spans):
+                    if iss is p.issue and d is None:
+                        rec.spans[i] = (iss, p.done)
         rec.stalls.append((before, after))
-        rec.last_done = todo[-1].done
 
     def blocking(self, fn, rec: CommRecord) -> None:
         """A synchronous collective (``fn()``) timed as fully exposed communication."""
-        a = self.mark()
+        a = self._point()
         fn()
-        rec.blocking.append((a, self.mark()))
+        rec.blocking.append((a, self._point()))
 
 
 class FedAvgRound:

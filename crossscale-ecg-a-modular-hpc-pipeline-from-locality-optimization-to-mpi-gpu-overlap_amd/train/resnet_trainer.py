@@ -26,6 +26,7 @@ from ..data.dataset import DeviceIndexSampler
 from ..ops.resnet_engine import ResNetStepEngine
 from ..parallel.env import DistContext
 from ..parallel.fedavg import allreduce_mean_
+from ..parallel.overlap import comm_stream
 
 
 class ResNetEngineTrainer:
@@ -46,7 +47,8 @@ class ResNetEngineTrainer:
                                        weight_decay=weight_decay, use_graph=use_graph,
                                        source=(self.x, self.y32, self.table), bucket_mb=bucket_mb)
         self.ddp = ddp
-        self._comm = torch.cuda.Stream(device=self.device, priority=-1) if ctx is not None and ctx.distributed \
+        # the device's one comm stream (shared with parallel.overlap.FedAvgComm: compute + side lane + comm + RCCL's)
+        self._comm = comm_stream(self.device) if ctx is not None and ctx.distributed and self.device.type == "cuda" \
             else None
         self.issue_log: List = []  # (segment, lo, hi) in issue order (tests / timeline)
         self.mom = self.engine.mom

@@ -15,7 +15,7 @@ import os
 import re
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DEFAULT_OUT = os.path.join(ROOT, "profiles", "r5", "bench_runs.jsonl")
+DEFAULT_OUT = os.path.join(ROOT, "profiles", "r6", "bench_runs.jsonl")
 KEEP = ("value", "ms_per_step", "gpu_ms_per_step", "steps", "warmup", "n_gpus")
 
 

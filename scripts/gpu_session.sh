@@ -8,7 +8,7 @@ set -u
 cd "$(dirname "$0")/.."
 TAG=${1:-base}
 shift
-OUT=gpurun_out/${ECG_ROUND:-r5}_$TAG
+OUT=gpurun_out/${ECG_ROUND:-r6}_$TAG
 mkdir -p "$OUT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {  # step <name> <timeout_s> <cmd...>
@@ -160,6 +160,14 @@ for s in "$@"; do
         python3 scripts/resnet_timeline.py run
       step prof_resnet 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_resnet" -o resnet -- \
         python3 bench.py --model resnet1d34 --steps 10 --warmup 3 --no-extras ;;
+    queues)  # stream -> hardware-queue audit of the N>1 layout (compute, side lane, comm, RCCL) under a kernel trace
+      export TMPDIR=/tmp
+      step queues 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/queues" -o q -- \
+        python3 scripts/probe_stream_queues.py run
+      step queues_parse 120 python scripts/probe_stream_queues.py parse "$OUT/queues"
+      ECG_RCCL_HIGH_PRIORITY=0 step queues_np 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/queues_np" \
+        -o q -- python3 scripts/probe_stream_queues.py run
+      step queues_np_parse 120 python scripts/probe_stream_queues.py parse "$OUT/queues_np" ;;
     tinypmc)
       export TMPDIR=/tmp
       step pmc_tiny 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAVE_CYCLES \

@@ -49,6 +49,10 @@ def test_bench_world2_reports_per_rank_comm_and_placement():
     assert len(rec["per_rank_gpu_ms_per_step"]) == 2
     assert len(rec["comm_ms"]) == 2 and all(c > 0 for c in rec["comm_ms"])  # two timed all-reduces per rank
     assert len(rec["comm_exposed_ms"]) == 2 and all(0 <= e for e in rec["comm_exposed_ms"])
+    # one comm-timing path (parallel/overlap.FedAvgComm): CPU tensors -> host clocks + work-completion callbacks;
+    # the wall-clock exposure (elapsed - the same steps without collectives) is reported next to the stall
+    assert rec["comm_timing"] == "host"
+    assert len(rec["comm_exposed_wall_ms"]) == 2 and all(0 <= e for e in rec["comm_exposed_wall_ms"])
     assert len(rec["rank_cpus"]) == 2 and all(s.startswith("node") for s in rec["rank_cpus"])
     assert rec["gc_paused_in_timed_region"] is True and rec["first_round_staged_in_warmup"] is True
 

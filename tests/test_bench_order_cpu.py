@@ -69,10 +69,19 @@ def test_tail_issue_before_stage_before_wait():
     ]
 
 
-def test_none_blocks_then_stages():
+def test_none_waits_then_stages():
     log, r = _run("none", [3, 3])
-    assert log == [("prepare", 3), ("launch", 3), ("issue", 0, False), ("stage", 3),
-                   ("launch", 3), ("issue", 1, False)]
+    assert log == [("prepare", 3), ("launch", 3), ("issue", 0, True), ("wait", 0), ("stage", 3),
+                   ("launch", 3), ("issue", 1, True), ("wait", 1)]
+
+
+def test_compute_only_pass_issues_nothing():
+    rec = _Recorder()
+    r = bench.FedAvgRunner(rec, None, SimpleNamespace(distributed=True), "tail", allreduce=rec.allreduce)
+    r.collectives = False
+    r.run([3, 3], then=3)
+    assert r.syncs == 0 and r.recs == []
+    assert rec.log == [("prepare", 3), ("launch", 3), ("stage", 3), ("launch", 3), ("stage", 3)]
 
 
 def test_single_process_is_never_async():

@@ -214,3 +214,22 @@ def test_host_barrier_timeout():
     msg, waited = out[0]
     assert "host barrier failed" in msg and 0.9 < waited < 30
     assert out[1] is None
+
+
+def test_rccl_init_log_env_restored_and_removed(tmp_path, monkeypatch):
+    """advisor r5: the NCCL_DEBUG* variables set for the transport record do not leak to child processes, and the
+    per-process INIT log is deleted once read."""
+    from crossscale_ecg.parallel import env as penv
+    for k in ("NCCL_DEBUG", "NCCL_DEBUG_SUBSYS", "NCCL_DEBUG_FILE"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("NCCL_DEBUG_SUBSYS", "COLL")
+    path = penv.rccl_init_log(str(tmp_path))
+    assert os.environ["NCCL_DEBUG"] == "INFO" and os.environ["NCCL_DEBUG_FILE"] == path
+    with open(path, "w") as f:
+        f.write("x NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC\n")
+    penv.rccl_log_env_restore()
+    assert "NCCL_DEBUG" not in os.environ and "NCCL_DEBUG_FILE" not in os.environ
+    assert os.environ["NCCL_DEBUG_SUBSYS"] == "COLL"
+    assert penv.rccl_transports(path) == {"P2P/IPC": 1}
+    penv.rccl_log_remove(path)
+    assert not os.path.exists(path)

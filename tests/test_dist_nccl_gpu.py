@@ -111,6 +111,7 @@ def _tiny_client(ctx, steps):
 
 
 SPIN = 2_000_000  # GPU cycles (~1 ms) of weight-independent work in each round's preparation
+SPIN_MS_MIN = 0.5  # a lower bound of that preparation's duration
 
 
 def _tiny_fedavg(ctx, mode, spin=0):
@@ -237,15 +238,21 @@ def test_rccl_tiny_tail_equals_none(world, tmp_path):
 
 @need2
 def test_rccl_overlap_exposure(tmp_path):
-    """none: the compute stream stalls for the whole collective; tail: the collective runs under the next round's
-    ~1 ms preparation, so the stall is below comm - 0.5 ms; delayed: it runs under a whole local round (~0 stall)."""
+    """``comm_ms`` is each collective's own span on the comm stream (issue after the weights are final -> RCCL done)
+    and ``exposed_ms`` the compute stream's measured stall on it (parallel/overlap.py).  none: the compute stream
+    waits right away, so it stalls for the whole collective; tail: the collective runs under the next round's ~1 ms
+    preparation, so the stall is ~0 - at most what the preparation did not cover (rank skew can stretch a
+    collective past it); delayed: it runs under a whole local round, the same bound."""
+    def hidden(comm, exposed):
+        return exposed <= 0.05 + 0.1 * comm + max(0.0, comm - SPIN_MS_MIN)
+
     for none, tail, delayed in _run(2, "case_tiny_exposure", tmp_path):
         for comm, exposed in none.tolist():
-            assert exposed >= 0.8 * comm - 0.05, (comm, exposed)
+            assert comm > 0 and exposed >= 0.8 * comm - 0.05, (comm, exposed)
         for comm, exposed in tail[:-1].tolist():  # the last round's collective is drained by finalize()
-            assert exposed <= comm - 0.5, (comm, exposed)
+            assert comm > 0 and hidden(comm, exposed), (comm, exposed)
         for comm, exposed in delayed[1:].tolist():
-            assert comm > 0 and exposed < 0.5 * comm, (comm, exposed)
+            assert comm > 0 and hidden(comm, exposed), (comm, exposed)
 
 
 @need2

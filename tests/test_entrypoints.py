@@ -147,12 +147,16 @@ def _rows(path):
 
 
 def test_overlap_modes_expose_what_they_should(tmp_path):
-    """Each round's weight-independent batch preparation sleeps DELAY ms (--inject-prep-delay-ms).
-    none: the compute side waits right after issuing -> exposed ~= comm;
-    tail: the next round's preparation runs between issue and wait -> exposed <= comm - DELAY;
+    """Each round's weight-independent batch preparation sleeps DELAY ms (--inject-prep-delay-ms).  ``comm_ms`` is
+    each collective's own span (issue -> work completion, parallel/overlap.py) and ``comm_exposed_ms`` the host
+    time blocked in ``wait``:
+    none: the host waits right after issuing -> exposed ~= comm;
+    tail: the next round's preparation runs between issue and wait -> exposed ~= 0 (whatever the preparation did
+    not cover, plus the wait call itself);
     delayed (default flags, i.e. --bcast-every-round on): the collective runs under the next round's steps ->
-    exposed well below comm while comm > 0 (the per-round broadcast must not drain it)."""
+    the same bound (the per-round broadcast must not drain it)."""
     delay = 40.0
+    slack = 0.3  # ms: the wait call on an already-complete work, on a loaded CPU container
     res = {}
     for mode in ("none", "tail", "delayed"):
         _fedavg_world2(tmp_path, ["--overlap", mode, "--inject-prep-delay-ms", str(delay)], 4, f"ov_{mode}.csv")
@@ -162,15 +166,16 @@ def test_overlap_modes_expose_what_they_should(tmp_path):
         comm, exposed = float(r["comm_ms"]), float(r["comm_exposed_ms"])
         assert comm > 0 and exposed >= 0.8 * comm - 0.5, r
     # tail: the all-reduce of round k is waited for inside round k+1's begin (after the delayed preparation);
-    # the last round's collective is drained by finalize() without a preparation in between
+    # the last round's collective is drained by finalize() without a preparation in between, and round 0's row
+    # also holds the initial model broadcast (a blocking collective: comm == exposed)
     for r in res["tail"]:
-        if int(r["round_idx"]) < 3:
+        if 0 < int(r["round_idx"]) < 3:
             comm, exposed = float(r["comm_ms"]), float(r["comm_exposed_ms"])
-            assert comm >= 0.9 * delay and exposed <= comm - 0.9 * delay, r
-    dl = [r for r in res["delayed"] if int(r["round_idx"]) < 3]
+            assert comm > 0 and exposed <= slack + 0.1 * comm + max(0.0, comm - 0.9 * delay), r
+    dl = [r for r in res["delayed"] if 0 < int(r["round_idx"]) < 3]
     comm = sum(float(r["comm_ms"]) for r in dl)
     exposed = sum(float(r["comm_exposed_ms"]) for r in dl)
-    assert comm > 0 and exposed < 0.5 * comm, (comm, exposed)
+    assert comm > 0 and exposed <= len(dl) * slack + 0.1 * comm, (comm, exposed)
 
 
 def test_delayed_trajectory_independent_of_ckpt_every(tmp_path):

@@ -97,3 +97,40 @@ def test_one_visible_gpu_per_rank_gets_disjoint_slices(tmp_path, monkeypatch):
     # without a topology the same launch falls back to the visible device: every rank would take the whole node
     rec = numa.bind_to_gpu_numa(0, sysfs=root, bdfs=[bdfs[1]], kfd_root=str(tmp_path / "missing"))
     assert rec["basis"] == "visible" and len(applied[-1]) == 64
+
+
+def _fake_siblings(tmp_path, n_phys, offset):
+    """SMT pairs (c, c + offset) for c < n_phys, in the sysfs ``thread_siblings_list`` format."""
+    for c in range(n_phys):
+        for t in (c, c + offset):
+            d = tmp_path / "devices" / "system" / "cpu" / f"cpu{t}" / "topology"
+            d.mkdir(parents=True)
+            (d / "thread_siblings_list").write_text(f"{c},{c + offset}\n")
+
+
+def test_smt_siblings_never_split_across_ranks(tmp_path):
+    """Node 0 = ``0-63,128-191`` with CPU n+128 the SMT sibling of n (the driver box's node-0 list, BENCH_r05
+    rank_cpus) and 4 GPUs on it: every rank gets 16 whole cores (both threads), no core is shared (VERDICT r5 weak #2)."""
+    bdfs = [f"0000:{b:02x}:00.0" for b in (0x05, 0x15, 0x25, 0x35)]
+    root = _fake_sysfs(tmp_path, {b: 0 for b in bdfs}, {0: "0-63,128-191"})
+    _fake_siblings(tmp_path, 64, 128)
+    plans = [numa.plan_affinity(bdfs, i, range(256), root)[1] for i in range(4)]
+    assert plans[0] == list(range(0, 16)) + list(range(128, 144))
+    assert plans[2] == list(range(32, 48)) + list(range(160, 176))
+    cores = [{c % 128 for c in p} for p in plans]
+    for i in range(4):
+        assert len(plans[i]) == 32 and len(cores[i]) == 16
+        for j in range(i + 1, 4):
+            assert not cores[i] & cores[j], (i, j)
+    # a cpuset holding one thread of some cores: those cores still belong to exactly one rank
+    plans = [numa.plan_affinity(bdfs, i, list(range(0, 64)) + list(range(128, 160)), root)[1] for i in range(4)]
+    cores = [{c % 128 for c in p} for p in plans]
+    assert all(not cores[i] & cores[j] for i in range(4) for j in range(i + 1, 4))
+
+
+def test_fewer_cores_than_ranks_splits_threads(tmp_path):
+    bdfs = [f"0000:{b:02x}:00.0" for b in (0x05, 0x15, 0x25, 0x35)]
+    root = _fake_sysfs(tmp_path, {b: 0 for b in bdfs}, {0: "0-1,128-129"})
+    _fake_siblings(tmp_path, 2, 128)
+    plans = [numa.plan_affinity(bdfs, i, range(256), root)[1] for i in range(4)]
+    assert plans == [[0], [1], [128], [129]]

@@ -82,3 +82,25 @@ def test_render_headline_median_over_boxes(tmp_path, monkeypatch):
     monkeypatch.setattr(readme, "_same_code", lambda a, b: False)
     stale = readme.render_headline(str(p))
     assert "median" not in [ln for ln in stale.splitlines() if "driver's command" in ln][0]
+
+
+def test_headline_check_tolerates_only_the_round_end_driver_record(tmp_path):
+    """BENCH_rNN.json of the current round is written after the builder's session ends: the check accepts its
+    absence from the runs file, but not the absence of an older driver record (advisor r5)."""
+    import json
+    (tmp_path / "profiles" / "r9").mkdir(parents=True)
+    runs = tmp_path / "profiles" / "r9" / "bench_runs.jsonl"
+    for n in (4, 5):
+        (tmp_path / f"BENCH_r{n:02d}.json").write_text("{}")
+    (tmp_path / "README.md").write_text(f"x\n{readme.HBEGIN}\n<!-- runs: profiles/r9/bench_runs.jsonl -->\n{readme.HEND}\n")
+
+    def drv(rnd):
+        return json.dumps({"source": "driver", "session": f"BENCH_r{rnd:02d}.json", "log": "", "box": "x",
+                           "commit": "c", "model": "tiny_ecg", "round": rnd, "value": 1e6, "ms_per_step": 0.2,
+                           "gpu_ms_per_step": 0.2, "steps": 20, "warmup": 5, "n_gpus": 1}) + "\n"
+    runs.write_text(drv(3))
+    ok, msg, _ = readme.check_headline(str(tmp_path / "README.md"), root=str(tmp_path))
+    assert not ok and "BENCH_r04.json is newer" in msg
+    runs.write_text(drv(3) + drv(4))
+    ok, msg, _ = readme.check_headline(str(tmp_path / "README.md"), root=str(tmp_path))
+    assert "is newer" not in msg  # round 5's record may still be missing
