@@ -315,6 +315,14 @@ def main(argv=None):
     else:
         model = TinyECG(num_classes=2).to(dev)
     flat = model.flatten_parameters()
+    if ctx.distributed:
+        # round-0 broadcast of the global model (reference part3_fedavg_overlap_mpi_gpu.py:186) - also the first use
+        # of the communicator - and one all-reduce of a scratch buffer of the weights' size, so RCCL's connection
+        # set-up and first-collective costs stay out of the timed region even with --warmup 0
+        from crossscale_ecg.parallel.fedavg import Communicator, broadcast_model, allreduce_mean_
+        broadcast_model(Communicator(ctx), model)
+        allreduce_mean_(torch.zeros_like(flat), ctx)
+        sync()
 
     if resnet and a.backend == "fused":  # native ResNet step engine (one hipGraph per step)
         from crossscale_ecg.train.resnet_trainer import ResNetEngineTrainer

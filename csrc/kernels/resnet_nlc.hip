@@ -21,6 +21,7 @@
 //
 // All reductions have a fixed order: the step is bitwise deterministic for a given batch.
 #include "../include/ecg_common.h"
+#include <cstdlib>
 
 #include "../include/bn_tail.h"
 
@@ -1241,8 +1242,13 @@ int side_lane(SideLane** out) {
     int lo = 0, hi = 0;
     ECG_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     ECG_HIP_CHECK(hipStreamCreateWithPriority(&l.side, hipStreamNonBlocking, lo));
-    ECG_HIP_CHECK(hipEventCreateWithFlags(&l.fork, hipEventDisableTiming));
-    ECG_HIP_CHECK(hipEventCreateWithFlags(&l.join, hipEventDisableTiming));
+    // ECG_SIDE_NOFENCE=1: the fork / join markers carry no system-scope fence (hipEventDisableSystemFence) - they
+    // only order two device streams; the producing kernel's own end-of-kernel release and the consumer's acquire
+    // already make the data visible device-wide (A/B: profiles/r6/side_fence_ab.txt)
+    const char* nf = getenv("ECG_SIDE_NOFENCE");
+    const unsigned ef = hipEventDisableTiming | ((nf && atoi(nf)) ? hipEventDisableSystemFence : 0u);
+    ECG_HIP_CHECK(hipEventCreateWithFlags(&l.fork, ef));
+    ECG_HIP_CHECK(hipEventCreateWithFlags(&l.join, ef));
   }
   *out = &l;
   return ecg::kOk;
