@@ -293,12 +293,8 @@ class ResNetStepEngine:
         # BN_FIN op after each conv forward and data-grad conv.  ECG_BN_TAIL=0: separate (one-launch) BN_FIN ops.
         use_tail = os.environ.get("ECG_BN_TAIL", "1") != "0"
         self.bn_tail = use_tail
-        # ECG_BN_TAIL_XCD=1: XCD-local level-1 groups in the kernels that support them (bn_tail.h)
-        xcd_tail = os.environ.get("ECG_BN_TAIL_XCD", "0") != "0"
-        self.bn_tail_xcd = xcd_tail
         tail_blobs: List[bytes] = []
-        TB = 320  # bytes per BnTail blob (5 header words + 2 BnFin, padded)
-        tails_dev = self._t(160 * TB, dtype=torch.uint8)  # room for 160 fused finalizes (ResNet-34 uses 68)
+        tails_dev = self._t(160 * 304, dtype=torch.uint8)  # room for 160 fused finalizes (ResNet-34 uses 68)
 
         def fin_fwd_words(st: _BN, n):
             bn = st.bn
@@ -317,17 +313,16 @@ class ResNetStepEngine:
             # larger level-1 groups - ~sqrt(2T) - measured 3.83-3.85 vs 3.78-3.79 ms/step at B=1024,
             # profiles/r3/resnet_epi_tail_ab.txt.)
             gs = max(8, -(-T // 32))
-            NG = max((T + gs - 1) // gs, 8)  # groups allocated: the default grouping's and the XCD-local 8
+            NG = (T + gs - 1) // gs
             cnt = torch.zeros((Cout // 64) * (NG + 1), dtype=torch.int32, device=dev)
             self._keep.append(cnt)
             gpart = self._t((Cout // 64) * NG * 3 * 64, dtype=torch.float64)
-            flags = len(fins) | ((1 << 16) if xcd_tail else 0)
-            blob = struct.pack("<qqqqq", cnt.data_ptr(), gpart.data_ptr(), gs, flags, NG) + b"".join(fins)
-            blob += b"\0" * (TB - len(blob))
+            blob = struct.pack("<qqqq", cnt.data_ptr(), gpart.data_ptr(), gs, len(fins)) + b"".join(fins)
+            blob += b"\0" * (304 - len(blob))
             tail_blobs.append(blob)
             if len(tail_blobs) > 160:
                 raise RuntimeError("too many fused BatchNorm finalizes")
-            return tails_dev.data_ptr() + TB * (len(tail_blobs) - 1)
+            return tails_dev.data_ptr() + 304 * (len(tail_blobs) - 1)
 
         # data-grad epilogues re-derive the BN1 ReLU mask from z1 and BN1's scale/shift instead of reading the stored
         # activation a1 (bitwise the same mask: the BN_ACT expression repeated; one activation read less per block).

@@ -42,18 +42,15 @@ struct BnFin {
 };
 
 struct BnTail {
-  unsigned* counters;  // [Cout/64][ngmax + 1] (column block nt uses row nt), zero between launches
-  double* gpart;       // [Cout/64][ngmax][3][64] level-1 group partials (row stride in doubles: ngmax * 3 * 64)
-  int64_t gs;          // M tiles per level-1 group (default grouping)
-  int64_t nfin;        // bits 0-7: 1 or 2 BatchNorms finalized from the same statistics (data-grad conv + downsample);
-                       // bits 8-15: diagnostic early exit (scripts/conv_cold_probe.py): 1 after the level-1 ticket, 2
-                       // after the level-2 ticket (counters reset, nothing finalized), 3 after the level-2 loads -
-                       // never set by the engine; bit 16 (kTailXcd): XCD-local level-1 groups where the kernel
-                       // supports them
-  int64_t ngmax;       // groups allocated per 64-column block (>= the default grouping's and >= 8)
+  unsigned* counters;  // [Cout/64][NG + 1] (column block nt uses row nt), zero between launches
+  double* gpart;       // [Cout/64][NG][3][64] level-1 group partials (row stride in doubles: NG * 3 * 64)
+  int64_t gs;          // M tiles per level-1 group
+  int64_t nfin;        // 1 or 2 BatchNorms finalized from the same statistics (data-grad conv + downsample); bits
+                       // 8+: diagnostic early exit (scripts/conv_cold_probe.py): 1 after the level-1 ticket, 2 after
+                       // the level-2 ticket (counters reset, nothing finalized), 3 after the level-2 loads - never
+                       // set by the engine
   BnFin fin[2];
 };
-constexpr int64_t kTailXcd = 1 << 16;
 
 __device__ __forceinline__ void bn_fin_channel(const BnFin& f, int c, double v1, double v2) {
   const double n = f.n;
@@ -92,62 +89,24 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Level-1 group of a partial row: the group index, its rows base + i * stride (i < members), and the group count.
-struct TailGroup {
-  int g, base, stride, members, NG;
-};
-
-// The default grouping: ``gs`` consecutive M tiles per group (BnTail::gs), any placement.
-__device__ __forceinline__ TailGroup tail_group_default(const BnTail* tp, int MT, int mt) {
-  const int gs = (int)tp->gs;
-  const int g = mt / gs;
-  return TailGroup{g, g * gs, 1, min(gs, MT - g * gs), (MT + gs - 1) / gs};
-}
-
-// XCD-local grouping: one group per XCD - the rows written by the workgroups of one XCD - so
-// the group's last arriver reads its members' rows from its OWN L2 (the members store them plain: plain stores keep
-// the line in the XCD's L2, sc1 stores drop it; MI355X guide, inter-workgroup visibility table) and level 2 reads
-// only 8 group rows across the fabric.  Placement: workgroups are dealt round-robin over the 8 XCDs (blocks b and
-// b + 8 share one; the guide's observed dispatch, probed at engine set-up by ecg_xcd_dealing_ok).
-// Bijective-remap kernels (tile wgid = contiguous range per XCD, mt = wgid / NT, nt = wgid % NT): rows of column
-// block nt on XCD x form the contiguous range [ceil((s_x - nt) / NT), ceil((s_x + c_x - nt) / NT)).
-__device__ __forceinline__ TailGroup tail_group_xcd_remap(int nwg, int NT, int nt, int xcd) {
-  const int q8 = nwg / 8, r8 = nwg % 8;
-  const int sx = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
-  const int cx = q8 + (xcd < r8 ? 1 : 0);
-  const int lo = (sx - nt + NT - 1) / NT, hi = (sx + cx - nt + NT - 1) / NT;
-  return TailGroup{xcd, lo, 1, hi - lo, 8};
-}
-// Persistent grids whose partial row is the block index itself (row gm = blockIdx.x of GM): rows x, x + 8, ...
-__device__ __forceinline__ TailGroup tail_group_xcd_strided(int GM, int gm) {
-  const int x = gm % 8;
-  return TailGroup{x, x, 8, (GM - x + 7) / 8, 8};
-}
-// Every group non-empty: each XCD holds at least NT consecutive tiles (remap) / one block (strided).
-__device__ __forceinline__ bool xcd_tail_ok(const BnTail* tp, int nwg, int NT) {
-  return tp != nullptr && (tp->nfin & kTailXcd) != 0 && nwg >= 8 * NT;
-}
-
-// Called by EVERY thread of a statistics-producing workgroup after it stored its partial row for M tile ``mt`` of
-// column block ``nt`` (columns n0 .. n0 + BN, BN <= 256 and a multiple of 64): sc1 (write-through) for the default
-// grouping, plain for an XCD-local group.  ``lds``: >= 3 * 256 doubles + 16 bytes of dead LDS.
+// Called by EVERY thread of a statistics-producing workgroup after it stored its partial row (sc1) for M tile
+// ``mt`` of column block ``nt`` (columns n0 .. n0 + BN, BN <= 256 and a multiple of 64).  ``lds``: >= 3 * 256
+// doubles + 16 bytes of dead LDS.
 template <int NTHR>
 __device__ __forceinline__ void bn_tail(const BnTail* __restrict__ tp, const float* __restrict__ stats, int NS,
-                                        int MT, int Cout, int mt, int n0, int BN, unsigned char* lds,
-                                        const TailGroup* grp = nullptr) {
+                                        int MT, int Cout, int mt, int n0, int BN, unsigned char* lds) {
   const int tid = threadIdx.x;
   int* flag = reinterpret_cast<int*>(lds);
   double* sums = reinterpret_cast<double*>(lds + 16);
-  const int stop = (int)((tp->nfin >> 8) & 0xff);
-  const TailGroup G = grp ? *grp : tail_group_default(tp, MT, mt);
-  const int g = G.g, members = G.members, NG = G.NG;
+  const int gs = (int)tp->gs;
+  const int stop = (int)(tp->nfin >> 8);
+  const int NG = (MT + gs - 1) / gs;
+  const int g = mt / gs, members = min(gs, MT - g * gs);
   const int nb0 = n0 / 64, nblk = BN / 64;  // 64-column blocks of this workgroup
   // counters / group partials are kept per 64-column block so the host need not know the tile width: the
-  // workgroup's blocks arrive together (one ticket on the first block's counter stands for all of them).  Row
-  // strides follow the allocation (BnTail::ngmax >= NG groups per block).
-  const int NGA = (int)tp->ngmax;
-  unsigned* cnt = tp->counters + (long)nb0 * (NGA + 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have completed
+  // workgroup's blocks arrive together (one ticket on the first block's counter stands for all of them).
+  unsigned* cnt = tp->counters + (long)nb0 * (NG + 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 partial stores have completed
   __syncthreads();
   if (tid == 0)
     flag[0] = __hip_atomic_fetch_add(&cnt[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(members - 1);
@@ -158,18 +117,16 @@ __device__ __forceinline__ void bn_tail(const BnTail* __restrict__ tp, const flo
     return;
   }
   // ---- level 1: the group's rows, in row order, per (stat, column).  Every load of a batch (up to 32 rows) is
-  // issued before the first add: one round trip per batch, not one per row.  sc1 loads bypass L1 and are served by
-  // L2: for an XCD-local group the rows are L2 hits.
-  const long gstride = (long)NGA * 3 * 64;  // doubles per 64-column block
+  // issued before the first add: one round trip per batch, not one per row.
+  const long gstride = (long)NG * 3 * 64;  // doubles per 64-column block
   for (int p = tid; p < NS * BN; p += NTHR) {
     const int st = p / BN, c = p - st * BN;
-    const float* src = stats + ((long)st * MT + G.base) * Cout + n0 + c;
-    const long rstep = (long)G.stride * Cout;
+    const float* src = stats + ((long)st * MT + g * gs) * Cout + n0 + c;
     double s = 0.0;
     for (int r0 = 0; r0 < members; r0 += 32) {
       float v[32];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) v[u] = ld_sc1(src + (long)min(r0 + u, members - 1) * rstep);  // clamped: no branch
+      for (int u = 0; u < 32; ++u) v[u] = ld_sc1(src + (long)min(r0 + u, members - 1) * Cout);  // clamped: no branch
 #pragma unroll
       for (int u = 0; u < 32; ++u) s += r0 + u < members ? (double)v[u] : 0.0;
     }

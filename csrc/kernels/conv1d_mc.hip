@@ -384,12 +384,10 @@ __device__ __forceinline__ void fwd_epi_tile(const FwdArgs& a, f32x4 (&acc)[BM /
 }
 
 // The lanes' running statistics -> one partial row ``row`` of ``nrows`` (columns n0 .. n0 + BN).  Block-uniform
-// call (a.stats != null); ``smem``: the dead epilogue region.  With a fused finalize the row is stored write-through
-// (sc1) for a reader on any XCD, or plain (``xcd_local``: the line stays in this XCD's L2, where the XCD-local tail
-// group's reader finds it; bn_tail.h).
+// call (a.stats != null); ``smem``: the dead epilogue region.
 template <int BM, int BN, int EPI, int NWR = 2>
 __device__ __forceinline__ void fwd_epi_stats(const FwdArgs& a, unsigned char* smem, EpiConst& k, int n0, int row,
-                                              int nrows, bool xcd_local = false) {
+                                              int nrows) {
   using Cfg = FwdCfg<BM, BN, NWR>;
   constexpr int WN = Cfg::WN, HR = Cfg::WM / 2, EP_LD = Cfg::EP_LD, CG = WN / 8;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -420,7 +418,7 @@ __device__ __forceinline__ void fwd_epi_stats(const FwdArgs& a, unsigned char* s
 #pragma unroll
     for (int r = 0; r < NWR; ++r) v += sred[(3 * r + st) * BN + c];
     float* dst = a.stats + ((long)st * nrows + row) * a.Cout + n0 + c;
-    if (a.tail && !xcd_local)
+    if (a.tail)
       ecg::st_sc1(dst, v);  // handed to the tail's last arriver inside this launch (write-through)
     else
       *dst = v;
@@ -829,13 +827,8 @@ __global__ __launch_bounds__(128 * NWR, 2) void conv1d_nlc_fwd_dma_mt_kernel(Fwd
     }
   }
   if (a.stats) {
-    const bool xl = a.tail && ecg::xcd_tail_ok(a.tail, nwg, NT);  // block-uniform
-    fwd_epi_stats<BM, BN, EPI, NWR>(a, eps, k, n0, gm, GM, xl);
-    if (a.tail) {
-      const ecg::TailGroup tg = ecg::tail_group_xcd_remap(nwg, NT, nt, xcd);
-      ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, GM, a.Cout, gm, n0, BN, smem,
-                              xl ? &tg : nullptr);
-    }
+    fwd_epi_stats<BM, BN, EPI, NWR>(a, eps, k, n0, gm, GM);
+    if (a.tail) ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, GM, a.Cout, gm, n0, BN, smem);
   }
 }
 
@@ -1045,13 +1038,9 @@ __global__ __launch_bounds__(512, 1) void conv1d_nlc_fwd_tap_kernel(FwdArgs a, i
   EpiConst k;
   k.load<EPI == 1>(a, EpiLane<BN, NWR>::n(n0));
   fwd_epi_tile<BM, BN, EPI, NWR, EPI == 1>(a, acc, smem, k, m0, n0, L, M, 1, 0);
-  const bool xl = a.tail && ecg::xcd_tail_ok(a.tail, nwg, NT);  // block-uniform
-  if (a.stats) fwd_epi_stats<BM, BN, EPI, NWR>(a, smem, k, n0, mt, MT, xl);  // block-uniform
-  if (a.tail && a.stats) {
-    const ecg::TailGroup tg = ecg::tail_group_xcd_remap(nwg, NT, nt, xcd);
-    ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, MT, a.Cout, mt, n0, BN, smem,
-                            xl ? &tg : nullptr);
-  }
+  if (a.stats) fwd_epi_stats<BM, BN, EPI, NWR>(a, smem, k, n0, mt, MT);  // block-uniform
+  if (a.tail && a.stats)
+    ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, MT, a.Cout, mt, n0, BN, smem);
 }
 
 // ------------------------------------------------------------------ tap-shared strided data-grad
@@ -1192,13 +1181,9 @@ __global__ __launch_bounds__(512, 1) void conv1d_nlc_dgrad_s2_tap_kernel(FwdArgs
   EpiConst kc;
   kc.load<EPI == 1>(a, EpiLane<BN, NWR>::n(n0));
   fwd_epi_tile<TAP_BM, BN, EPI, NWR, EPI == 1>(a, acc, smem, kc, i0, n0, Lz, Mi, 2, -1);
-  const bool xl = a.tail && ecg::xcd_tail_ok(a.tail, nwg, NT);  // block-uniform
-  if (a.stats) fwd_epi_stats<TAP_BM, BN, EPI, NWR>(a, smem, kc, n0, mt, MT, xl);  // block-uniform
-  if (a.tail && a.stats) {
-    const ecg::TailGroup tg = ecg::tail_group_xcd_remap(nwg, NT, nt, xcd);
-    ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, MT, a.Cout, mt, n0, BN, smem,
-                            xl ? &tg : nullptr);
-  }
+  if (a.stats) fwd_epi_stats<TAP_BM, BN, EPI, NWR>(a, smem, kc, n0, mt, MT);  // block-uniform
+  if (a.tail && a.stats)
+    ecg::bn_tail<Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, MT, a.Cout, mt, n0, BN, smem);
 }
 
 // ------------------------------------------------------------------ persistent tap-shared 64-channel kernel
@@ -1341,13 +1326,8 @@ __global__ __launch_bounds__(256, 2) void conv1d_nlc_tap64_kernel(FwdArgs a, int
     fwd_epi_tile_rowwise<BM, BN, EPI, NWR>(a, acc, eps, k, m0, 0, L, M, 1, 0);
   }
   if (a.stats) {
-    const bool xl = a.tail && ecg::xcd_tail_ok(a.tail, GM, 1);  // block-uniform
-    fwd_epi_stats<BM, BN, EPI, NWR>(a, eps, k, 0, gm, GM, xl);
-    if (a.tail) {
-      const ecg::TailGroup tg = ecg::tail_group_xcd_strided(GM, gm);
-      ecg::bn_tail<T64Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, GM, a.Cout, gm, 0, BN, smem,
-                                 xl ? &tg : nullptr);
-    }
+    fwd_epi_stats<BM, BN, EPI, NWR>(a, eps, k, 0, gm, GM);
+    if (a.tail) ecg::bn_tail<T64Cfg::NTHR>(a.tail, a.stats, EPI == 1 && a.szd ? 3 : 2, GM, a.Cout, gm, 0, BN, smem);
   }
 }
 

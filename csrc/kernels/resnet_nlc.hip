@@ -1242,11 +1242,13 @@ int side_lane(SideLane** out) {
     int lo = 0, hi = 0;
     ECG_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     ECG_HIP_CHECK(hipStreamCreateWithPriority(&l.side, hipStreamNonBlocking, lo));
-    // ECG_SIDE_NOFENCE=1: the fork / join markers carry no system-scope fence (hipEventDisableSystemFence) - they
-    // only order two device streams; the producing kernel's own end-of-kernel release and the consumer's acquire
-    // already make the data visible device-wide (A/B: profiles/r6/side_fence_ab.txt)
+    // The fork / join markers carry no system-scope fence (hipEventDisableSystemFence; ECG_SIDE_NOFENCE=0 restores
+    // the default event): they only order two streams of this device, and the producing kernel's own end-of-kernel
+    // release plus the consumer kernel's acquire already make the data visible device-wide; the system-scope fence
+    // of a default event made each fork's marker flush caches on the main lane.  3.308-3.329 vs 3.344-3.361 ms/step
+    // (ResNet1D-34 B=1024, interleaved; profiles/r6/bn_tail_xcd_ab.txt), engine GPU tests pass with it.
     const char* nf = getenv("ECG_SIDE_NOFENCE");
-    const unsigned ef = hipEventDisableTiming | ((nf && atoi(nf)) ? hipEventDisableSystemFence : 0u);
+    const unsigned ef = hipEventDisableTiming | ((nf == nullptr || atoi(nf)) ? hipEventDisableSystemFence : 0u);
     ECG_HIP_CHECK(hipEventCreateWithFlags(&l.fork, ef));
     ECG_HIP_CHECK(hipEventCreateWithFlags(&l.join, ef));
   }

@@ -514,7 +514,11 @@ struct TinySample {
                 // relu'(h2) = (acc > 0) as clamp(acc * 2^126, 0, 1): ONE v_mul_f32 with the clamp modifier instead of
                 // a compare + select.  Exactly 1 for every acc >= 2^-126; a bf16 x bf16 MFMA sum plus a bf16 bias is
                 // a multiple of products of bf16 ulps, so a non-zero acc below 2^-126 needs |weights x inputs|
-                // below ~2^-63 (not reachable by a trained or initialised TinyECG).
+                // below ~2^-63 (not reachable by a trained or initialised TinyECG).  Divergences from the reference's
+                // (h2 > 0), by construction: a subnormal positive acc gives a fractional mask (its h2 contribution is
+                // itself subnormal), and a NaN acc gives whatever v_med3 returns for NaN under this file's
+                // -fno-honor-nans build (the reference's mask is 0 there) - with a NaN pre-activation the pooled
+                // features, the loss and every gradient of the sample are NaN in both implementations anyway.
                 mk[i] = ecg::to_bf16(__builtin_amdgcn_fmed3f(a * 0x1p126f, 0.f, 1.f));
               }
               *reinterpret_cast<bf16x4*>(ms + (t + 4) * C + 4 * h) = mk;

@@ -48,12 +48,12 @@ def graph_time(fns, reps):
     return a.elapsed_time(b) / (3 * reps) * 1e3
 
 
-def make_tail(dev, T, C, n, stop=0, gs=None, xcd=False):
+def make_tail(dev, T, C, n, stop=0, gs=None):
     """A device BnTail blob (csrc/include/bn_tail.h) with one forward finalize, packed as the ResNet engine packs it:
     the launch then also runs the fused BatchNorm finalize (the in-step configuration of every statistics conv)."""
     import struct
     gs = gs or max(8, -(-T // 32))
-    NG = max((T + gs - 1) // gs, 8)
+    NG = (T + gs - 1) // gs
     keep = [torch.zeros((C // 64) * (NG + 1), dtype=torch.int32, device=dev),
             torch.zeros((C // 64) * NG * 3 * 64, dtype=torch.float64, device=dev),
             torch.ones(C, device=dev), torch.zeros(C, device=dev)] + [torch.zeros(C, device=dev) for _ in range(6)]
@@ -61,8 +61,8 @@ def make_tail(dev, T, C, n, stop=0, gs=None, xcd=False):
     P = lambda t: t.data_ptr()  # noqa: E731
     fin = struct.pack("<qqddd12q", 0, 1, float(n), 1e-5, 0.1, P(gam), P(bet), P(mean), P(rstd), P(scale), P(shift),
                       P(rm), P(rv), 0, 0, 0, 0)
-    blob = struct.pack("<qqqqq", P(cnt), P(gpart), gs, 1 | (stop << 8) | ((1 << 16) if xcd else 0), NG) + fin
-    blob += b"\0" * (320 - len(blob))
+    blob = struct.pack("<qqqq", P(cnt), P(gpart), gs, 1 | (stop << 8)) + fin
+    blob += b"\0" * (304 - len(blob))
     dt = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
     keep.append(dt)
     return dt.data_ptr(), keep
@@ -96,12 +96,10 @@ def main():
             warm = graph_time(fns[:1], reps)
             cold = graph_time(fns, max(reps, nbuf))
             tails = {}
-            # full tail; diagnostic exits after the level-1 / level-2 tickets (bn_tail.h); the same with XCD-local
-            # level-1 groups (kernels that support them; others ignore the flag)
+            # full tail; diagnostic exits after the level-1 / level-2 tickets (bn_tail.h); one level-1 group
             for key, kw in (("warm_tail_us", {}), ("tail_stop1_us", {"stop": 1}), ("tail_stop2_us", {"stop": 2}),
-                            ("tail_stop3_us", {"stop": 3}), ("xcd_tail_us", {"xcd": True}),
-                            ("xcd_stop1_us", {"xcd": True, "stop": 1}), ("xcd_stop2_us", {"xcd": True, "stop": 2}),
-                            ("xcd_stop3_us", {"xcd": True, "stop": 3})):
+                            ("tail_stop3_us", {"stop": 3}),
+                            ("tail_1group_us", {"gs": rows})):
                 tail_ptr, keep = make_tail(dev, rows, Co, B * L, **kw)
 
                 def ft():
