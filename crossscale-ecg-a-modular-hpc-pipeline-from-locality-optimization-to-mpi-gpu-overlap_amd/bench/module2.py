@@ -254,8 +254,16 @@ def steady_host_for_single_calls() -> Dict[str, object]:
     (``naive_conv_ab_nonpacked_fwd_nchw``, ~5 us of device time) in every cell; the 32-108 us spread of torch's
     single calls inside one cell is host-side (MIOpen's ~40 us per-call host path plus the synchronize wake-up).
     Returns what was applied; ``run_part2`` writes it to ``part2_hip_host.json`` next to the CSV."""
-    rec = spin_sync_flag()
+    # A/B knobs (profiles/r6/module2_host_ab.txt): ECG_M2_SPIN=0 keeps the runtime's default synchronize;
+    # ECG_M2_PIN=early pins the whole process before the first GPU call (round 5's form), none never pins
+    rec = spin_sync_flag() if os.environ.get("ECG_M2_SPIN", "1") != "0" else {"spin_sync": False}
     rec["pinned_cpu"] = None
+    rec["pin"] = os.environ.get("ECG_M2_PIN", "late")
+    if rec["pin"] == "early":
+        cpus = sorted(os.sched_getaffinity(0))
+        if len(cpus) > 1:
+            os.sched_setaffinity(0, {cpus[0]})
+            rec["pinned_cpu"] = cpus[0]
     return rec
 
 
@@ -286,7 +294,7 @@ def run_part2(results_dir: str = "results", gpu: bool = True, cpu: bool = True, 
             for bs in batch_sizes:
                 for K in kernel_sizes:
                     bench_pair_gpu(bs, K, np.random.default_rng(7), max(3, trials // 5))
-                    if host["pinned_cpu"] is None:  # after the first warm pass: runtime threads already exist
+                    if host["pinned_cpu"] is None and host["pin"] == "late":  # after the first warm pass
                         pin_timing_thread(host)
                         if verbose:
                             print(f"[HIP] single-call host settings: {host}", flush=True)

@@ -256,9 +256,12 @@ struct TinySample {
     for (int s = 0; s < 3; ++s) pf_wf[s] = *reinterpret_cast<const bf16x8*>(wb + WP_FRAGF + (s * 64 + lane) * 8);
   }
   __device__ __forceinline__ void pf_load_dgrad(const unsigned char* __restrict__ wp) {
-    // only waves 0..2 scale the dgrad fragments (dgrad()): wave w loads set s = w into pf_wd[0]
+    // only the head wave scales the dgrad fragments (head_and_M, right after g): wave 0 loads all three sets
     const __bf16* wb = reinterpret_cast<const __bf16*>(wp);
-    if (w < 3) pf_wd[0] = *reinterpret_cast<const bf16x8*>(wb + WP_FRAGD + (w * 64 + lane) * 8);
+    if (w == 0) {
+#pragma unroll
+      for (int s = 0; s < 3; ++s) pf_wd[s] = *reinterpret_cast<const bf16x8*>(wb + WP_FRAGD + (s * 64 + lane) * 8);
+    }
   }
 
   __device__ __forceinline__ TinySample(unsigned char* smem, int L_, int nc_)
@@ -653,7 +656,27 @@ struct TinySample {
         // dpooled[co] = sum_n dlogit[n] * Wh[n][co]; lane co (< 16)
         float dp = 0.f;
         for (int nn = 0; nn < nc; ++nn) dp = fmaf(lane_bcast(dlogit, nn), ps[lay.wh + nn * C + c], dp);
-        if (lane < 16) red[RED_G + c] = dp * (1.0f / (float)L);
+        const float gl = dp * (1.0f / (float)L);
+        if (lane < 16) red[RED_G + c] = gl;
+        if constexpr (PF) {
+          // The g-scaled conv2 dgrad fragments (phase 4's A operand; the same in every wave), built here by the head
+          // wave as soon as g exists - it finishes ~270 cycles before the last M wave - into the LDS fragD slots, so
+          // phase 4 needs no barrier of its own.  B[r][ci] = g[co] * w2[co][ci][k], co = 8(h&1) + j: the same
+          // products and rounding as the per-wave scaling of the LDS-built kernel (bitwise equal operands).
+          float gq[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float lo = lane_bcast(gl, j), hi = lane_bcast(gl, 8 + j);
+            gq[j] = (h & 1) ? hi : lo;
+          }
+#pragma unroll
+          for (int s = 0; s < 3; ++s) {
+            bf16x8 sc;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sc[j] = ecg::to_bf16(ecg::from_bf16(pf_wd[s][j]) * gq[j]);
+            *reinterpret_cast<bf16x8*>(fragD + (s * 64 + lane) * 8) = sc;
+          }
+        }
       }
     } else if (TRAIN && w <= 5 * msplit(WAVES)) {
       // work item (tap k, pair range part): M_k[co][ci] = sum_t m[t][co] * h1[t+k-2][ci]
@@ -731,18 +754,11 @@ struct TinySample {
     if constexpr (!F32) {
       // (g W2) fragments, used as A[ci][(k,co)]
       if constexpr (PF) {
-        // The scaled fragments are the same in every wave: waves 0..2 build set s = w once into the LDS fragD slots
-        // (unused by the prepared-fragment kernels: their operands come from the global image) and every wave
-        // reads its three back - 16 waves x 48 scaling VALU become 3 x 16 plus one barrier (the step is VALU-issue
-        // bound: profiles/r3/tiny_fp_flags_ab.txt).  Same products, same rounding: bitwise the same operands.
-        if (w < 3) {  // wave-uniform
-          const bf16x8 raw = pf_wd[0];  // set s = w (pf_load_dgrad)
-          bf16x8 sc;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) sc[j] = ecg::to_bf16(ecg::from_bf16(raw[j]) * gq[j]);
-          *reinterpret_cast<bf16x8*>(fragD + (w * 64 + lane) * 8) = sc;
-        }
-        __syncthreads();
+        // The scaled fragments are the same in every wave: the head wave built them into the LDS fragD slots in
+        // phase 3 (unused by the prepared-fragment kernels otherwise: their operands come from the global image),
+        // published by the phase-3 barrier; every wave reads its three back (16 waves x 48 scaling VALU become one
+        // wave's 48; the round-5 form, waves 0..2 scaling one set each behind an extra barrier, cost that barrier).
+        // Same products, same rounding: bitwise the same operands.
 #pragma unroll
         for (int s = 0; s < 3; ++s) Bd[s] = *reinterpret_cast<const bf16x8*>(fragD + (s * 64 + lane) * 8);
       } else {

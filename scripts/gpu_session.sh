@@ -74,6 +74,11 @@ for s in "$@"; do
         --results-dir "$OUT/modules" ;;
     module2)
       step module2 900 python benchmark_part_2.py --results-dir "$OUT/modules" ;;
+    m2host)  # Module-2 single-call host settings A/B (GPU part only): spin-wait sync x timing-thread pin
+      for r in 1 2; do for sp in 1 0; do for pin in late early; do
+        ECG_M2_SPIN=$sp ECG_M2_PIN=$pin step m2host_s${sp}_${pin}_$r 300 python benchmark_part_2.py --no-cpu \
+          --results-dir "$OUT/m2host_s${sp}_${pin}_$r"
+      done; done; done ;;
     m2trace)  # which MIOpen kernels / HIP calls torch.nn.Conv1d runs per Module-2 cell
       export TMPDIR=/tmp
       step m2trace 400 rocprofv3 --kernel-trace --hip-trace --marker-trace --output-format csv -d "$OUT/m2trace" \

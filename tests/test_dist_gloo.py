@@ -233,3 +233,30 @@ def test_rccl_init_log_env_restored_and_removed(tmp_path, monkeypatch):
     assert penv.rccl_transports(path) == {"P2P/IPC": 1}
     penv.rccl_log_remove(path)
     assert not os.path.exists(path)
+
+
+def case_comm_span_is_completion_time(ctx):
+    """FedAvgComm host timing: comm_ms ends when the collective COMPLETED (its future's callback), not when the
+    consumer looked; the host stall is only the time blocked in ``wait``."""
+    import time
+    from crossscale_ecg.parallel.overlap import CommRecord, FedAvgComm
+    comm = FedAvgComm(ctx)
+    t = torch.full((1458,), float(ctx.rank))
+    out = []
+    for _ in range(3):
+        dist.barrier()
+        rec = CommRecord()
+        p = comm.issue(t, rec)
+        time.sleep(0.05)  # 50 ms of weight-independent work before the consumer waits
+        comm.wait([p], rec)
+        out.append((rec.comm_ms(), rec.exposed_ms()))
+    return comm.kind, out, float(t[0])
+
+
+def test_fedavgcomm_host_span_and_stall():
+    res = _run(2, "case_comm_span_is_completion_time")
+    for kind, spans, v in res.values():
+        assert kind == "host" and v == 0.5  # the average of ranks 0 and 1 (SUM + divide chained on the future)
+        # the collective itself is far shorter than the 50 ms before the wait; nothing left to wait for
+        assert sum(c for c, _ in spans) / len(spans) < 25.0, spans
+        assert all(e < 5.0 for _, e in spans), spans
