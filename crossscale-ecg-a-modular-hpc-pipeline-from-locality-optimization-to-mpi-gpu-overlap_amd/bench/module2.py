@@ -247,18 +247,20 @@ def spin_sync_flag() -> Dict[str, object]:
 
 
 def steady_host_for_single_calls() -> Dict[str, object]:
-    """Host settings for the single-call (``time_once``) GPU timings: the spin-wait synchronize (``spin_sync_flag``)
-    applied before the first GPU call of the run.  The timing thread is pinned later (``pin_timing_thread``), once
-    the HIP context, MIOpen handles and torch's helper threads exist, so none of them inherits the one-CPU mask.
+    """Host settings for the single-call (``time_once``) GPU timings, applied before the first GPU call of the run:
+    the process pinned to one CPU of its affinity set (``ECG_M2_PIN``: ``early`` = default; ``late`` = only the timing
+    thread, after the first warm cell; ``none``), and ``hipDeviceScheduleSpin`` through torch's own HIP runtime when
+    ``ECG_M2_SPIN=1`` (``spin_sync_flag``; default off).  Measured (profiles/r6/module2_host_ab.txt, 2 runs per
+    setting): the early process pin gives torch single calls of 31-36 us in every cell; pinning only the timing thread
+    later leaves the first cells at 50-84 us, and the spin-wait synchronize changes nothing measurable - so the default
+    is round 5's effective setting (early pin, runtime-default synchronize), now recorded as what it is.
     Round 4/5 traces (scripts/trace_module2_miopen.py, profiles/r5/module2_miopen_trace.txt) show ONE MIOpen solver
-    (``naive_conv_ab_nonpacked_fwd_nchw``, ~5 us of device time) in every cell; the 32-108 us spread of torch's
-    single calls inside one cell is host-side (MIOpen's ~40 us per-call host path plus the synchronize wake-up).
+    (``naive_conv_ab_nonpacked_fwd_nchw``, ~5 us of device time) in every cell; the spread of torch's single calls is
+    host-side (MIOpen's per-call host path plus the synchronize wake-up).
     Returns what was applied; ``run_part2`` writes it to ``part2_hip_host.json`` next to the CSV."""
-    # A/B knobs (profiles/r6/module2_host_ab.txt): ECG_M2_SPIN=0 keeps the runtime's default synchronize;
-    # ECG_M2_PIN=early pins the whole process before the first GPU call (round 5's form), none never pins
-    rec = spin_sync_flag() if os.environ.get("ECG_M2_SPIN", "1") != "0" else {"spin_sync": False}
+    rec = spin_sync_flag() if os.environ.get("ECG_M2_SPIN", "0") != "0" else {"spin_sync": False}
     rec["pinned_cpu"] = None
-    rec["pin"] = os.environ.get("ECG_M2_PIN", "late")
+    rec["pin"] = os.environ.get("ECG_M2_PIN", "early")
     if rec["pin"] == "early":
         cpus = sorted(os.sched_getaffinity(0))
         if len(cpus) > 1:
