@@ -29,6 +29,7 @@ import torch
 
 from ..ops.conv1d import HipConv1dValid, conv1d_valid, run_omp_conv, conv1d_valid_reference
 from ..utils import usable_cpus
+from ..utils.hip_host import _loaded_hip_runtime, spin_sync_flag  # noqa: F401  (re-exported)
 from ..utils.csvio import PART2_COLUMNS, PART2_RAW_COLUMNS, PART2_SCALING_COLUMNS, safe_write_csv
 
 BATCH_SIZES = [64, 128, 256, 512]
@@ -206,44 +207,6 @@ HIP_COLUMNS = ["batch_size", "kernel_size", "backend", "torch_ms_median", "torch
                "torch_ms_p95", "hip_ms_median", "hip_ms_mean", "hip_ms_std", "hip_ms_p95", "torch_sps", "hip_sps",
                "speedup_med", "torch_burst_ms_median", "hip_burst_ms_median", "speedup_burst", "torch_ev_ms",
                "hip_ev_ms", "speedup_ev", "max_abs_err"]
-
-
-def _loaded_hip_runtime() -> str | None:
-    """Path of the HIP runtime this process has mapped (torch's, torch/lib/libamdhip64.so.*), from /proc/self/maps."""
-    try:
-        with open("/proc/self/maps") as f:
-            for line in f:
-                i = line.find("/")
-                if i >= 0 and "libamdhip64.so" in line[i:]:
-                    return line[i:].strip()
-    except OSError:
-        pass
-    return None
-
-
-def spin_sync_flag() -> Dict[str, object]:
-    """``hipSetDeviceFlags(hipDeviceScheduleSpin)`` through the HIP runtime torch already loaded (RTLD_NOLOAD on
-    the mapped path: never a second runtime whose flags torch would not see), read back with ``hipGetDeviceFlags``.
-    ``torch.cuda.synchronize()`` then spins instead of yielding the CPU, as the HIP op's own completion wait already
-    does (host-flag spin), so both sides of a single-call timing pay the same wake-up cost."""
-    import ctypes
-    rec: Dict[str, object] = {"spin_sync": False, "hip_runtime": None, "device_flags": None}
-    path = _loaded_hip_runtime()
-    rec["hip_runtime"] = path
-    if path is None:
-        return rec
-    try:
-        hip = ctypes.CDLL(path, mode=os.RTLD_NOLOAD | ctypes.RTLD_GLOBAL)
-    except OSError as e:
-        rec["error"] = repr(e)[:120]
-        return rec
-    st = hip.hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
-    flags = ctypes.c_uint(0)
-    if hip.hipGetDeviceFlags(ctypes.byref(flags)) == 0:
-        rec["device_flags"] = int(flags.value)
-    rec["set_status"] = int(st)
-    rec["spin_sync"] = rec["device_flags"] is not None and (rec["device_flags"] & 0x7) == 1
-    return rec
 
 
 def steady_host_for_single_calls() -> Dict[str, object]:
