@@ -83,7 +83,8 @@ for s in "$@"; do
       export TMPDIR=/tmp
       step m2trace 400 rocprofv3 --kernel-trace --hip-trace --marker-trace --output-format csv -d "$OUT/m2trace" \
         -o t -- python3 scripts/trace_module2_miopen.py run
-      step m2parse 120 python scripts/trace_module2_miopen.py parse "$OUT/m2trace" ;;
+      step m2parse 120 python scripts/trace_module2_miopen.py parse "$OUT/m2trace"
+      rm -rf "$OUT/m2trace" ;;  # the raw HIP-API trace exceeds what gpurun copies back; the parse is the record
     module3)
       [ -d data/shards ] || step shard_prep 300 python shard_prep.py --dataset synthetic
       step pseudo_fl 600 python part3_mpi_gpu_train.py --steps 200 --results-csv "$OUT/modules/part3_mpi_cuda_results.csv"
