@@ -4,7 +4,8 @@ Reference scripts and formulas reproduced:
   * plot_locality       <- Module_1/plot_locality.py:7-76 (throughput vs batch, stacked data/h2d/compute)
   * plot_all_results    <- Module_1/plot_all_results.py:1-130 (A0-A4 merge; effective A4 throughput
                            ``sps / (1 + shard_time / (EPOCHS * N / sps))`` with EPOCHS=10 (:53-58);
-                           per-step shard ms ``(shard_time/EPOCHS)/(N/bs)*1e3`` (:84-90))
+                           per-step shard ms ``(shard_time/EPOCHS)/(N/bs)*1e3`` (:84-90)); its two figures:
+                           plot_all_results_figures
   * plot_part2          <- Module_2/benchmark_part_2.py:149-173 and Module_2/plot_part2.py
   * plot_pseudo_fl      <- Module_3/plot_part3.py (mean per (world, config), throughput-vs-world + stacked bars)
   * plot_fedavg         <- Module_3/TRUE_FL_M3/plot_part3.py (``step_ms = local_train_ms + comm_ms`` (:48));
@@ -89,6 +90,49 @@ def plot_all_results(results_dir: str) -> Optional[str]:
     return out
 
 
+def plot_all_results_figures(results_dir: str, batch: int = 512) -> List[str]:
+    """The two figures of Module_1/plot_all_results.py from ``part1_all_results.csv`` (written first): throughput
+    vs batch for every configuration plus the A4 curve with the shard preparation amortised (when the shard-prep
+    JSON exists), and the per-step time breakdown at ``batch`` with A4's amortised shard ms stacked on top."""
+    csv_path = plot_all_results(results_dir)
+    if csv_path is None:
+        return []
+    plt = _plt()
+    df = _read(csv_path)
+    outs = []
+    fig = plt.figure(figsize=(6.8, 4.2))
+    for cfg in df["config"].unique():
+        sub = df[df["config"] == cfg].sort_values("batch_size")
+        plt.plot(sub["batch_size"], sub["samples_per_s"], marker="o", label=cfg)
+    if "effective_samples_per_s" in df:
+        a4 = df[df["effective_samples_per_s"].notna()].sort_values("batch_size")
+        if len(a4):
+            plt.plot(a4["batch_size"], a4["effective_samples_per_s"], marker="x", linestyle="--",
+                     label="A4_LABL (shard prep amortised)")
+    plt.xlabel("Batch size"); plt.ylabel("Samples / second"); plt.title("Throughput Comparison (A0-A4, MI355X)")
+    plt.grid(True); plt.legend(fontsize=7); plt.tight_layout()
+    p = os.path.join(results_dir, "throughput_comparison_A0_A4.png"); plt.savefig(p, dpi=150); plt.close(fig)
+    outs.append(p)
+    d = df[df["batch_size"] == batch]
+    if len(d):
+        x = np.arange(len(d))
+        fig = plt.figure(figsize=(7.2, 4.2))
+        bottom = np.zeros(len(d))
+        for col in ("data_ms", "h2d_ms", "compute_ms"):
+            v = d[col].fillna(0.0).values
+            plt.bar(x, v, width=0.6, bottom=bottom, label=col)
+            bottom = bottom + v
+        if "shard_ms_per_step" in d and d["shard_ms_per_step"].notna().any():
+            plt.bar(x, d["shard_ms_per_step"].fillna(0.0).values, width=0.6, bottom=bottom, hatch="//",
+                    label="shard_ms (amortised)")
+        plt.xticks(x, d["config"], rotation=20, fontsize=7); plt.ylabel("Milliseconds per step")
+        plt.title(f"Time Breakdown per Step (batch={batch})"); plt.legend(fontsize=7); plt.tight_layout()
+        p = os.path.join(results_dir, f"time_breakdown_batch{batch}_A0_A4.png"); plt.savefig(p, dpi=150)
+        plt.close(fig)
+        outs.append(p)
+    return outs
+
+
 def plot_part2(results_dir: str) -> List[str]:
     plt = _plt()
     outs = []
@@ -145,6 +189,23 @@ def plot_pseudo_fl(csv_path: str, out_dir: str) -> List[str]:
     plt.xlabel("World size"); plt.ylabel("Samples / second (per rank, mean)"); plt.title("Pseudo-FL throughput")
     plt.grid(True); plt.legend(); plt.tight_layout()
     p = os.path.join(out_dir, "part3_throughput_vs_world.png"); plt.savefig(p, dpi=150); plt.close(fig); outs.append(p)
+    # grouped stacked bars (Module_3/plot_part3.py plot 2): per world size one bar per configuration, each stacked
+    # h2d_ms + compute_ms (the reference leaves data_ms out of this figure)
+    worlds = sorted(g["world_size"].unique())
+    cfgs = list(g["config"].unique())
+    width = 0.8 / max(1, len(cfgs))
+    x = np.arange(len(worlds))
+    fig = plt.figure(figsize=(7.2, 4.2))
+    for i, cfg in enumerate(cfgs):
+        d = g[g["config"] == cfg].set_index("world_size").reindex(worlds)
+        pos = x + (i - (len(cfgs) - 1) / 2) * width
+        h2d, comp = d["h2d_ms"].fillna(0.0).values, d["compute_ms"].fillna(0.0).values
+        plt.bar(pos, h2d, width=width, label=f"{cfg} h2d_ms")
+        plt.bar(pos, comp, width=width, bottom=h2d, label=f"{cfg} compute_ms")
+    plt.xticks(x, [str(w) for w in worlds]); plt.xlabel("World size (ranks)"); plt.ylabel("Milliseconds per step (mean)")
+    plt.title("Pseudo-FL time breakdown (h2d + compute)"); plt.legend(fontsize=6); plt.tight_layout()
+    p = os.path.join(out_dir, "part3_step_breakdown_grouped.png"); plt.savefig(p, dpi=150); plt.close(fig)
+    outs.append(p)
     return outs
 
 

@@ -20,7 +20,7 @@ def main(argv=None):
     loc = os.path.join(d, "part1_locality_results.csv")
     if os.path.exists(loc):
         made += plots.plot_locality(loc, d)
-        plots.plot_all_results(d)
+        made += plots.plot_all_results_figures(d)
     made += plots.plot_part2(d)
     p3 = os.path.join(d, "part3_mpi_cuda_results.csv")
     if os.path.exists(p3):
