@@ -2581,9 +2581,11 @@ ECG_API int ecg_conv1d_nlc_wgrad_splits(int B, int Lin, int Cin, int Lout, int C
 // 128x128 shapes take the two-group LDS-DMA kernel at the split count that target implies; B = 0: assume it does.
 ECG_API int ecg_conv1d_nlc_wgrad_target_wgs(int Cout, int Kw, int Cin, int B, int Lin, int Lout) {
   if (wgrad_big(Cout, Cin)) return 512;
-  // 128x128 tiles: the two-group 8-wave kernel, one workgroup per CU (B=1024 ResNet1D-34: 3.43 ms/step at 256
-  // workgroups vs 3.51 at 512 and 3.81 at 768; profiles/r4/wgrad_g2_ab.txt) - when its 32-bit offsets hold;
-  // otherwise the 4-wave register-staged 128x128 kernel, which wants ~4 workgroups per CU (advisor r4)
+  // 128x128 tiles: the two-group 8-wave kernel, a little under one workgroup per CU - 224 (ECG_WGRAD_TARGET, read
+  // once): B=1024 ResNet1D-34 3.256-3.275 ms/step at 192-224 workgroups vs 3.30-3.35 at 256, 3.31 at 160-176 and
+  // 3.43-3.45 at 128 / 384 on three boxes (profiles/r6/wgrad_target_ab.txt; round 4: 256 beat 512 and 768,
+  // profiles/r4/wgrad_g2_ab.txt): the side lane's weight gradients leave CUs to the data-gradient chain - when its
+  // 32-bit offsets hold; otherwise the 4-wave register-staged 128x128 kernel, which wants ~4 workgroups per CU
   if (Cout % 128 == 0 && Cin % 128 == 0) {
     if (B <= 0 || Lout <= 0) return 256;
     const int tiles = ecg_conv1d_nlc_wgrad_tiles(Cout, Kw, Cin);
@@ -2591,7 +2593,13 @@ ECG_API int ecg_conv1d_nlc_wgrad_target_wgs(int Cout, int Kw, int Cin, int B, in
     long splits = (256 + tiles - 1) / tiles;
     splits = splits < 1 ? 1 : splits;
     const long cps = (chunks + splits - 1) / splits;
-    return wgrad_dma_ok(cps, Lin, Cin, Lout, Cout) ? 256 : 1024;
+    static int tgt = -1;
+    if (tgt < 0) {
+      const char* e = getenv("ECG_WGRAD_TARGET");
+      tgt = e ? atoi(e) : 224;
+      if (tgt <= 0) tgt = 224;
+    }
+    return wgrad_dma_ok(cps, Lin, Cin, Lout, Cout) ? tgt : 1024;
   }
   return 1024;
 }
