@@ -222,9 +222,11 @@ class ResNetStepEngine:
             chunks = (R + 63) // 64
             tiles = self.lib.ecg_conv1d_nlc_wgrad_tiles(Cout, K, Cin)
             target = self.lib.ecg_conv1d_nlc_wgrad_target_wgs(Cout, K, Cin, B, Lin or 0, Lout or 0)
-            # A/B knob: capping the splits shrinks the reduce (S x |dW|) but starves the wgrad kernel of workgroups
-            # (B=1024: cap 16 -> 5.86, cap 8 -> 7.66 ms/step vs 4.61 uncapped, profiles/r2/resnet_conv_ab.txt)
-            cap = 64
+            # cap (ECG_WGRAD_SPLIT_CAP): fewer splits shrink the reduce (S x |dW|) but starve the wgrad kernel of
+            # workgroups (round 2: cap 16 -> 5.86, cap 8 -> 7.66 ms/step vs 4.61 uncapped, profiles/r2/
+            # resnet_conv_ab.txt); round 6 at target 224: 96 -0.3 % vs 64 on two boxes, 24-48 slower
+            # (profiles/r6/wgrad_target_ab.txt)
+            cap = int(os.environ.get("ECG_WGRAD_SPLIT_CAP", "96"))
             return max(1, min(cap, 256, max(1, chunks // 8), max(1, target // tiles)))
 
         ws_need = 0
